@@ -1,0 +1,150 @@
+"""Synthetic read sets for the overlapInCore path (no network, no datasets here).
+
+A random genome is sampled into reads with substitution / insertion / deletion errors,
+random strand, optional 'N' bases and optional planted repeats.  The generator is
+deterministic in its seed.  Reads are returned the way gkStore hands them to
+overlapInCore (Process_Overlaps.C:118-126): one byte per base, upper case, concatenated,
+with 64-bit offsets and 32-bit lengths; read i gets gkStore ID first_iid + i.
+"""
+from __future__ import annotations
+
+import dataclasses
+import struct
+
+import numpy as np
+
+_ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+_COMP = np.zeros(256, dtype=np.uint8)
+for _a, _b in zip(b"ACGTN", b"TGCAN"):
+    _COMP[_a] = _b
+
+
+@dataclasses.dataclass
+class ReadSet:
+    bases: np.ndarray        # uint8, concatenated
+    offsets: np.ndarray      # uint64, start of each read in bases
+    lengths: np.ndarray      # uint32
+    quals: np.ndarray | None = None   # uint8 0..60, same layout as bases
+    first_iid: int = 1
+
+    @property
+    def nreads(self) -> int:
+        return int(self.lengths.shape[0])
+
+    def read(self, i: int) -> bytes:
+        o = int(self.offsets[i])
+        return self.bases[o:o + int(self.lengths[i])].tobytes()
+
+    def total_bases(self) -> int:
+        return int(self.lengths.sum(dtype=np.uint64))
+
+
+# Named profiles of BASELINE.json's configs.  "ont" is the headline workload.
+PROFILES = {
+    # configs[0]: 1k PacBio-like 3 kb reads at E. coli scale (4.6 Mbp genome).
+    "pacbio-ecoli": dict(n_reads=1000, read_len=3000, genome_len=4_600_000, error_rate=0.02),
+    # configs[1]/[2]: 50k ONT-like 10 kb reads; 20 Mbp genome -> 25x coverage.
+    "ont-50k": dict(n_reads=50_000, read_len=10_000, genome_len=20_000_000, error_rate=0.015),
+}
+
+
+def random_genome(rng: np.random.Generator, length: int, n_repeats: int = 0,
+                  repeat_len: int = 0) -> np.ndarray:
+    g = _ACGT[rng.integers(0, 4, size=length, dtype=np.int64)]
+    if n_repeats and repeat_len:
+        unit = _ACGT[rng.integers(0, 4, size=repeat_len, dtype=np.int64)]
+        for _ in range(n_repeats):
+            p = int(rng.integers(0, max(1, length - repeat_len)))
+            g[p:p + repeat_len] = unit
+    return g
+
+
+def _mutate(rng: np.random.Generator, seg: np.ndarray, out_len: int, error_rate: float,
+            sub_frac: float, ins_frac: float) -> np.ndarray:
+    n = seg.shape[0]
+    r = rng.random(n)
+    p_sub = error_rate * sub_frac
+    p_ins = error_rate * ins_frac
+    is_sub = r < p_sub
+    is_ins = (r >= p_sub) & (r < p_sub + p_ins)
+    is_del = (r >= p_sub + p_ins) & (r < error_rate)
+    out = seg.copy()
+    if is_sub.any():
+        shift = rng.integers(1, 4, size=int(is_sub.sum()))
+        idx = np.searchsorted(_ACGT, out[is_sub])
+        out[is_sub] = _ACGT[(idx + shift) % 4]
+    counts = np.ones(n, dtype=np.int64)
+    counts[is_del] = 0
+    counts[is_ins] = 2
+    rep = np.repeat(out, counts)
+    # the first copy of each inserted position becomes a random base
+    ins_pos = np.cumsum(counts)[is_ins] - 2
+    if ins_pos.size:
+        rep[ins_pos] = _ACGT[rng.integers(0, 4, size=ins_pos.size)]
+    return rep[:out_len]
+
+
+def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
+                seed: int = 1, sub_frac: float = 0.4, ins_frac: float = 0.3,
+                len_jitter: float = 0.0, n_rate: float = 0.0, n_repeats: int = 0,
+                repeat_len: int = 0, with_quals: bool = False,
+                genome: np.ndarray | None = None) -> ReadSet:
+    """Sample `n_reads` reads of about `read_len` bases from a random genome."""
+    rng = np.random.default_rng(seed)
+    if genome is None:
+        genome = random_genome(rng, genome_len, n_repeats, repeat_len)
+    genome_len = genome.shape[0]
+    lengths = np.empty(n_reads, dtype=np.uint32)
+    chunks = []
+    for i in range(n_reads):
+        L = read_len
+        if len_jitter > 0:
+            L = max(64, int(read_len * (1.0 + len_jitter * (2.0 * rng.random() - 1.0))))
+        L = min(L, genome_len)
+        span = min(genome_len, int(L * (1.0 + 2.0 * error_rate)) + 32)
+        start = int(rng.integers(0, genome_len - span + 1))
+        seg = genome[start:start + span]
+        rd = _mutate(rng, seg, L, error_rate, sub_frac, ins_frac)
+        if rng.random() < 0.5:
+            rd = _COMP[rd[::-1]]
+        if n_rate > 0:
+            m = rng.random(rd.shape[0]) < n_rate
+            rd = rd.copy()
+            rd[m] = ord("N")
+        chunks.append(rd)
+        lengths[i] = rd.shape[0]
+    bases = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
+    offsets = np.zeros(n_reads, dtype=np.uint64)
+    if n_reads > 1:
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    quals = None
+    if with_quals:
+        quals = rng.integers(2, 41, size=bases.shape[0]).astype(np.uint8)
+    return ReadSet(bases=bases, offsets=offsets, lengths=lengths, quals=quals)
+
+
+def profile(name: str, seed: int = 1, **over) -> ReadSet:
+    kw = dict(PROFILES[name])
+    kw.update(over)
+    return synth_reads(seed=seed, **kw)
+
+
+def scaled_profile(name: str, n_reads: int, seed: int = 1) -> ReadSet:
+    """The same read length / error / coverage as `name`, with fewer reads (the genome
+    shrinks with the read count, so per-read work stays the same)."""
+    kw = dict(PROFILES[name])
+    scale = n_reads / kw["n_reads"]
+    kw["genome_len"] = max(kw["read_len"] * 4, int(kw["genome_len"] * scale))
+    kw["n_reads"] = n_reads
+    return synth_reads(seed=seed, **kw)
+
+
+def write_reads_file(path: str, rs: ReadSet) -> None:
+    """The reads file oracle/ref_harness.cpp reads ("OICR" v1)."""
+    with open(path, "wb") as f:
+        f.write(b"OICR")
+        f.write(struct.pack("<III", 1, rs.nreads, 1 if rs.quals is not None else 0))
+        f.write(rs.lengths.astype("<u4").tobytes())
+        f.write(rs.bases.tobytes())
+        if rs.quals is not None:
+            f.write(rs.quals.tobytes())

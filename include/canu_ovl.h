@@ -1,0 +1,161 @@
+/*
+ * canu_ovl.h -- C-ABI of the MI355X-native overlapInCore seed-and-extend path.
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no torch / HIP types.
+ * It replaces the compute inside canu's overlapInCore driver:
+ *
+ *   reference                                               replaced by
+ *   -----------------------------------------------------   -------------------------------
+ *   src/overlapInCore/overlapInCore.C:190 OverlapDriver()    ovl_ctx_* lifecycle below
+ *   src/overlapInCore/overlapInCore.C:306 main() (options)   ovl_params + ovl_params_init()
+ *   src/overlapInCore/overlapInCore.C:487-529 (HSF/Bit_Eq.)  done inside ovl_ctx_create()
+ *   src/overlapInCore/overlapInCore-Build_Hash_Index.C:443   ovl_build_hash_index()
+ *     Build_Hash_Index(gkStore*, bgnID, endID)
+ *   src/overlapInCore/overlapInCore-Build_Hash_Index.C:235   ovl_set_skip_kmers()
+ *     Mark_Skip_Kmers() (-k <frequentMers.fasta>)
+ *   src/overlapInCore/overlapInCore-Process_Overlaps.C:78    ovl_find_overlaps()
+ *     Process_Overlaps() -> Find_Overlaps(FORWARD/REVERSE)
+ *     -> Process_String_Olaps -> Process_Matches
+ *     -> prefixEditDistance::Extend_Alignment
+ *     -> Output_Overlap / Output_Partial_Overlap
+ *   src/stores/ovStoreFile.C:198 ovFile::writeOverlap()      ovl_fetch_overlaps() returns the
+ *                                                            records; the caller keeps writing
+ *                                                            them with its own ovFile.
+ *
+ * Records are returned in ovOverlap's in-memory layout for AS_MAX_READLEN_BITS == 21
+ * (src/stores/ovOverlap.H:93-116): a_iid, b_iid, then the two 64-bit bitfield words
+ * (ahg5:21 ahg3:21 evalue:12 flipped:1 forOBT:1 forDUP:1 forUTG:1 extra1:6 |
+ *  bhg5:21 bhg3:21 span:21 extra2:1).
+ *
+ * Reads are handed over as the gkStore hands them to overlapInCore
+ * (gkStore::gkStore_loadReadData -> char* sequence, char* qualities): bases in any case
+ * (the library lowercases, as Process_Overlaps.C:122 does), qualities as small integers
+ * (already minus '!'), or NULL when the window filter is not used.
+ *
+ * All functions return 0 on success and a negative ovl_status on error; ovl_last_error()
+ * gives a message.  There is no CPU fallback: without a usable gfx950 device
+ * ovl_ctx_create() fails with OVL_ERR_NO_DEVICE.
+ */
+#ifndef CANU_OVL_H
+#define CANU_OVL_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OVL_ABI_VERSION 1
+
+typedef enum {
+  OVL_OK               =  0,
+  OVL_ERR_NO_DEVICE    = -1,   /* no HIP device / not gfx950                          */
+  OVL_ERR_BAD_PARAM    = -2,   /* parameter outside what the reference accepts        */
+  OVL_ERR_UNSUPPORTED  = -3,   /* reference option this build does not implement      */
+  OVL_ERR_BAD_INPUT    = -4,   /* read data the GPU path cannot represent             */
+  OVL_ERR_HIP          = -5,   /* a HIP runtime call failed                           */
+  OVL_ERR_OOM          = -6,   /* device or host allocation failed                    */
+  OVL_ERR_STATE        = -7    /* call order violated (e.g. find before build)        */
+} ovl_status;
+
+/* One overlap, ovOverlap (src/stores/ovOverlap.H:285) without the gkStore pointer. */
+typedef struct {
+  uint32_t a_iid;
+  uint32_t b_iid;
+  uint64_t dat[2];
+} ovl_record;
+
+/* overlapInCore options (oicParameters, src/overlapInCore/overlapInCore.H:418). */
+typedef struct {
+  uint32_t kmer_len;              /* -k <n>              G.Kmer_Len                      */
+  double   max_erate;             /* --maxerate          G.maxErate (host mirror parses  */
+                                  /*                     with strtof, as main() does)    */
+  int32_t  min_olap_len;          /* --minlength         G.Min_Olap_Len                  */
+  int32_t  partial;               /* -G                  G.Doing_Partial_Overlaps        */
+  int32_t  unique_olap_per_pair;  /* -u / -m             G.Unique_Olap_Per_Pair          */
+  int32_t  use_window_filter;     /* -w                  G.Use_Window_Filter             */
+  int32_t  use_hopeless_check;    /* -z clears it        G.Use_Hopeless_Check            */
+  uint64_t frag_olap_limit;       /* -l                  G.Frag_Olap_Limit (UINT64_MAX)  */
+  uint64_t filter_by_kmer_count;  /* --minkmers          G.Filter_By_Kmer_Count          */
+} ovl_params;
+
+/* Defaults of oicParameters::initialize() (overlapInCore.H:425). kmer_len is left 0, as
+ * there; ovl_ctx_create() rejects 0 like main() does (overlapInCore.C:426). */
+void        ovl_params_init(ovl_params *p);
+
+/* The fix-ups main() applies after option parsing (overlapInCore.C:416-421):
+ * maxErate > 0.06 turns the window filter and the hopeless check off. */
+void        ovl_params_finalize(ovl_params *p);
+
+typedef struct ovl_ctx ovl_ctx;
+
+/* Create a context on HIP device `device` (ordinal; one process per GPU). */
+int         ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out);
+void        ovl_ctx_destroy(ovl_ctx *ctx);
+const char *ovl_last_error(void);
+int         ovl_abi_version(void);
+
+/* Load reads first_iid .. first_iid+nreads-1 (gkStore IDs, 1-based in canu).
+ *   bases    concatenated sequence bytes, read i at bases[offsets[i]] for lengths[i] bytes
+ *   quals    same layout, or NULL (required only when use_window_filter is set)
+ * The data are copied to device memory (2-bit packed + exception masks) once; every
+ * later call works on the resident copy. */
+int         ovl_load_reads(ovl_ctx *ctx, uint32_t first_iid, uint32_t nreads,
+                           const uint8_t *bases, const uint64_t *offsets,
+                           const uint32_t *lengths, const uint8_t *quals);
+
+/* The same, but the caller's buffers are already device pointers (HBM resident). */
+int         ovl_load_reads_device(ovl_ctx *ctx, uint32_t first_iid, uint32_t nreads,
+                                  const uint8_t *d_bases, const uint64_t *d_offsets,
+                                  const uint32_t *h_lengths, const uint8_t *d_quals);
+
+/* Frequent k-mers that must not seed overlaps (-k <fasta>, Mark_Skip_Kmers).
+ * kmers: n_kmers * kmer_len bytes of ACGT text, back to back. Both orientations are
+ * screened, as the reference does. Must be called before ovl_build_hash_index(). */
+int         ovl_set_skip_kmers(ovl_ctx *ctx, const char *kmers, uint64_t n_kmers);
+
+/* Build the k-mer index over hash reads bgn_iid..end_iid (inclusive, like -h). */
+int         ovl_build_hash_index(ovl_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);
+
+/* Search ref reads bgn_iid..end_iid (inclusive, like -r) against the index, both
+ * orientations, and keep the resulting records on the device. Returns the number of
+ * records found in *n_out. Work is done on the context's stream; the call returns
+ * after the stream is synchronized. */
+int         ovl_find_overlaps(ovl_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid,
+                              uint64_t *n_out);
+
+/* Copy the records of the last ovl_find_overlaps() to host memory, sorted by
+ * ovOverlap::operator< (a_iid, b_iid, dat[0], dat[1]).  max_records bounds the copy. */
+int         ovl_fetch_overlaps(ovl_ctx *ctx, ovl_record *out, uint64_t max_records,
+                               uint64_t *n_copied);
+
+/* Statistics of the last find (the counters overlapInCore prints with -s). */
+typedef struct {
+  uint64_t kmer_hits_without_olap;
+  uint64_t kmer_hits_with_olap;
+  uint64_t kmer_hits_skipped;
+  uint64_t multi_overlaps;
+  uint64_t total_overlaps;
+  uint64_t contained_overlaps;
+  uint64_t dovetail_overlaps;
+  uint64_t seed_hits;              /* kmer hits (Add_Ref calls)                        */
+  uint64_t pairs;                  /* (query, orientation, target) pairs with hits     */
+  double   ms_index;               /* device time of the index build                   */
+  double   ms_seed;                /* device time of seed lookup + chaining            */
+  double   ms_extend;              /* device time of extension + output                */
+  double   ms_probe_kernel;        /* device time of the hash-probe kernel alone       */
+  uint64_t probe_bytes;            /* algorithmic bytes of the hash-probe kernel       */
+} ovl_stats;
+
+int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);
+
+/* HIP stream the context runs on (as void*, a hipStream_t), for callers that time or
+ * order work around it. */
+void       *ovl_ctx_stream(ovl_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,1292 @@
+/*
+ * oic_oracle.c -- CPU restatement of canu's overlapInCore seed-and-extend path.
+ *
+ *   TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP path in
+ *   canu_amd/csrc.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ *   may load it, and only to check or time against.  It is never linked into, called by,
+ *   or used as a fallback for the product library.
+ *
+ * It restates, in plain C, the algorithm of (reference = /root/reference/src):
+ *   overlapInCore/overlapInCore.C               option fix-ups, Bit_Equivalent (487-529)
+ *   overlapInCore/overlapInCore-Build_Hash_Index.C   k-mer index, Mark_Skip_Kmers
+ *   overlapInCore/overlapInCore-Find_Overlaps.C      Find_Overlaps, Add_Ref, Add_Match
+ *   overlapInCore/overlapInCore-Process_String_Overlaps.C
+ *                                               Process_String_Olaps, Process_Matches,
+ *                                               Add_Overlap, Combine_Into_One_Olap, ...
+ *   overlapInCore/liboverlap/prefixEditDistance*.C   Extend_Alignment, forward, reverse
+ *   overlapInCore/liboverlap/Binomial_Bound.C        Edit_Match_Limit table
+ *   overlapInCore/overlapInCore-Output.C             Output_Overlap / Output_Partial_Overlap
+ *   stores/ovOverlap.H                               record bit layout (21-bit reads)
+ *
+ * The k-mer index is a sorted array instead of the reference's open-addressing bucket
+ * table.  Both answer "every occurrence of this exact ACGT k-mer in the hash reads, in
+ * chain order"; the chain order of Hash_Insert (Build_Hash_Index.C:320-323, new entries
+ * are pushed on the front) is descending (read, offset), which the sort reproduces.
+ *
+ * Pinned by: oracle/ref_harness.cpp (the reference sources themselves, compiled by
+ * oracle/Makefile into oracle/_ref/oic_ref) -- tests/test_oracle_vs_reference.py and the
+ * golden fixtures under tests/golden/ compare this restatement record-for-record.
+ */
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <stdio.h>
+#include <ctype.h>
+#include <assert.h>
+
+#define AS_MAX_READLEN_BITS   21
+#define AS_MAX_READLEN        ((1u << AS_MAX_READLEN_BITS) - 1)
+#define AS_MAX_EVALUE         4095
+
+#define HOPELESS_MATCH        90                   /* overlapInCore.H:122 */
+#define MAX_DISTINCT_OLAPS    3                    /* overlapInCore.H:151 */
+#define MIN_INTERSECTION      10                   /* overlapInCore.H:171 */
+#define SHIFT_SLACK           1                    /* overlapInCore.H:197 */
+#define QUALITY_CUTOFF        20                   /* overlapInCore.H:190 */
+#define BAD_WINDOW_LEN        50
+#define BAD_WINDOW_VALUE      (8 * QUALITY_CUTOFF)
+#define STRING_OLAP_SHIFT     8
+#define STRING_OLAP_MODULUS   (1 << STRING_OLAP_SHIFT)
+#define STRING_OLAP_MASK      (STRING_OLAP_MODULUS - 1)
+
+typedef struct {
+  uint32_t kmer_len;
+  double   max_erate;
+  int32_t  min_olap_len;
+  int32_t  partial;
+  int32_t  unique_olap_per_pair;
+  int32_t  use_window_filter;
+  int32_t  use_hopeless_check;
+  uint64_t frag_olap_limit;
+  uint64_t filter_by_kmer_count;
+} oracle_params;                                    /* same layout as ovl_params */
+
+typedef struct {
+  uint32_t a_iid, b_iid;
+  uint64_t dat[2];
+} oracle_record;
+
+typedef struct {
+  uint64_t kmer_hits_without_olap, kmer_hits_with_olap, kmer_hits_skipped;
+  uint64_t multi_overlaps, total_overlaps, contained_overlaps, dovetail_overlaps;
+  uint64_t seed_hits, pairs;
+} oracle_stats;
+
+/* ------------------------------------------------------------------------------------ */
+/* Tables that depend only on maxErate: prefixEditDistance.C:40-116, Binomial_Bound.C    */
+
+typedef struct {
+  double   max_erate;
+  int      partial;
+  int32_t  max_errors;               /* MAX_ERRORS = 1 + ceil(maxErate * AS_MAX_READLEN) */
+  int32_t *error_bound;              /* [AS_MAX_READLEN+1], ceil(i*maxErate)               */
+  int32_t *match_limit;              /* Edit_Match_Limit[MAX_ERRORS+1]                     */
+  double   branch_match_value;
+  double   min_branch_tail_slope;
+  int32_t  min_branch_end_dist;
+} ped_tables;
+
+/* Binomial_Bound.C:47 -- smallest n >= start with P[>= e errors in n trials] > 1e-4 */
+static int binomial_bound(int e, double p, int start) {
+  const double bound = 1e-4, thold = 3.62;
+  double q = 1.0 - p;
+  if (start < e) start = e;
+  for (int n = start; n < (int)AS_MAX_READLEN; n++) {
+    if (n <= 35) {
+      double sum = 0.0, p_pow = 1.0, q_pow = pow(q, n);
+      int bin = 1, ct = 0;
+      for (int k = 0; k < e && 1.0 - sum > bound; k++) {
+        double x = bin * p_pow * q_pow;
+        sum += x;
+        bin *= n - ct;
+        bin /= ++ct;
+        p_pow *= p;
+        q_pow /= q;
+      }
+      if (1.0 - sum > bound) return n;
+    } else {
+      double z = (e - 0.5 - n * p) / sqrt(n * p * q);
+      if (z <= thold) return n;
+      double sum = 0.0, mu_pow = 1.0, fact = 1.0, pc = exp(-n * p);
+      for (int k = 0; k < e; k++) {
+        sum += mu_pow * pc / fact;
+        mu_pow *= n * p;
+        fact *= k + 1;
+      }
+      if (1.0 - sum > bound) return n;
+    }
+  }
+  return AS_MAX_READLEN;
+}
+
+/* Binomial_Bound.C:121 Initialize_Match_Limit, AS_MAX_READLEN_BITS == 21 branch */
+static void init_match_limit(int32_t *ml, double erate, int32_t max_errors) {
+  int32_t e = 0, s = 1, l = max_errors < 2000 ? max_errors : 2000;
+  while (e <= 1) ml[e++] = 0;                      /* ERRORS_FOR_FREE = 1 */
+  while (e < l) {
+    s = binomial_bound(e - 1, erate, s);
+    ml[e] = s - 1;
+    e++;
+  }
+  double sl = 0.982064188397525 / erate + 0.067835741959926;
+  double vl = ml[e - 1] + sl;
+  while (e < max_errors) {
+    ml[e] = (int32_t)ceil(vl);
+    vl += sl;
+    e++;
+  }
+}
+
+static void ped_tables_init(ped_tables *t, double erate, int partial) {
+  t->max_erate  = erate;
+  t->partial    = partial;
+  t->max_errors = 1 + (int32_t)ceil(erate * AS_MAX_READLEN);
+  t->min_branch_end_dist   = 20;
+  t->min_branch_tail_slope = (erate > 0.06) ? 1.0 : 0.20;
+  t->error_bound = (int32_t *)malloc(sizeof(int32_t) * (AS_MAX_READLEN + 1));
+  for (uint32_t i = 0; i <= AS_MAX_READLEN; i++)
+    t->error_bound[i] = (int32_t)ceil(i * erate);
+  t->match_limit = (int32_t *)calloc(t->max_errors + 1, sizeof(int32_t));
+  init_match_limit(t->match_limit, erate, t->max_errors);
+  t->branch_match_value = erate / (1 + erate);
+}
+
+static void ped_tables_free(ped_tables *t) {
+  free(t->error_bound);
+  free(t->match_limit);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Greedy prefix edit distance: prefixEditDistance-forward.C / -reverse.C / -extend.C    */
+
+typedef struct {
+  const ped_tables *t;
+  int32_t  rows;                     /* rows allocated                                  */
+  int32_t *space;                    /* triangle: row e covers diagonals [-e-2, e+2]     */
+  int32_t  left_delta_len, right_delta_len;
+  int32_t *left_delta, *right_delta, *delta_stack;
+  int32_t  delta_cap;
+} ped;
+
+static inline int32_t *ped_row(ped *p, int32_t e) {
+  return p->space + ((int64_t)e * e + 5 * (int64_t)e + 2);  /* base of row e = e^2+5e+2 */
+}
+
+static void ped_reserve(ped *p, int32_t e_max) {
+  if (e_max + 1 <= p->rows) return;
+  int32_t rows = e_max + 1;
+  int64_t cells = (int64_t)rows * rows + 4 * (int64_t)rows;
+  p->space = (int32_t *)realloc(p->space, sizeof(int32_t) * cells);
+  p->rows  = rows;
+  if (rows + 8 > p->delta_cap) {
+    p->delta_cap   = rows + 8;
+    p->left_delta  = (int32_t *)realloc(p->left_delta,  sizeof(int32_t) * 2 * p->delta_cap);
+    p->right_delta = (int32_t *)realloc(p->right_delta, sizeof(int32_t) * p->delta_cap);
+    p->delta_stack = (int32_t *)realloc(p->delta_stack, sizeof(int32_t) * p->delta_cap);
+  }
+}
+
+static inline int sign_of(int a) { return (a > 0) - (a < 0); }
+
+/* forward.C:51 Set_Right_Delta */
+static void set_right_delta(ped *p, int32_t e, int32_t d) {
+  int32_t last = ped_row(p, e)[d];
+  int32_t n = 0;
+  for (int32_t k = e; k > 0; k--) {
+    int32_t *prev = ped_row(p, k - 1);
+    int32_t from = d, mx = 1 + prev[d], j;
+    if ((j = prev[d - 1]) > mx)     { from = d - 1; mx = j; }
+    if ((j = 1 + prev[d + 1]) > mx) { from = d + 1; mx = j; }
+    if (from == d - 1) {
+      p->delta_stack[n++] = mx - last - 1;
+      d--;
+      last = prev[from];
+    } else if (from == d + 1) {
+      p->delta_stack[n++] = last - (mx - 1);
+      d++;
+      last = prev[from];
+    }
+  }
+  p->delta_stack[n++] = last + 1;
+  int32_t k = 0;
+  for (int32_t i = n - 1; i > 0; i--)
+    p->right_delta[k++] = abs(p->delta_stack[i]) * sign_of(p->delta_stack[i - 1]);
+  p->right_delta_len = n - 1;
+}
+
+/* reverse.C:49 Set_Left_Delta */
+static void set_left_delta(ped *p, int32_t e, int32_t d, int32_t *leftover, int32_t *t_end,
+                           int32_t t_len) {
+  int32_t last = ped_row(p, e)[d];
+  p->left_delta_len = 0;
+  for (int32_t k = e; k > 0; k--) {
+    int32_t *prev = ped_row(p, k - 1);
+    int32_t from = d, mx = 1 + prev[d], j;
+    if ((j = prev[d - 1]) > mx)     { from = d - 1; mx = j; }
+    if ((j = 1 + prev[d + 1]) > mx) { from = d + 1; mx = j; }
+    if (from == d - 1) {
+      p->left_delta[p->left_delta_len++] = mx - last - 1;
+      d--;
+      last = prev[from];
+    } else if (from == d + 1) {
+      p->left_delta[p->left_delta_len++] = last - (mx - 1);
+      d++;
+      last = prev[from];
+    }
+  }
+  *leftover = last;
+  if (p->left_delta_len > 1 && p->left_delta[0] == 1 && *t_end + t_len > 0) {
+    if (p->left_delta[1] > 0) p->left_delta[0] = p->left_delta[1] + 1;
+    else                      p->left_delta[0] = p->left_delta[1] - 1;
+    for (int32_t i = 2; i < p->left_delta_len; i++)
+      p->left_delta[i - 1] = p->left_delta[i];
+    p->left_delta_len--;
+    (*t_end)--;
+    if (p->left_delta_len == 0) (*leftover)++;
+  }
+}
+
+static inline int bases_match(char a, char b) {
+  return a == b || a == 'n' || b == 'n';
+}
+
+/* The shared body of forward() and reverse(): dir = +1 walks A[Row], T[Row+d];
+ * dir = -1 walks A[-Row], T[-Row-d].  Returns errors; sets a_end/t_end (unsigned
+ * extents, negated by the caller for reverse), match_to_end, and the best (e,d) used
+ * for the traceback in *tb_e, *tb_d. */
+static int32_t ped_extend(ped *p, const char *A, int32_t m, const char *T, int32_t n,
+                          int32_t error_limit, int dir, int32_t *a_len, int32_t *t_len,
+                          int *match_to_end, int32_t *tb_e, int32_t *tb_d) {
+  const ped_tables *t = p->t;
+  double  score, max_score = 0.0;
+  int32_t max_score_len = 0, max_score_best_d = 0, max_score_best_e = 0;
+  int32_t best_d = 0, best_e = 0, longest = 0, row, j;
+  assert(m <= n);
+
+  for (row = 0; row < m && bases_match(A[dir * row], T[dir * row]); row++)
+    ;
+  ped_reserve(p, error_limit);
+  ped_row(p, 0)[0] = row;
+
+  if (row == m) {
+    *a_len = *t_len = m;
+    *match_to_end = 1;
+    *tb_e = -1; *tb_d = 0;                      /* exact match: no traceback */
+    return 0;
+  }
+
+  int32_t left = 0, right = 0, e;
+  for (e = 1; e <= error_limit; e++) {
+    int32_t *prev = ped_row(p, e - 1);
+    int32_t *cur  = ped_row(p, e);
+    left  = (left - 1 > -e) ? left - 1 : -e;
+    right = (right + 1 < e) ? right + 1 : e;
+    prev[left] = -2;  prev[left - 1] = -2;
+    prev[right] = -2; prev[right + 1] = -2;
+
+    for (int32_t d = left; d <= right; d++) {
+      row = 1 + prev[d];
+      if ((j = prev[d - 1]) > row) row = j;
+      if ((j = 1 + prev[d + 1]) > row) row = j;
+      while (row < m && row + d < n && bases_match(A[dir * row], T[dir * (row + d)]))
+        row++;
+      cur[d] = row;
+
+      if (row == m || row + d == n) {
+        score = row * t->branch_match_value - e;
+        int32_t tail_len = row - max_score_len;
+        int abort_here = 0;
+        double slope = (double)(max_score - score) / tail_len;
+        if (t->partial && score < max_score)
+          abort_here = 1;
+        if (e > t->min_branch_end_dist / 2 && tail_len >= t->min_branch_end_dist &&
+            slope >= t->min_branch_tail_slope)
+          abort_here = 1;
+        if (abort_here) {
+          *a_len = max_score_len;
+          *t_len = max_score_len + max_score_best_d;
+          *match_to_end = 0;
+          *tb_e = max_score_best_e; *tb_d = max_score_best_d;
+          return max_score_best_e;
+        }
+        /* forward.C:212 -- force the last error to be a mismatch (forward only) */
+        if (dir > 0 && row == m && 1 + prev[d + 1] == cur[d] && d < right) {
+          d++;
+          cur[d] = cur[d - 1];
+        }
+        *a_len = row;
+        *t_len = row + d;
+        *match_to_end = 1;
+        *tb_e = e; *tb_d = d;
+        return e;
+      }
+    }
+
+    while (left <= right && left < 0 && cur[left] < t->match_limit[e]) left++;
+    if (left >= 0)
+      while (left <= right && cur[left] + left < t->match_limit[e]) left++;
+    if (left > right) break;
+    while (right > 0 && cur[right] + right < t->match_limit[e]) right--;
+    if (right <= 0)
+      while (cur[right] < t->match_limit[e]) right--;
+    assert(left <= right);
+
+    for (int32_t d = left; d <= right; d++)
+      if (cur[d] > longest) { best_d = d; best_e = e; longest = cur[d]; }
+
+    score = longest * t->branch_match_value - e;
+    if (score > max_score) {
+      max_score = score;
+      max_score_len = longest;
+      max_score_best_d = best_d;
+      max_score_best_e = best_e;
+    }
+  }
+
+  *a_len = max_score_len;
+  *t_len = max_score_len + max_score_best_d;
+  *match_to_end = 0;
+  *tb_e = max_score_best_e; *tb_d = max_score_best_d;
+  return max_score_best_e;
+}
+
+/* forward.C:103 */
+static int32_t ped_forward(ped *p, const char *A, int32_t m, const char *T, int32_t n,
+                           int32_t lim, int32_t *a_end, int32_t *t_end, int *mte) {
+  int32_t e_tb, d_tb;
+  p->right_delta_len = 0;
+  int32_t err = ped_extend(p, A, m, T, n, lim, +1, a_end, t_end, mte, &e_tb, &d_tb);
+  if (e_tb >= 0) set_right_delta(p, e_tb, d_tb);
+  return err;
+}
+
+/* reverse.C:119 */
+static int32_t ped_reverse(ped *p, const char *A, int32_t m, const char *T, int32_t n,
+                           int32_t lim, int32_t *a_end, int32_t *t_end, int32_t *leftover,
+                           int *mte) {
+  int32_t e_tb, d_tb, al, tl;
+  p->left_delta_len = 0;
+  int32_t err = ped_extend(p, A, m, T, n, lim, -1, &al, &tl, mte, &e_tb, &d_tb);
+  *a_end = -al;
+  *t_end = -tl;
+  if (e_tb < 0) {
+    *leftover = m;                               /* exact match */
+  } else {
+    set_left_delta(p, e_tb, d_tb, leftover, t_end, n);
+  }
+  return err;
+}
+
+typedef struct { int32_t Offset, Len, Start, Next; } match_node;
+
+enum { OLAP_NONE = 0, LEFT_BRANCH_PT, RIGHT_BRANCH_PT, DOVETAIL };
+
+/* prefixEditDistance-extend.C:86 Extend_Alignment */
+static int extend_alignment(ped *p, const match_node *M, const char *S, int32_t S_Len,
+                            const char *T, int32_t T_Len, int32_t *S_Lo, int32_t *S_Hi,
+                            int32_t *T_Lo, int32_t *T_Hi, int32_t *Errors) {
+  const ped_tables *t = p->t;
+  int32_t right_errors = 0, left_errors = 0, leftover = 0;
+  int rmte = 1, lmte = 1;
+  int32_t S_Left_Begin = M->Start - 1, S_Right_Begin = M->Start + M->Len;
+  int32_t S_Right_Len = S_Len - S_Right_Begin;
+  int32_t T_Left_Begin = M->Offset - 1, T_Right_Begin = M->Offset + M->Len;
+  int32_t T_Right_Len = T_Len - T_Right_Begin;
+  int32_t total = (M->Start < M->Offset ? M->Start : M->Offset) + M->Len +
+                  (S_Right_Len < T_Right_Len ? S_Right_Len : T_Right_Len);
+  int32_t error_limit = t->error_bound[total];
+
+  p->left_delta_len = 0;
+  p->right_delta_len = 0;
+
+  if (S_Right_Len == 0 || T_Right_Len == 0) {
+    *S_Hi = 0; *T_Hi = 0; rmte = 1;
+  } else if (S_Right_Len <= T_Right_Len) {
+    right_errors = ped_forward(p, S + S_Right_Begin, S_Right_Len, T + T_Right_Begin,
+                               T_Right_Len, error_limit, S_Hi, T_Hi, &rmte);
+    for (int32_t i = 0; i < p->right_delta_len; i++) p->right_delta[i] *= -1;
+  } else {
+    right_errors = ped_forward(p, T + T_Right_Begin, T_Right_Len, S + S_Right_Begin,
+                               S_Right_Len, error_limit, T_Hi, S_Hi, &rmte);
+  }
+  *S_Hi += S_Right_Begin - 1;
+  *T_Hi += T_Right_Begin - 1;
+
+  if (S_Left_Begin < 0 || T_Left_Begin < 0) {
+    *S_Lo = 0; *T_Lo = 0; lmte = 1;
+  } else if (S_Right_Begin <= T_Right_Begin) {
+    left_errors = ped_reverse(p, S + S_Left_Begin, S_Left_Begin + 1, T + T_Left_Begin,
+                              T_Left_Begin + 1, error_limit - right_errors, S_Lo, T_Lo,
+                              &leftover, &lmte);
+  } else {
+    left_errors = ped_reverse(p, T + T_Left_Begin, T_Left_Begin + 1, S + S_Left_Begin,
+                              S_Left_Begin + 1, error_limit - right_errors, T_Lo, S_Lo,
+                              &leftover, &lmte);
+    for (int32_t i = 0; i < p->left_delta_len; i++) p->left_delta[i] *= -1;
+  }
+  *S_Lo += S_Left_Begin + 1;
+  *T_Lo += T_Left_Begin + 1;
+
+  *Errors = left_errors + right_errors;
+  assert(*Errors <= error_limit);
+
+  int kind = (rmte == 0) ? ((lmte == 0) ? OLAP_NONE : RIGHT_BRANCH_PT)
+                         : ((lmte == 0) ? LEFT_BRANCH_PT : DOVETAIL);
+
+  if (p->right_delta_len > 0) {
+    if (p->right_delta[0] > 0)
+      p->left_delta[p->left_delta_len++] = -(p->right_delta[0] + leftover + M->Len);
+    else
+      p->left_delta[p->left_delta_len++] = -(p->right_delta[0] - leftover - M->Len);
+  }
+  for (int32_t i = 1; i < p->right_delta_len; i++)
+    p->left_delta[p->left_delta_len++] = -p->right_delta[i];
+  p->right_delta_len = 0;
+  return kind;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Reads and the k-mer index                                                             */
+
+typedef struct {
+  uint32_t first_iid, nreads;
+  char   **seq;                      /* lowercased, NUL terminated                       */
+  char   **qlt;                      /* may hold NULL entries                            */
+  uint32_t *len;
+} read_set;
+
+typedef struct {
+  uint64_t key;                      /* 2 bits per base, first base in the low bits      */
+  uint32_t str;                      /* hash string index (iid - hash_bgn)               */
+  uint32_t off;
+} kmer_occ;
+
+typedef struct {
+  uint32_t   k;
+  uint32_t   hash_bgn;               /* Hash_String_Num_Offset                           */
+  uint32_t   n_str;
+  const char **seq;                  /* hash strings (NULL if not loaded)                */
+  const char **qlt;
+  uint32_t  *len;                    /* String_Info.length                               */
+  uint8_t   *lscreen, *rscreen;      /* String_Info.l/rfrag_end_screened                 */
+  kmer_occ  *occ;                    /* sorted by key, then (str,off) descending         */
+  uint64_t   n_occ;
+  uint64_t  *skip;                   /* sorted skip keys (both strands)                  */
+  uint64_t   n_skip;
+  int        use_hopeless;
+} kmer_index;
+
+static const int8_t bit_eq[256] = {
+  ['a'] = 0, ['c'] = 1, ['g'] = 2, ['t'] = 3, ['A'] = 0, ['C'] = 1, ['G'] = 2, ['T'] = 3 };
+
+static inline int is_acgt(char c) { return c == 'a' || c == 'c' || c == 'g' || c == 't'; }
+
+static int occ_cmp(const void *x, const void *y) {
+  const kmer_occ *a = (const kmer_occ *)x, *b = (const kmer_occ *)y;
+  if (a->key != b->key) return a->key < b->key ? -1 : 1;
+  if (a->str != b->str) return a->str > b->str ? -1 : 1;   /* chain order: newest first */
+  if (a->off != b->off) return a->off > b->off ? -1 : 1;
+  return 0;
+}
+
+static int u64_cmp(const void *x, const void *y) {
+  uint64_t a = *(const uint64_t *)x, b = *(const uint64_t *)y;
+  return a < b ? -1 : (a > b);
+}
+
+static uint64_t kmer_key(const char *s, uint32_t k, int *ok) {
+  uint64_t key = 0;
+  *ok = 1;
+  for (uint32_t j = 0; j < k; j++) {
+    if (!is_acgt(s[j])) *ok = 0;
+    key |= (uint64_t)bit_eq[(uint8_t)s[j]] << (2 * j);
+  }
+  return key;
+}
+
+/* AS_UTL_reverseComplement.C:39 -- only acgtACGT have complements; all else becomes 0 */
+static char comp_of(char c) {
+  switch (c) {
+    case 'a': return 't'; case 'c': return 'g'; case 'g': return 'c'; case 't': return 'a';
+    case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
+    default:  return 0;
+  }
+}
+
+static int skip_contains(const kmer_index *ix, uint64_t key) {
+  if (ix->n_skip == 0) return 0;
+  return bsearch(&key, ix->skip, ix->n_skip, sizeof(uint64_t), u64_cmp) != NULL;
+}
+
+/* Build_Hash_Index.C:443 + Put_String_In_Hash (:360) + Mark_Skip_Kmers (:235) */
+static void index_build(kmer_index *ix, const read_set *rs, const oracle_params *P,
+                        uint32_t bgn, uint32_t end, const char *skip_txt, uint64_t n_skip) {
+  memset(ix, 0, sizeof(*ix));
+  ix->k = P->kmer_len;
+  ix->hash_bgn = bgn;
+  ix->use_hopeless = P->use_hopeless_check;
+  if (end < bgn) return;
+  ix->n_str = end - bgn + 1;
+  ix->seq = (const char **)calloc(ix->n_str, sizeof(char *));
+  ix->qlt = (const char **)calloc(ix->n_str, sizeof(char *));
+  ix->len = (uint32_t *)calloc(ix->n_str, sizeof(uint32_t));
+  ix->lscreen = (uint8_t *)calloc(ix->n_str, 1);
+  ix->rscreen = (uint8_t *)calloc(ix->n_str, 1);
+
+  uint64_t cap = 0;
+  for (uint32_t s = 0; s < ix->n_str; s++) {
+    uint32_t iid = bgn + s;
+    ix->lscreen[s] = ix->rscreen[s] = 1;            /* Build_Hash_Index.C:549 */
+    if (iid < rs->first_iid || iid >= rs->first_iid + rs->nreads) continue;
+    uint32_t r = iid - rs->first_iid;
+    if ((int32_t)rs->len[r] < P->min_olap_len) continue;
+    ix->seq[s] = rs->seq[r];
+    ix->qlt[s] = rs->qlt[r];
+    ix->len[s] = rs->len[r];
+    ix->lscreen[s] = ix->rscreen[s] = 0;
+    if (rs->len[r] >= ix->k) cap += rs->len[r] - ix->k + 1;
+  }
+  ix->occ = (kmer_occ *)malloc(sizeof(kmer_occ) * (cap ? cap : 1));
+  for (uint32_t s = 0; s < ix->n_str; s++) {
+    if (!ix->seq[s] || ix->len[s] < ix->k) continue;
+    for (uint32_t o = 0; o + ix->k <= ix->len[s]; o++) {
+      int ok;
+      uint64_t key = kmer_key(ix->seq[s] + o, ix->k, &ok);
+      if (!ok) continue;                              /* key_is_bad */
+      ix->occ[ix->n_occ].key = key;
+      ix->occ[ix->n_occ].str = s;
+      ix->occ[ix->n_occ].off = o;
+      ix->n_occ++;
+    }
+  }
+  qsort(ix->occ, ix->n_occ, sizeof(kmer_occ), occ_cmp);
+
+  if (n_skip > 0) {
+    ix->skip = (uint64_t *)malloc(sizeof(uint64_t) * 2 * n_skip);
+    char *buf = (char *)malloc(ix->k + 1);
+    for (uint64_t i = 0; i < n_skip; i++) {
+      int ok;
+      for (uint32_t j = 0; j < ix->k; j++) buf[j] = (char)tolower(skip_txt[i * ix->k + j]);
+      ix->skip[ix->n_skip++] = kmer_key(buf, ix->k, &ok);
+      for (uint32_t j = 0; j < ix->k / 2; j++) {            /* reverseComplementSequence */
+        char c = buf[j];
+        buf[j] = comp_of(buf[ix->k - 1 - j]);
+        buf[ix->k - 1 - j] = comp_of(c);
+      }
+      if (ix->k & 1) buf[ix->k / 2] = comp_of(buf[ix->k / 2]);
+      ix->skip[ix->n_skip++] = kmer_key(buf, ix->k, &ok);
+    }
+    free(buf);
+    qsort(ix->skip, ix->n_skip, sizeof(uint64_t), u64_cmp);
+    /* Mark_Screened_Ends_Chain for every occurrence of a screened k-mer (:147) */
+    for (uint64_t i = 0; i < ix->n_occ; i++) {
+      if (!skip_contains(ix, ix->occ[i].key)) continue;
+      uint32_t s = ix->occ[i].str, off = ix->occ[i].off;
+      if (off < HOPELESS_MATCH) ix->lscreen[s] = 1;
+      if ((int64_t)ix->len[s] - off - ix->k + 1 < HOPELESS_MATCH) ix->rscreen[s] = 1;
+    }
+  }
+}
+
+static void index_free(kmer_index *ix) {
+  free(ix->seq); free(ix->qlt); free(ix->len); free(ix->lscreen); free(ix->rscreen);
+  free(ix->occ); free(ix->skip);
+}
+
+/* Returns the occurrence range for key, [lo, hi). */
+static void index_find(const kmer_index *ix, uint64_t key, uint64_t *lo, uint64_t *hi) {
+  uint64_t a = 0, b = ix->n_occ;
+  while (a < b) { uint64_t m = (a + b) / 2; if (ix->occ[m].key < key) a = m + 1; else b = m; }
+  *lo = a;
+  b = ix->n_occ;
+  while (a < b) { uint64_t m = (a + b) / 2; if (ix->occ[m].key <= key) a = m + 1; else b = m; }
+  *hi = a;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Work area and the per-query search                                                    */
+
+typedef struct {
+  uint32_t String_Num;
+  int32_t  Match_List;
+  double   diag_sum;
+  int32_t  diag_ct, diag_bgn, diag_end;
+  int32_t  Next;
+  int      Full, consistent;
+} string_olap;
+
+typedef struct {
+  int32_t s_lo, s_hi, t_lo, t_hi;
+  double  quality;
+  int32_t *delta;
+  int32_t delta_ct;
+  int32_t s_left_boundary, s_right_boundary, t_left_boundary, t_right_boundary;
+  int32_t min_diag, max_diag;
+} olap_info;
+
+typedef struct {
+  const oracle_params *P;
+  const kmer_index    *ix;
+  ped                  ed;
+  string_olap         *so;  int32_t so_size, so_next;
+  match_node          *mn;  int32_t mn_size, mn_next;
+  int32_t A_Olaps_For_Frag, B_Olaps_For_Frag;
+  int     left_end_screened, right_end_screened;
+  olap_info            distinct[MAX_DISTINCT_OLAPS];
+  int32_t              delta_cap;
+  char                *q_diff;
+  oracle_record       *out;  uint64_t n_out, cap_out;
+  oracle_stats         st;
+  double               minkmer_exp;            /* exp(-k * maxErate), computeExpected */
+} work_area;
+
+/* Find_Overlaps.C:79 Add_Match */
+static void add_match(work_area *W, uint32_t ref_off, int32_t *start, int32_t offset,
+                      int *consistent) {
+  int32_t k = (int32_t)W->ix->k;
+  int32_t diag = 0, expected_start = 0, num_checked = 0;
+  int     move_to_front = 0;
+  int32_t new_diag = (int32_t)ref_off - offset;
+  int32_t *p;
+
+  for (p = start; *p != 0; p = &W->mn[*p].Next) {
+    expected_start = W->mn[*p].Start + W->mn[*p].Len - k + 1;
+    diag = W->mn[*p].Offset - W->mn[*p].Start;
+    if (expected_start < offset) break;
+    if (expected_start == offset) {
+      if (new_diag == diag) {
+        W->mn[*p].Len += 1;
+        if (move_to_front) {
+          int32_t save = *p;
+          *p = W->mn[*p].Next;
+          W->mn[save].Next = *start;
+          *start = save;
+        }
+        return;
+      } else
+        move_to_front = 1;
+    }
+    num_checked++;
+  }
+
+  if (W->mn_next == W->mn_size) {
+    W->mn_size *= 2;
+    W->mn = (match_node *)realloc(W->mn, sizeof(match_node) * W->mn_size);
+  }
+  if (*start != 0 && (num_checked > 0 || abs(diag - new_diag) > 3 ||
+                      offset < expected_start + k - 2))
+    *consistent = 0;
+
+  int32_t save = *start;
+  *start = W->mn_next++;
+  W->mn[*start].Offset = (int32_t)ref_off;
+  W->mn[*start].Len    = k;
+  W->mn[*start].Start  = offset;
+  W->mn[*start].Next   = save;
+}
+
+/* Find_Overlaps.C:158 Add_Ref */
+static void add_ref(work_area *W, uint32_t str_num, uint32_t ref_off, int32_t offset) {
+  uint32_t sub = (str_num ^ (str_num >> STRING_OLAP_SHIFT)) & STRING_OLAP_MASK, prev;
+  while (W->so[sub].Full && W->so[sub].String_Num != str_num) {
+    prev = sub;
+    sub = (uint32_t)W->so[sub].Next;
+    if (sub == 0) {
+      if (W->so_next == W->so_size) {
+        W->so_size *= 2;
+        W->so = (string_olap *)realloc(W->so, sizeof(string_olap) * W->so_size);
+      }
+      sub = (uint32_t)W->so_next++;
+      W->so[prev].Next = (int32_t)sub;
+      W->so[sub].Full = 0;
+      break;
+    }
+  }
+  string_olap *s = &W->so[sub];
+  if (!s->Full) {
+    s->String_Num = str_num;
+    s->Match_List = 0;
+    s->diag_sum = 0.0;
+    s->diag_ct = 0;
+    s->diag_bgn = AS_MAX_READLEN;
+    s->diag_end = 0;
+    s->Next = 0;
+    s->Full = 1;
+    s->consistent = 1;
+  }
+  int consistent = s->consistent;
+  s->diag_sum += (double)ref_off - offset;
+  s->diag_ct++;
+  if (s->diag_bgn > offset) s->diag_bgn = offset;
+  if (s->diag_end < offset) s->diag_end = offset;
+  add_match(W, ref_off, &s->Match_List, offset, &consistent);
+  s->consistent = consistent;
+}
+
+static void emit(work_area *W, const oracle_record *r) {
+  if (W->n_out == W->cap_out) {
+    W->cap_out = W->cap_out ? 2 * W->cap_out : 1024;
+    W->out = (oracle_record *)realloc(W->out, sizeof(oracle_record) * W->cap_out);
+  }
+  W->out[W->n_out++] = *r;
+}
+
+/* ovOverlap.H:93 bit layout for AS_MAX_READLEN_BITS == 21 */
+#define W0_AHG5(x)    ((uint64_t)(x) & 0x1fffff)
+#define W0_AHG3(x)    (((uint64_t)(x) & 0x1fffff) << 21)
+#define W0_EVALUE(x)  (((uint64_t)(x) & 0xfff) << 42)
+#define W0_FLIPPED    ((uint64_t)1 << 54)
+#define W0_FOROBT     ((uint64_t)1 << 55)
+#define W0_FORDUP     ((uint64_t)1 << 56)
+#define W0_FORUTG     ((uint64_t)1 << 57)
+#define W1_BHG5(x)    ((uint64_t)(x) & 0x1fffff)
+#define W1_BHG3(x)    (((uint64_t)(x) & 0x1fffff) << 21)
+#define W1_SPAN(x)    (((uint64_t)(x) & 0x1fffff) << 42)
+
+/* ovOverlap.H:40 AS_OVS_encodeEvalue */
+static uint32_t encode_evalue(double q) {
+  return (q < AS_MAX_EVALUE / 10000.0) ? (uint32_t)(int)(10000.0 * q + 0.5) : AS_MAX_EVALUE;
+}
+
+/* Output.C:75 Output_Overlap */
+static void output_overlap(work_area *W, uint32_t S_ID, int32_t S_Len, int S_Dir,
+                           uint32_t T_ID, int32_t T_Len, const olap_info *o) {
+  oracle_record r;
+  memset(&r, 0, sizeof(r));
+  uint32_t span = (uint32_t)((o->s_hi - o->s_lo) + (o->t_hi - o->t_lo) + o->delta_ct);
+  assert(span % 2 == 0);
+  span /= 2;
+  assert(S_ID < T_ID);
+  int32_t S_Right_Hang = S_Len - o->s_hi - 1;
+  int32_t T_Right_Hang = T_Len - o->t_hi - 1;
+  int Sleft = (o->s_lo > o->t_lo) || (o->s_lo == o->t_lo && S_Right_Hang > T_Right_Hang);
+  char orient;
+  int32_t ahg, bhg;
+  if (Sleft) { r.a_iid = S_ID; r.b_iid = T_ID; }
+  else       { r.a_iid = T_ID; r.b_iid = S_ID; }
+  if (Sleft) {
+    orient = (S_Dir == 0) ? 'N' : 'O';
+    ahg = o->s_lo;
+    bhg = T_Right_Hang - S_Right_Hang;
+  } else {
+    orient = (S_Dir == 0) ? 'N' : 'I';
+    ahg = o->t_lo;
+    bhg = S_Right_Hang - T_Right_Hang;
+  }
+  if (orient == 'O' && S_Right_Hang >= T_Right_Hang) {
+    orient = 'I';
+    ahg = -(T_Right_Hang - S_Right_Hang);
+    bhg = -(o->s_lo);
+  }
+  int32_t a_hang = ahg, b_hang = bhg;
+  if (orient == 'O') { a_hang = -bhg; b_hang = -ahg; }
+  uint64_t w0 = W0_FORUTG | W0_EVALUE(encode_evalue(o->quality));
+  uint64_t w1 = W1_SPAN(span);
+  /* ovOverlap::a_hang(a) / b_hang(b) setters (ovOverlap.H:199-200) */
+  w0 |= W0_AHG5(a_hang < 0 ? 0 : a_hang);
+  w1 |= W1_BHG5(a_hang < 0 ? -a_hang : 0);
+  w1 |= W1_BHG3(b_hang < 0 ? 0 : b_hang);
+  w0 |= W0_AHG3(b_hang < 0 ? -b_hang : 0);
+  if (orient != 'N') w0 |= W0_FLIPPED;
+  r.dat[0] = w0;
+  r.dat[1] = w1;
+  emit(W, &r);
+  W->st.total_overlaps++;
+  if (bhg <= 0) W->st.contained_overlaps++;
+  else          W->st.dovetail_overlaps++;
+}
+
+/* Output.C:253 Output_Partial_Overlap */
+static void output_partial(work_area *W, uint32_t s_id, uint32_t t_id, int dir,
+                           const olap_info *o, int32_t s_len, int32_t t_len) {
+  oracle_record r;
+  memset(&r, 0, sizeof(r));
+  W->st.total_overlaps++;
+  assert(s_id < t_id);
+  r.a_iid = s_id;
+  r.b_iid = t_id;
+  uint32_t span = (uint32_t)((o->s_hi - o->s_lo) + (o->t_hi - o->t_lo) + o->delta_ct);
+  assert(span % 2 == 0);
+  span /= 2;
+  uint64_t w0 = W0_FOROBT | W0_FORDUP | W0_EVALUE(encode_evalue(o->quality));
+  uint64_t w1 = W1_SPAN(span);
+  if (dir == 0) {
+    w0 |= W0_AHG5(o->s_lo) | W0_AHG3(s_len - (o->s_hi + 1));
+    w1 |= W1_BHG5(o->t_lo) | W1_BHG3(t_len - (o->t_hi + 1));
+  } else {
+    w0 |= W0_AHG5(s_len - (o->s_hi + 1)) | W0_AHG3(o->s_lo) | W0_FLIPPED;
+    w1 |= W1_BHG5(t_len - (o->t_hi + 1)) | W1_BHG3(o->t_lo);
+  }
+  r.dat[0] = w0;
+  r.dat[1] = w1;
+  emit(W, &r);
+}
+
+static void copy_left_delta(work_area *W, olap_info *o) {
+  if (W->ed.left_delta_len > W->delta_cap) {
+    W->delta_cap = W->ed.left_delta_len * 2;
+    for (int i = 0; i < MAX_DISTINCT_OLAPS; i++)
+      W->distinct[i].delta = (int32_t *)realloc(W->distinct[i].delta,
+                                                sizeof(int32_t) * W->delta_cap);
+  }
+  memcpy(o->delta, W->ed.left_delta, sizeof(int32_t) * W->ed.left_delta_len);
+  o->delta_ct = W->ed.left_delta_len;
+}
+
+/* Process_String_Overlaps.C:222 Add_Overlap */
+static void add_overlap(work_area *W, int32_t s_lo, int32_t s_hi, int32_t t_lo,
+                        int32_t t_hi, double qual, olap_info *olap, int *ct) {
+  if (!W->P->partial) {
+    int32_t new_diag = t_lo - s_lo;
+    for (int i = 0; i < *ct; i++) {
+      int32_t old_diag = olap[i].t_lo - olap[i].s_lo;
+      if ((new_diag > 0 && old_diag > 0 &&
+           olap[i].t_right_boundary - new_diag - olap[i].s_left_boundary >= MIN_INTERSECTION) ||
+          (new_diag <= 0 && old_diag <= 0 &&
+           olap[i].s_right_boundary + new_diag - olap[i].t_left_boundary >= MIN_INTERSECTION)) {
+        if (new_diag < olap[i].min_diag) olap[i].min_diag = new_diag;
+        if (new_diag > olap[i].max_diag) olap[i].max_diag = new_diag;
+        if (s_lo < olap[i].s_left_boundary)  olap[i].s_left_boundary = s_lo;
+        if (s_hi > olap[i].s_right_boundary) olap[i].s_right_boundary = s_hi;
+        if (t_lo < olap[i].t_left_boundary)  olap[i].t_left_boundary = t_lo;
+        if (t_hi > olap[i].t_right_boundary) olap[i].t_right_boundary = t_hi;
+        if (qual < olap[i].quality) {
+          olap[i].s_lo = s_lo; olap[i].s_hi = s_hi;
+          olap[i].t_lo = t_lo; olap[i].t_hi = t_hi;
+          olap[i].quality = qual;
+          copy_left_delta(W, &olap[i]);
+        }
+        return;
+      }
+    }
+  }
+  if (*ct >= MAX_DISTINCT_OLAPS) return;
+  olap_info *o = &olap[*ct];
+  o->s_lo = o->s_left_boundary = s_lo;
+  o->s_hi = o->s_right_boundary = s_hi;
+  o->t_lo = o->t_left_boundary = t_lo;
+  o->t_hi = o->t_right_boundary = t_hi;
+  o->quality = qual;
+  copy_left_delta(W, o);
+  o->min_diag = o->max_diag = t_lo - s_lo;
+  (*ct)++;
+}
+
+/* Process_String_Overlaps.C:307 Lies_On_Alignment */
+static int lies_on_alignment(work_area *W, int32_t start, int32_t offset, int32_t s_lo,
+                             int32_t t_lo) {
+  int32_t diag = t_lo - s_lo, new_diag = offset - start;
+  for (int32_t i = 0; i < W->ed.left_delta_len; i++) {
+    s_lo += abs(W->ed.left_delta[i]);
+    if (start < s_lo) return abs(new_diag - diag) <= SHIFT_SLACK;
+    if (W->ed.left_delta[i] < 0) diag++;
+    else { s_lo++; diag--; }
+  }
+  return abs(new_diag - diag) <= SHIFT_SLACK;
+}
+
+static void combine_into_one(olap_info *o, int ct, int *deleted) {
+  int best = 0;
+  int32_t min_diag = o[0].min_diag, max_diag = o[0].max_diag;
+  int32_t slb = o[0].s_left_boundary, srb = o[0].s_right_boundary;
+  int32_t tlb = o[0].t_left_boundary, trb = o[0].t_right_boundary;
+  for (int i = 1; i < ct; i++) {
+    if (o[i].quality < o[best].quality) best = i;
+    if (o[i].min_diag < min_diag) min_diag = o[i].min_diag;
+    if (o[i].max_diag > max_diag) max_diag = o[i].max_diag;
+    if (o[i].s_left_boundary < slb) slb = o[i].s_left_boundary;
+    if (o[i].s_right_boundary > srb) srb = o[i].s_right_boundary;
+    if (o[i].t_left_boundary < tlb) tlb = o[i].t_left_boundary;
+    if (o[i].t_right_boundary > trb) trb = o[i].t_right_boundary;
+  }
+  o[best].min_diag = min_diag; o[best].max_diag = max_diag;
+  o[best].s_left_boundary = slb; o[best].s_right_boundary = srb;
+  o[best].t_left_boundary = tlb; o[best].t_right_boundary = trb;
+  for (int i = 0; i < ct; i++) deleted[i] = (i != best);
+}
+
+static void merge_intersecting(olap_info *p, int ct, int *deleted) {
+  for (int i = 0; i < ct - 1; i++)
+    for (int j = i + 1; j < ct; j++) {
+      if (deleted[i] || deleted[j]) continue;
+      int32_t lo = p[i].min_diag, hi = p[i].max_diag;
+      if ((lo <= 0 && p[j].min_diag > 0) || (lo > 0 && p[j].min_diag <= 0)) continue;
+      if ((lo >= 0 && p[j].t_right_boundary - lo - p[j].s_left_boundary >= MIN_INTERSECTION) ||
+          (lo <= 0 && p[j].s_right_boundary + lo - p[j].t_left_boundary >= MIN_INTERSECTION) ||
+          (hi >= 0 && p[j].t_right_boundary - hi - p[j].s_left_boundary >= MIN_INTERSECTION) ||
+          (hi <= 0 && p[j].s_right_boundary + hi - p[j].t_left_boundary >= MIN_INTERSECTION)) {
+        olap_info *keep, *discard;
+        if (p[i].quality < p[j].quality) { keep = p + i; discard = p + j; deleted[j] = 1; }
+        else                             { keep = p + j; discard = p + i; deleted[i] = 1; }
+        if (discard->min_diag < keep->min_diag) keep->min_diag = discard->min_diag;
+        if (discard->max_diag > keep->max_diag) keep->max_diag = discard->max_diag;
+        if (discard->s_left_boundary < keep->s_left_boundary)
+          keep->s_left_boundary = discard->s_left_boundary;
+        if (discard->s_right_boundary > keep->s_right_boundary)
+          keep->s_right_boundary = discard->s_right_boundary;
+        if (discard->t_left_boundary < keep->t_left_boundary)
+          keep->t_left_boundary = discard->t_left_boundary;
+        if (discard->t_right_boundary > keep->t_right_boundary)
+          keep->t_right_boundary = discard->t_right_boundary;
+      }
+    }
+}
+
+static void choose_best_partial(olap_info *o, int ct, int *deleted) {
+  int best = 0;
+  double mbest = (1.0 - o[0].quality) * (2 + o[0].s_hi - o[0].s_lo + o[0].t_hi - o[0].t_lo);
+  for (int i = 1; i < ct; i++) {
+    double mb = (1.0 - o[i].quality) * (2 + o[i].s_hi - o[i].s_lo + o[i].t_hi - o[i].t_lo);
+    if (mbest < mb || (mbest == mb && o[i].quality < o[best].quality)) best = i;
+  }
+  for (int i = 0; i < ct; i++) deleted[i] = (i != best);
+}
+
+static int has_bad_window(const char *a, int n, int wl, int thr) {
+  if (n < wl) return 0;
+  int32_t sum = 0, i, j = 0;
+  for (i = 0; i < wl; i++) sum += a[i];
+  if (sum >= thr) return 1;
+  while (i < n) {
+    sum -= a[j++];
+    sum += a[i++];
+    if (sum >= thr) return 1;
+  }
+  return 0;
+}
+
+/* Process_String_Overlaps.C:400 Process_Matches */
+static void process_matches(work_area *W, int32_t *Start, const char *S, int32_t S_Len,
+                            const char *S_quality, uint32_t S_ID, int Dir, const char *T,
+                            uint32_t t_str, const char *T_quality, uint32_t T_ID,
+                            int consistent) {
+  const oracle_params *P = W->P;
+  const kmer_index *ix = W->ix;
+  int32_t t_len = (int32_t)ix->len[t_str];
+  int kind = OLAP_NONE;
+  int overlaps_output = 0, distinct_ct = 0;
+  int32_t S_Lo = 0, S_Hi = 0, T_Lo = 0, T_Hi = 0, Errors = 0;
+
+  assert(*Start != 0);
+
+  if (P->use_hopeless_check && W->mn[*Start].Next == 0 && !P->partial) {
+    int32_t s_head = W->mn[*Start].Start, t_head = W->mn[*Start].Offset;
+    int hopeless = 0;
+    if (s_head <= t_head) {
+      if (s_head > HOPELESS_MATCH && !W->left_end_screened) hopeless = 1;
+    } else {
+      if (t_head > HOPELESS_MATCH && !ix->lscreen[t_str]) hopeless = 1;
+    }
+    int32_t s_tail = S_Len - s_head - W->mn[*Start].Len + 1;
+    int32_t t_tail = t_len - t_head - W->mn[*Start].Len + 1;
+    if (s_tail <= t_tail) {
+      if (s_tail > HOPELESS_MATCH && !W->right_end_screened) hopeless = 1;
+    } else {
+      if (t_tail > HOPELESS_MATCH && !ix->rscreen[t_str]) hopeless = 1;
+    }
+    if (hopeless) {
+      *Start = 0;
+      W->st.kmer_hits_without_olap++;
+      return;
+    }
+  }
+
+  olap_info *distinct = W->distinct;
+  while (*Start != 0) {
+    int32_t max_len = W->mn[*Start].Len;
+    match_node *longest = &W->mn[*Start];
+    for (int32_t p = W->mn[*Start].Next; p != 0; p = W->mn[p].Next)
+      if (W->mn[p].Len > max_len) { max_len = W->mn[p].Len; longest = &W->mn[p]; }
+
+    int32_t a_hang = longest->Start - longest->Offset;
+    int32_t b_hang = a_hang + S_Len - t_len;
+    int hit_limit = ((uint64_t)W->A_Olaps_For_Frag >= P->frag_olap_limit && a_hang <= 0) ||
+                    ((uint64_t)W->B_Olaps_For_Frag >= P->frag_olap_limit && b_hang <= 0);
+    if (!hit_limit) {
+      kind = extend_alignment(&W->ed, longest, S, S_Len, T, t_len, &S_Lo, &S_Hi, &T_Lo,
+                              &T_Hi, &Errors);
+      if (kind == DOVETAIL || P->partial) {
+        if (1 + S_Hi - S_Lo >= P->min_olap_len && 1 + T_Hi - T_Lo >= P->min_olap_len) {
+          int32_t olap_len = 1 + ((S_Hi - S_Lo) < (T_Hi - T_Lo) ? (S_Hi - S_Lo) : (T_Hi - T_Lo));
+          double quality = (double)Errors / olap_len;
+          if (Errors <= W->ed.t->error_bound[olap_len])
+            add_overlap(W, S_Lo, S_Hi, T_Lo, T_Hi, quality, distinct, &distinct_ct);
+        }
+      }
+    }
+    if (consistent) *Start = 0;
+
+    for (int32_t *ref = Start; *ref != 0;) {
+      match_node *ptr = &W->mn[*ref];
+      if (ptr == longest ||
+          ((kind == DOVETAIL || P->partial) && S_Lo - SHIFT_SLACK <= ptr->Start &&
+           ptr->Start + ptr->Len <= (S_Hi + 1) + SHIFT_SLACK - 1 &&
+           lies_on_alignment(W, ptr->Start, ptr->Offset, S_Lo, T_Lo)))
+        *ref = ptr->Next;
+      else
+        ref = &ptr->Next;
+    }
+  }
+
+  if (distinct_ct > 0) {
+    int deleted[MAX_DISTINCT_OLAPS] = {0};
+    if (P->partial) {
+      if (P->unique_olap_per_pair) choose_best_partial(distinct, distinct_ct, deleted);
+    } else {
+      if (P->unique_olap_per_pair) combine_into_one(distinct, distinct_ct, deleted);
+      else                         merge_intersecting(distinct, distinct_ct, deleted);
+    }
+    for (int i = 0; i < distinct_ct; i++) {
+      olap_info *p = &distinct[i];
+      if (deleted[i]) continue;
+      int rejected = 0;
+      if (P->use_window_filter) {
+        int32_t si = p->s_lo, tj = p->t_lo, q_len = 0, d;
+        char *q = W->q_diff;
+        for (int32_t k = 0; k < p->delta_ct; k++) {
+          int32_t len = abs(p->delta[k]);
+          for (int32_t n = 1; n < len; n++) {
+            if (S[si] == T[tj] || S[si] == 'n' || T[tj] == 'n') d = 0;
+            else {
+              d = S_quality[si] < T_quality[tj] ? S_quality[si] : T_quality[tj];
+              if (d > QUALITY_CUTOFF) d = QUALITY_CUTOFF;
+            }
+            q[q_len++] = (char)d;
+            si++; tj++;
+          }
+          if (p->delta[k] > 0) { d = S_quality[si]; si++; }
+          else                 { d = T_quality[tj]; tj++; }
+          q[q_len++] = (char)(d < QUALITY_CUTOFF ? d : QUALITY_CUTOFF);
+        }
+        while (si <= p->s_hi) {
+          if (S[si] == T[tj] || S[si] == 'n' || T[tj] == 'n') d = 0;
+          else {
+            d = S_quality[si] < T_quality[tj] ? S_quality[si] : T_quality[tj];
+            if (d > QUALITY_CUTOFF) d = QUALITY_CUTOFF;
+          }
+          q[q_len++] = (char)d;
+          si++; tj++;
+        }
+        if (has_bad_window(q, q_len, BAD_WINDOW_LEN, BAD_WINDOW_VALUE)) rejected = 1;
+        else if (has_bad_window(q, q_len, 100, 240))                     rejected = 1;
+      }
+      if (!rejected) {
+        if (P->partial) output_partial(W, S_ID, T_ID, Dir, p, S_Len, t_len);
+        else            output_overlap(W, S_ID, S_Len, Dir, T_ID, t_len, p);
+        overlaps_output++;
+        if (p->s_lo == 0) W->A_Olaps_For_Frag++;
+        if (p->s_hi >= S_Len - 1) W->B_Olaps_For_Frag++;
+      }
+    }
+  }
+  if (overlaps_output == 0) W->st.kmer_hits_without_olap++;
+  else {
+    W->st.kmer_hits_with_olap++;
+    if (overlaps_output > 1) W->st.multi_overlaps++;
+  }
+}
+
+static uint64_t compute_min_kmers(work_area *W, double ovl_len) {
+  const oracle_params *P = W->P;
+  if (P->filter_by_kmer_count == 0) return 0;
+  if (ovl_len < 0) ovl_len = -ovl_len;
+  uint64_t expct = 0;
+  if (!(ovl_len < P->kmer_len))
+    expct = (uint64_t)(int)floor(W->minkmer_exp * (ovl_len - P->kmer_len + 1));
+  return expct > P->filter_by_kmer_count ? expct : P->filter_by_kmer_count;
+}
+
+static int by_diag_sum(const void *a, const void *b) {
+  const string_olap *x = (const string_olap *)a, *y = (const string_olap *)b;
+  if (x->diag_sum < y->diag_sum) return -1;
+  if (x->diag_sum > y->diag_sum) return 1;
+  return 0;
+}
+
+/* Process_String_Overlaps.C:687 Process_String_Olaps */
+static void process_string_olaps(work_area *W, const char *S, int32_t Len,
+                                 const char *S_quality, uint32_t ID, int Dir) {
+  const kmer_index *ix = W->ix;
+  int32_t ct = 0;
+  for (int32_t i = 0; i < W->so_next; i++)
+    if (W->so[i].Full) {
+      uint32_t root = W->so[i].String_Num;
+      if (root + ix->hash_bgn > ID) {
+        if (i != ct) W->so[ct] = W->so[i];
+        W->so[ct].diag_sum /= W->so[ct].diag_ct;
+        ct++;
+      }
+    }
+  if (ct == 0) return;
+  W->st.pairs += ct;
+
+#define PROCESS_ONE(i)                                                                     \
+  do {                                                                                     \
+    uint32_t root = W->so[i].String_Num;                                                   \
+    if (compute_min_kmers(W, (double)(W->so[i].diag_end - W->so[i].diag_bgn)) >           \
+        (uint64_t)W->so[i].diag_ct) {                                                      \
+      W->st.kmer_hits_skipped++;                                                           \
+      continue;                                                                            \
+    }                                                                                      \
+    process_matches(W, &W->so[i].Match_List, S, Len, S_quality, ID, Dir, ix->seq[root],    \
+                    root, ix->qlt[root], root + ix->hash_bgn, W->so[i].consistent);        \
+  } while (0)
+
+  if ((uint64_t)ct <= W->P->frag_olap_limit) {
+    for (int32_t i = 0; i < ct; i++) PROCESS_ONE(i);
+    return;
+  }
+  qsort(W->so, ct, sizeof(string_olap), by_diag_sum);
+  int32_t start;
+  for (start = 0; start < ct && W->so[start].diag_sum < 0; start++)
+    ;
+  for (int32_t i = start; i < ct && (uint64_t)W->A_Olaps_For_Frag < W->P->frag_olap_limit; i++)
+    PROCESS_ONE(i);
+  for (int32_t i = start - 1; i >= 0 && (uint64_t)W->B_Olaps_For_Frag < W->P->frag_olap_limit; i--)
+    PROCESS_ONE(i);
+#undef PROCESS_ONE
+}
+
+/* Find_Overlaps.C:284 Find_Overlaps */
+static void find_overlaps(work_area *W, const char *Frag, int32_t Frag_Len,
+                          const char *quality, uint32_t Frag_Num, int Dir) {
+  const kmer_index *ix = W->ix;
+  const int32_t k = (int32_t)ix->k;
+  memset(W->so, 0, sizeof(string_olap) * STRING_OLAP_MODULUS);
+  W->so_next = STRING_OLAP_MODULUS;
+  W->mn_next = 1;
+  W->left_end_screened = W->right_end_screened = 0;
+  W->A_Olaps_For_Frag = W->B_Olaps_For_Frag = 0;
+  assert(Frag_Len >= k);
+
+  /* Windows are visited while the window's last char is not NUL (the reference's
+   * `while (*P != '\0')`); a NUL inside the query (reverse complement of 'n') stops it.
+   * Window 0 is always visited. */
+  for (int32_t off = 0;; off++) {
+    if (off > 0 && Frag[off + k - 1] == 0) break;
+    int ok;
+    uint64_t key = kmer_key(Frag + off, (uint32_t)k, &ok);
+    /* A window with a non-ACGT char never strncmp-matches a hashed k-mer. */
+    if (!ok) continue;
+    if (skip_contains(ix, key)) {
+      /* Hash_Find returned an Empty entry: hi_hits. With the hopeless check off the
+       * extra string is not added (Build_Hash_Index.C:209), but then the flags are
+       * never read, so setting them is harmless. */
+      if (off == 0 || off < HOPELESS_MATCH) W->left_end_screened = 1;
+      if (off > 0 && Frag_Len - off - k + 1 < HOPELESS_MATCH) W->right_end_screened = 1;
+      continue;
+    }
+    uint64_t lo, hi;
+    index_find(ix, key, &lo, &hi);
+    for (uint64_t i = lo; i < hi; i++) {
+      const kmer_occ *o = &ix->occ[i];
+      if (Frag_Num < o->str + ix->hash_bgn) {
+        add_ref(W, o->str, o->off, off);
+        W->st.seed_hits++;
+      }
+    }
+  }
+  process_string_olaps(W, Frag, Frag_Len, quality, Frag_Num, Dir);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Entry point                                                                           */
+
+int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
+                   const uint8_t *bases, const uint64_t *offsets, const uint32_t *lengths,
+                   const uint8_t *quals, const char *skip_kmers, uint64_t n_skip,
+                   uint32_t hash_bgn, uint32_t hash_end, uint32_t ref_bgn, uint32_t ref_end,
+                   oracle_record **out, uint64_t *n_out, oracle_stats *stats) {
+  if (P->kmer_len == 0 || P->kmer_len > 31) return -2;
+  read_set rs;
+  rs.first_iid = first_iid;
+  rs.nreads = nreads;
+  rs.seq = (char **)calloc(nreads, sizeof(char *));
+  rs.qlt = (char **)calloc(nreads, sizeof(char *));
+  rs.len = (uint32_t *)calloc(nreads, sizeof(uint32_t));
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < nreads; i++) {
+    rs.len[i] = lengths[i];
+    if (lengths[i] > max_len) max_len = lengths[i];
+    rs.seq[i] = (char *)malloc(lengths[i] + 1);
+    rs.qlt[i] = (char *)malloc(lengths[i] + 1);
+    for (uint32_t j = 0; j < lengths[i]; j++) {
+      rs.seq[i][j] = (char)tolower(bases[offsets[i] + j]);
+      rs.qlt[i][j] = quals ? (char)quals[offsets[i] + j] : 0;
+    }
+    rs.seq[i][lengths[i]] = 0;
+    rs.qlt[i][lengths[i]] = 0;
+  }
+
+  ped_tables tabs;
+  ped_tables_init(&tabs, P->max_erate, P->partial);
+
+  kmer_index ix;
+  if (hash_end > first_iid + nreads - 1) hash_end = first_iid + nreads - 1;
+  if (hash_bgn < 1) hash_bgn = 1;
+  index_build(&ix, &rs, P, hash_bgn, hash_end, skip_kmers, n_skip);
+
+  work_area W;
+  memset(&W, 0, sizeof(W));
+  W.P = P;
+  W.ix = &ix;
+  W.ed.t = &tabs;
+  W.so_size = 5000;                                   /* INIT_STRING_OLAP_SIZE */
+  W.so = (string_olap *)calloc(W.so_size, sizeof(string_olap));
+  W.mn_size = 10000;                                  /* INIT_MATCH_NODE_SIZE  */
+  W.mn = (match_node *)calloc(W.mn_size, sizeof(match_node));
+  W.delta_cap = 1024;
+  for (int i = 0; i < MAX_DISTINCT_OLAPS; i++)
+    W.distinct[i].delta = (int32_t *)malloc(sizeof(int32_t) * W.delta_cap);
+  W.q_diff = (char *)malloc(2 * (size_t)max_len + 16);
+  W.minkmer_exp = exp(-1.0 * (double)P->kmer_len * P->max_erate);
+
+  char *fbuf = (char *)malloc(max_len + 1), *qbuf = (char *)malloc(max_len + 1);
+  if (ref_bgn < 1) ref_bgn = 1;
+  if (ref_end > first_iid + nreads - 1) ref_end = first_iid + nreads - 1;
+  for (uint32_t a = ref_bgn; a <= ref_end; a++) {
+    if (a < first_iid) continue;
+    uint32_t r = a - first_iid;
+    int32_t len = (int32_t)rs.len[r];
+    if (len < P->min_olap_len) continue;
+    if (len < (int32_t)P->kmer_len) continue;            /* reference would assert */
+    memcpy(fbuf, rs.seq[r], len + 1);
+    memcpy(qbuf, rs.qlt[r], len + 1);
+    find_overlaps(&W, fbuf, len, qbuf, a, 0);
+    /* AS_UTL_reverseComplement.C reverseComplement(seq, qlt, len) */
+    for (int32_t i = 0, j = len - 1; i <= j; i++, j--) {
+      char c = fbuf[i], q = qbuf[i];
+      fbuf[i] = comp_of(fbuf[j]); qbuf[i] = qbuf[j];
+      fbuf[j] = comp_of(c);       qbuf[j] = q;
+    }
+    find_overlaps(&W, fbuf, len, qbuf, a, 1);
+  }
+
+  *out = W.out;
+  *n_out = W.n_out;
+  if (stats) *stats = W.st;
+
+  free(fbuf); free(qbuf);
+  free(W.so); free(W.mn); free(W.q_diff);
+  for (int i = 0; i < MAX_DISTINCT_OLAPS; i++) free(W.distinct[i].delta);
+  free(W.ed.space); free(W.ed.left_delta); free(W.ed.right_delta); free(W.ed.delta_stack);
+  index_free(&ix);
+  ped_tables_free(&tabs);
+  for (uint32_t i = 0; i < nreads; i++) { free(rs.seq[i]); free(rs.qlt[i]); }
+  free(rs.seq); free(rs.qlt); free(rs.len);
+  return 0;
+}
+
+void oic_oracle_free(void *p) { free(p); }
+
+/* Exposed for tests of the table code. */
+int oic_oracle_match_limit(double erate, int32_t *out, int32_t n) {
+  ped_tables t;
+  ped_tables_init(&t, erate, 0);
+  for (int32_t i = 0; i < n && i <= t.max_errors; i++) out[i] = t.match_limit[i];
+  int32_t me = t.max_errors;
+  ped_tables_free(&t);
+  return me;
+}

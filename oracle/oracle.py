@@ -1,0 +1,200 @@
+"""Python access to the parity checkers (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+  * run_oracle(...)    -- the C restatement in oic_oracle.c (oracle/_build/liboic_oracle.so)
+  * run_reference(...) -- the reference overlapInCore built from its own sources
+                          (oracle/_ref/oic_ref, see ref_harness.cpp)
+Both return records as a numpy structured array with fields a, b, w0, w1 (the ovOverlap
+a_iid, b_iid and dat[0], dat[1]), sorted by ovOverlap::operator<.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import tempfile
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboic_oracle.so")
+REF_BIN = os.path.join(HERE, "_ref", "oic_ref")
+
+RECORD_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("w0", "<u8"), ("w1", "<u8")])
+
+
+class OracleParams(ctypes.Structure):
+    _fields_ = [("kmer_len", ctypes.c_uint32), ("max_erate", ctypes.c_double),
+                ("min_olap_len", ctypes.c_int32), ("partial", ctypes.c_int32),
+                ("unique_olap_per_pair", ctypes.c_int32), ("use_window_filter", ctypes.c_int32),
+                ("use_hopeless_check", ctypes.c_int32), ("frag_olap_limit", ctypes.c_uint64),
+                ("filter_by_kmer_count", ctypes.c_uint64)]
+
+
+class OracleStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "kmer_hits_without_olap", "kmer_hits_with_olap", "kmer_hits_skipped", "multi_overlaps",
+        "total_overlaps", "contained_overlaps", "dovetail_overlaps", "seed_hits", "pairs")]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.oic_oracle_run.restype = ctypes.c_int
+        lib.oic_oracle_run.argtypes = [
+            ctypes.POINTER(OracleParams), ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_char_p, ctypes.c_uint64,
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64),
+            ctypes.POINTER(OracleStats)]
+        lib.oic_oracle_free.argtypes = [ctypes.c_void_p]
+        lib.oic_oracle_match_limit.restype = ctypes.c_int
+        lib.oic_oracle_match_limit.argtypes = [ctypes.c_double, ctypes.c_void_p, ctypes.c_int32]
+        _lib = lib
+    return _lib
+
+
+def default_params(**kw) -> dict:
+    """oicParameters::initialize() defaults (overlapInCore.H:425), plus main()'s
+    fix-up for maxErate > 0.06 (overlapInCore.C:416)."""
+    p = dict(kmer_len=22, max_erate=0.06, min_olap_len=0, partial=0, unique_olap_per_pair=1,
+             use_window_filter=0, use_hopeless_check=1, frag_olap_limit=(1 << 64) - 1,
+             filter_by_kmer_count=0)
+    p.update(kw)
+    # main() parses --maxerate with strtof: the value is float-rounded.
+    p["max_erate"] = float(np.float32(p["max_erate"]))
+    if p["max_erate"] > 0.06:
+        p["use_window_filter"] = 0
+        p["use_hopeless_check"] = 0
+    return p
+
+
+def sort_records(rec: np.ndarray) -> np.ndarray:
+    return rec[np.lexsort((rec["w1"], rec["w0"], rec["b"], rec["a"]))]
+
+
+def run_oracle(rs, params: dict, hash_range=None, ref_range=None, skip_kmers=None,
+               with_stats=False):
+    lib = _load()
+    P = OracleParams(**params)
+    first = rs.first_iid
+    last = first + rs.nreads - 1
+    hb, he = hash_range if hash_range else (first, last)
+    rb, re_ = ref_range if ref_range else (first, last)
+    skip = b""
+    n_skip = 0
+    if skip_kmers:
+        skip = b"".join(k.encode() if isinstance(k, str) else k for k in skip_kmers)
+        n_skip = len(skip_kmers)
+    out = ctypes.c_void_p()
+    n = ctypes.c_uint64()
+    st = OracleStats()
+    bases = np.ascontiguousarray(rs.bases)
+    offs = np.ascontiguousarray(rs.offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(rs.lengths, dtype=np.uint32)
+    quals = None if rs.quals is None else np.ascontiguousarray(rs.quals)
+    rc = lib.oic_oracle_run(ctypes.byref(P), first, rs.nreads,
+                            bases.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                            None if quals is None else quals.ctypes.data,
+                            skip, n_skip, hb, he, rb, re_, ctypes.byref(out), ctypes.byref(n),
+                            ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oic_oracle_run failed: {rc}")
+    count = n.value
+    rec = np.zeros(count, dtype=RECORD_DTYPE)
+    if count:
+        ctypes.memmove(rec.ctypes.data, out.value, count * RECORD_DTYPE.itemsize)
+    if out.value:
+        lib.oic_oracle_free(out)
+    rec = sort_records(rec)
+    if with_stats:
+        return rec, {f: getattr(st, f) for f, _ in OracleStats._fields_}
+    return rec
+
+
+def match_limit(erate: float, n: int) -> tuple[int, np.ndarray]:
+    lib = _load()
+    out = np.zeros(n, dtype=np.int32)
+    me = lib.oic_oracle_match_limit(erate, out.ctypes.data, n)
+    return me, out
+
+
+def reference_available() -> bool:
+    return os.path.exists(REF_BIN)
+
+
+def params_to_ref_args(params: dict) -> list[str]:
+    a = ["-k", str(params["kmer_len"]), "--maxerate", repr(params["max_erate"]),
+         "--minlength", str(params["min_olap_len"])]
+    if params.get("partial"):
+        a.append("-G")
+    a.append("-u" if params.get("unique_olap_per_pair", 1) else "-m")
+    if params.get("use_window_filter"):
+        a.append("-w")
+    if not params.get("use_hopeless_check", 1):
+        a.append("-z")
+    lim = params.get("frag_olap_limit", (1 << 64) - 1)
+    if lim != (1 << 64) - 1:
+        a += ["-l", str(lim)]
+    return a
+
+
+def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
+                  skip_kmers=None, minkmers: bool = False, extra=None, workdir=None,
+                  with_time=False):
+    """Run the reference overlapInCore (built from its sources) on `rs`.
+
+    The whole read set is one hash batch and one ref range, so every pair (a<b) is
+    searched once, as the reference's full -h/-r ranges do."""
+    from canu_amd.synth import write_reads_file  # input writer only
+    if not reference_available():
+        raise FileNotFoundError(REF_BIN)
+    own = workdir is None
+    wd = workdir or tempfile.mkdtemp(prefix="oicref_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        reads = os.path.join(wd, "reads.bin")
+        write_reads_file(reads, rs)
+        out = os.path.join(wd, "records.bin")
+        args = [REF_BIN, reads, os.path.join(wd, "w"), out, "-t", str(threads),
+                "--hashbits", str(hash_bits), "--hashstrings", str(max(rs.nreads + 10, 1000)),
+                "--hashdatalen", str(rs.total_bases() + rs.nreads + 1024), "--time"]
+        args += params_to_ref_args(params)
+        if minkmers:
+            args.append("--minkmers")
+        if skip_kmers:
+            sk = os.path.join(wd, "skip.fasta")
+            with open(sk, "w") as f:
+                for i, k in enumerate(skip_kmers):
+                    f.write(f">{i}\n{k if isinstance(k, str) else k.decode()}\n")
+            args += ["--skip", sk]
+        if extra:
+            args += list(extra)
+        t0 = time.time()
+        cp = subprocess.run(args, capture_output=True, text=True)
+        wall = time.time() - t0
+        if cp.returncode != 0:
+            raise RuntimeError(f"oic_ref failed ({cp.returncode}): {cp.stderr[-2000:]}")
+        secs = None
+        for line in cp.stdout.splitlines():
+            if line.startswith("OVERLAPDRIVER_SECONDS"):
+                secs = float(line.split()[1])
+        rec = np.fromfile(out, dtype=RECORD_DTYPE)
+        rec = sort_records(rec)
+        if with_time:
+            return rec, secs, wall
+        return rec
+    finally:
+        if own:
+            subprocess.run(["rm", "-rf", wd])
