@@ -1,0 +1,795 @@
+// ovl_api.hip -- the C-ABI (include/canu_ovl.h) and the host side of the HIP path.
+//
+// Host responsibilities mirror overlapInCore's driver (overlapInCore.C:190 OverlapDriver,
+// :306 main): option fix-ups, the maxErate tables (prefixEditDistance.C:40-116,
+// Binomial_Bound.C), read loading, then the per-batch kernel sequence
+//   k_probe -> k_chain -> k_extend
+// over (query, orientation) units.  There is no CPU fallback for any of it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/canu_ovl.h"
+#include "ovl_common.h"
+
+#include "ovl_index.hip"
+#include "ovl_seed.hip"
+#include "ovl_extend.hip"
+
+using namespace ovl;
+
+// ---------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPC(x)                                                                         \
+  do {                                                                                  \
+    hipError_t _e = (x);                                                                \
+    if (_e != hipSuccess)                                                               \
+      return fail(OVL_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #x,                 \
+                  hipGetErrorString(_e));                                               \
+  } while (0)
+
+template <typename T>
+struct DBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    hipError_t e = hipMalloc((void **)&p, bytes);
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+};
+
+static const uint32_t AS_MAX_READLEN = (1u << 21) - 1;
+
+// ---------------------------------------------------------------------------------------
+// maxErate tables (prefixEditDistance.C:40-116; Binomial_Bound.C:47 and :121)
+
+static int binomial_bound(int e, double p, int start) {
+  const double bound = 1e-4, thold = 3.62;
+  double q = 1.0 - p;
+  if (start < e) start = e;
+  for (int n = start; n < (int)AS_MAX_READLEN; n++) {
+    if (n <= 35) {
+      double sum = 0.0, p_pow = 1.0, q_pow = pow(q, n);
+      int bin = 1, ct = 0;
+      for (int k = 0; k < e && 1.0 - sum > bound; k++) {
+        double x = bin * p_pow * q_pow;
+        sum += x;
+        bin *= n - ct;
+        bin /= ++ct;
+        p_pow *= p;
+        q_pow /= q;
+      }
+      if (1.0 - sum > bound) return n;
+    } else {
+      double z = (e - 0.5 - n * p) / sqrt(n * p * q);
+      if (z <= thold) return n;
+      double sum = 0.0, mu_pow = 1.0, fact = 1.0, pc = exp(-n * p);
+      for (int k = 0; k < e; k++) {
+        sum += mu_pow * pc / fact;
+        mu_pow *= n * p;
+        fact *= k + 1;
+      }
+      if (1.0 - sum > bound) return n;
+    }
+  }
+  return AS_MAX_READLEN;
+}
+
+static void init_match_limit(std::vector<int32_t> &ml, double erate, int32_t max_errors) {
+  ml.assign(max_errors + 1, 0);
+  int32_t e = 0, s = 1, l = std::min<int32_t>(max_errors, 2000);
+  while (e <= 1) ml[e++] = 0;
+  while (e < l) {
+    s = binomial_bound(e - 1, erate, s);
+    ml[e] = s - 1;
+    e++;
+  }
+  double sl = 0.982064188397525 / erate + 0.067835741959926;   // AS_MAX_READLEN_BITS 21
+  double vl = ml[e - 1] + sl;
+  while (e < max_errors) {
+    ml[e] = (int32_t)ceil(vl);
+    vl += sl;
+    e++;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+
+struct ovl_ctx {
+  ovl_params P;
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8];
+
+  // tables
+  int32_t max_errors = 0;
+  double branch_match_value = 0, min_branch_tail_slope = 0;
+  DBuf<int32_t> d_error_bound, d_match_limit;
+  std::vector<int32_t> h_error_bound;
+
+  // reads
+  uint32_t first_iid = 0, nreads = 0;
+  std::vector<uint32_t> h_len;
+  std::vector<uint64_t> h_wofs;
+  DBuf<uint64_t> d_fwd, d_rc, d_wofs;
+  DBuf<uint32_t> d_fwdN, d_rcNul, d_len, d_flags, d_rcFirstNul;
+  uint32_t max_len = 0;
+
+  // skip k-mers (both strands, deduplicated codes)
+  std::vector<uint64_t> h_skip;
+  DBuf<uint64_t> d_skip;
+
+  // index
+  bool have_index = false;
+  uint32_t hash_bgn_iid = 0, hash_end_iid = 0;
+  DBuf<uint64_t> d_occ, d_tmpM, d_tmpP, d_tmpM2;
+  DBuf<TabEntry> d_tab;
+  uint32_t tab_bits = 0, slice_bits = 0;
+
+  // results
+  DBuf<Rec> d_out;
+  uint64_t nout = 0;
+  ovl_stats stats;
+
+  ReadsDev reads() const {
+    ReadsDev R;
+    R.fwd = d_fwd.p;
+    R.rc = d_rc.p;
+    R.fwdN = d_fwdN.p;
+    R.rcNul = d_rcNul.p;
+    R.wofs = d_wofs.p;
+    R.len = d_len.p;
+    R.flags = d_flags.p;
+    R.rcFirstNul = d_rcFirstNul.p;
+    R.first_iid = first_iid;
+    R.nreads = nreads;
+    return R;
+  }
+};
+
+extern "C" {
+
+int ovl_abi_version(void) { return OVL_ABI_VERSION; }
+
+const char *ovl_last_error(void) { return g_err.c_str(); }
+
+void ovl_params_init(ovl_params *p) {
+  p->kmer_len = 0;
+  p->max_erate = 0.06;
+  p->min_olap_len = 0;
+  p->partial = 0;
+  p->unique_olap_per_pair = 1;
+  p->use_window_filter = 0;
+  p->use_hopeless_check = 1;
+  p->frag_olap_limit = UINT64_MAX;
+  p->filter_by_kmer_count = 0;
+}
+
+void ovl_params_finalize(ovl_params *p) {
+  if (p->max_erate > 0.06) {
+    p->use_window_filter = 0;
+    p->use_hopeless_check = 0;
+  }
+}
+
+void *ovl_ctx_stream(ovl_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
+  *out = nullptr;
+  if (p->kmer_len == 0) return fail(OVL_ERR_BAD_PARAM, "kmer length (-k) needed");
+  if (p->kmer_len > 31) return fail(OVL_ERR_BAD_PARAM, "kmer length must be <= 31");
+  if (!(p->max_erate > 0.0) || p->max_erate >= 1.0)
+    return fail(OVL_ERR_BAD_PARAM, "maxErate out of range");
+  if (p->use_window_filter && p->max_erate <= 0.06)
+    return fail(OVL_ERR_UNSUPPORTED, "-w (window filter) is not implemented on the GPU path");
+  if (p->frag_olap_limit != UINT64_MAX)
+    return fail(OVL_ERR_UNSUPPORTED, "-l (frag olap limit) is not implemented on the GPU path");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(OVL_ERR_NO_DEVICE, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(OVL_ERR_NO_DEVICE, "bad device ordinal %d", device);
+  hipDeviceProp_t prop;
+  HIPC(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(OVL_ERR_NO_DEVICE, "device %d is %s, not gfx950", device, prop.gcnArchName);
+  HIPC(hipSetDevice(device));
+
+  ovl_ctx *c = new ovl_ctx();
+  c->P = *p;
+  ovl_params_finalize(&c->P);
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount;
+  memset(&c->stats, 0, sizeof(c->stats));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(OVL_ERR_HIP, "stream create failed");
+  }
+  for (int i = 0; i < 8; i++) (void)hipEventCreate(&c->ev[i]);
+
+  double er = c->P.max_erate;
+  c->max_errors = 1 + (int32_t)ceil(er * AS_MAX_READLEN);
+  c->branch_match_value = er / (1 + er);
+  c->min_branch_tail_slope = (er > 0.06) ? 1.0 : 0.20;
+  c->h_error_bound.resize(AS_MAX_READLEN + 1);
+  for (uint32_t i = 0; i <= AS_MAX_READLEN; i++)
+    c->h_error_bound[i] = (int32_t)ceil(i * er);
+  std::vector<int32_t> ml;
+  init_match_limit(ml, er, c->max_errors);
+  if (c->d_error_bound.alloc(AS_MAX_READLEN + 1) != hipSuccess ||
+      c->d_match_limit.alloc(ml.size()) != hipSuccess) {
+    ovl_ctx_destroy(c);
+    return fail(OVL_ERR_OOM, "table alloc");
+  }
+  (void)hipMemcpy(c->d_error_bound.p, c->h_error_bound.data(), 4ull * (AS_MAX_READLEN + 1),
+                  hipMemcpyHostToDevice);
+  (void)hipMemcpy(c->d_match_limit.p, ml.data(), 4ull * ml.size(), hipMemcpyHostToDevice);
+  *out = c;
+  return OVL_OK;
+}
+
+void ovl_ctx_destroy(ovl_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int i = 0; i < 8; i++)
+    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const uint8_t *d_bases,
+                       const uint64_t *d_offsets, const uint32_t *h_lengths) {
+  c->first_iid = first_iid;
+  c->nreads = nreads;
+  c->have_index = false;
+  c->h_len.assign(h_lengths, h_lengths + nreads);
+  c->h_wofs.resize(nreads + 1);
+  uint64_t w = 0;
+  c->max_len = 0;
+  for (uint32_t i = 0; i < nreads; i++) {
+    if (h_lengths[i] > AS_MAX_READLEN)
+      return fail(OVL_ERR_BAD_INPUT, "read %u longer than AS_MAX_READLEN", first_iid + i);
+    c->h_wofs[i] = w;
+    w += (h_lengths[i] + 31) / 32 + 1;
+    c->max_len = std::max(c->max_len, h_lengths[i]);
+  }
+  c->h_wofs[nreads] = w;
+  w += 2;
+  if (c->d_fwd.alloc(w) || c->d_rc.alloc(w) || c->d_fwdN.alloc(w) || c->d_rcNul.alloc(w) ||
+      c->d_wofs.alloc(nreads + 1) || c->d_len.alloc(nreads) || c->d_flags.alloc(nreads) ||
+      c->d_rcFirstNul.alloc(nreads))
+    return fail(OVL_ERR_OOM, "read buffers (%llu words)", (unsigned long long)w);
+  HIPC(hipMemsetAsync(c->d_fwd.p, 0, 8 * w, c->stream));
+  HIPC(hipMemsetAsync(c->d_rc.p, 0, 8 * w, c->stream));
+  HIPC(hipMemsetAsync(c->d_fwdN.p, 0, 4 * w, c->stream));
+  HIPC(hipMemsetAsync(c->d_rcNul.p, 0, 4 * w, c->stream));
+  HIPC(hipMemcpyAsync(c->d_wofs.p, c->h_wofs.data(), 8ull * (nreads + 1), hipMemcpyHostToDevice,
+                      c->stream));
+  HIPC(hipMemcpyAsync(c->d_len.p, h_lengths, 4ull * nreads, hipMemcpyHostToDevice, c->stream));
+  DBuf<uint32_t> err;
+  if (err.alloc(1)) return fail(OVL_ERR_OOM, "err flag");
+  HIPC(hipMemsetAsync(err.p, 0, 4, c->stream));
+  if (nreads)
+    hipLaunchKernelGGL(k_pack, dim3(nreads), dim3(128), 0, c->stream, d_bases, d_offsets,
+                       c->d_len.p, c->d_wofs.p, c->d_fwd.p, c->d_rc.p, c->d_fwdN.p,
+                       c->d_rcNul.p, c->d_flags.p, c->d_rcFirstNul.p, err.p,
+                       c->P.kmer_len);
+  HIPC(hipGetLastError());
+  uint32_t h_err = 0;
+  HIPC(hipMemcpyAsync(&h_err, err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (h_err)
+    return fail(OVL_ERR_BAD_INPUT,
+                "reads hold characters other than ACGTN; the GPU path cannot represent them");
+  return OVL_OK;
+}
+
+int ovl_load_reads(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const uint8_t *bases,
+                   const uint64_t *offsets, const uint32_t *lengths, const uint8_t *quals) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  (void)quals;
+  HIPC(hipSetDevice(c->device));
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nreads; i++) total = std::max(total, offsets[i] + lengths[i]);
+  DBuf<uint8_t> db;
+  DBuf<uint64_t> doff;
+  if (db.alloc(total + 64) || doff.alloc(nreads + 1)) return fail(OVL_ERR_OOM, "staging");
+  HIPC(hipMemcpyAsync(db.p, bases, total, hipMemcpyHostToDevice, c->stream));
+  HIPC(hipMemcpyAsync(doff.p, offsets, 8ull * nreads, hipMemcpyHostToDevice, c->stream));
+  int rc = load_common(c, first_iid, nreads, db.p, doff.p, lengths);
+  (void)hipStreamSynchronize(c->stream);
+  return rc;
+}
+
+int ovl_load_reads_device(ovl_ctx *c, uint32_t first_iid, uint32_t nreads,
+                          const uint8_t *d_bases, const uint64_t *d_offsets,
+                          const uint32_t *h_lengths, const uint8_t *d_quals) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  (void)d_quals;
+  HIPC(hipSetDevice(c->device));
+  return load_common(c, first_iid, nreads, d_bases, d_offsets, h_lengths);
+}
+
+static uint64_t kmer_code(const char *s, uint32_t k, bool *ok) {
+  uint64_t key = 0;
+  *ok = true;
+  for (uint32_t j = 0; j < k; j++) {
+    int v;
+    switch (s[j] | 0x20) {
+      case 'a': v = 0; break;
+      case 'c': v = 1; break;
+      case 'g': v = 2; break;
+      case 't': v = 3; break;
+      default: v = 0; *ok = false;
+    }
+    key |= (uint64_t)v << (2 * j);
+  }
+  return key;
+}
+
+int ovl_set_skip_kmers(ovl_ctx *c, const char *kmers, uint64_t n) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  uint32_t k = c->P.kmer_len;
+  c->h_skip.clear();
+  std::vector<char> rc(k);
+  for (uint64_t i = 0; i < n; i++) {
+    const char *s = kmers + i * k;
+    bool ok;
+    uint64_t f = kmer_code(s, k, &ok);
+    if (!ok) return fail(OVL_ERR_BAD_INPUT, "skip k-mer %llu is not ACGT", (unsigned long long)i);
+    c->h_skip.push_back(f);
+    uint64_t r = 0;                                // reverse complement code
+    for (uint32_t j = 0; j < k; j++) {
+      uint64_t b = (f >> (2 * j)) & 3;
+      r |= (3 - b) << (2 * (k - 1 - j));
+    }
+    c->h_skip.push_back(r);
+  }
+  std::sort(c->h_skip.begin(), c->h_skip.end());
+  c->h_skip.erase(std::unique(c->h_skip.begin(), c->h_skip.end()), c->h_skip.end());
+  c->have_index = false;
+  return OVL_OK;
+}
+
+static __global__ void k_clear_screen(uint32_t *flags, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] &= 1u;
+}
+
+static uint32_t ceil_log2(uint64_t x) {
+  uint32_t b = 0;
+  while ((1ull << b) < x) b++;
+  return b;
+}
+
+int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  uint32_t k = c->P.kmer_len;
+  if (bgn < 1) bgn = 1;
+  if (bgn < c->first_iid) bgn = c->first_iid;
+  uint32_t last = c->first_iid + c->nreads - 1;
+  if (end > last) end = last;
+  c->hash_bgn_iid = bgn;
+  c->hash_end_iid = end;
+  c->have_index = false;
+  HIPC(hipEventRecord(c->ev[0], s));
+  hipLaunchKernelGGL(k_clear_screen, dim3((c->nreads + 255) / 256), dim3(256), 0, s,
+                     c->d_flags.p, c->nreads);
+
+  uint32_t h0 = bgn - c->first_iid, h1 = (end >= bgn) ? end - c->first_iid + 1 : h0;
+  uint64_t P = 0;
+  for (uint32_t r = h0; r < h1; r++)
+    if ((int32_t)c->h_len[r] >= c->P.min_olap_len && c->h_len[r] >= k)
+      P += c->h_len[r] - k + 1;
+  uint32_t n_skip = (uint32_t)c->h_skip.size();
+  P += n_skip;
+  if (P >= 0xFFFFFFF0ull)
+    return fail(OVL_ERR_UNSUPPORTED, "hash batch with %llu k-mers; use a smaller -h range",
+                (unsigned long long)P);
+  if (n_skip) {
+    if (c->d_skip.alloc(n_skip)) return fail(OVL_ERR_OOM, "skip");
+    HIPC(hipMemcpyAsync(c->d_skip.p, c->h_skip.data(), 8ull * n_skip, hipMemcpyHostToDevice, s));
+  }
+
+  uint32_t cb = std::min<uint32_t>(12, std::max<uint32_t>(4, ceil_log2(P / 2048 + 1)));
+  uint64_t per_cb = (P >> cb) + 1;
+  uint32_t fb = std::min<uint32_t>(11, ceil_log2((per_cb + 255) / 256));
+  uint32_t ncb = 1u << cb, nfb = 1u << fb, nfine = ncb * nfb;
+
+  if (c->d_tmpM.alloc(P) || c->d_tmpP.alloc(P) || c->d_tmpM2.alloc(P) || c->d_occ.alloc(P))
+    return fail(OVL_ERR_OOM, "index records (%llu)", (unsigned long long)P);
+  DBuf<uint32_t> hist, cstart, cursor, fstart, fcnt, misc, big;
+  if (hist.alloc(ncb) || cstart.alloc(ncb) || cursor.alloc(ncb) || fstart.alloc(nfine) ||
+      fcnt.alloc(nfine) || misc.alloc(8) || big.alloc(2 * (size_t)nfine))
+    return fail(OVL_ERR_OOM, "index scratch");
+  HIPC(hipMemsetAsync(hist.p, 0, 4 * ncb, s));
+  HIPC(hipMemsetAsync(misc.p, 0, 32, s));
+
+  BuildArgs A;
+  A.R = c->reads();
+  A.h0 = h0;
+  A.h1 = h1;
+  uint32_t nblk = std::max<uint32_t>(1, std::min<uint32_t>(h1 - h0, 4u * c->n_cu));
+  A.reads_per_block = (h1 - h0 + nblk - 1) / nblk;
+  if (A.reads_per_block == 0) A.reads_per_block = 1;
+  A.k = k;
+  A.min_len = c->P.min_olap_len;
+  A.kmask = (1ull << (2 * k)) - 1;
+  A.skip = n_skip ? c->d_skip.p : nullptr;
+  A.n_skip = n_skip;
+  A.cb_bits = cb;
+  A.fb_bits = fb;
+  hipLaunchKernelGGL(k_coarse_hist, dim3(nblk), dim3(256), 0, s, A, hist.p);
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, hist.p, cstart.p, ncb, misc.p + 0);
+  HIPC(hipMemcpyAsync(cursor.p, cstart.p, 4 * ncb, hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(k_coarse_scatter, dim3(nblk), dim3(256), 0, s, A, cursor.p, c->d_tmpM.p,
+                     c->d_tmpP.p);
+  FineArgs F;
+  F.inM = c->d_tmpM.p;
+  F.inP = c->d_tmpP.p;
+  F.outM = c->d_tmpM2.p;
+  F.outP = c->d_occ.p;
+  F.cstart = cstart.p;
+  F.ccnt = hist.p;
+  F.fstart = fstart.p;
+  F.fcnt = fcnt.p;
+  F.big_list = big.p;
+  F.big_n = misc.p + 1;
+  F.max_distinct = misc.p + 2;
+  F.cb_bits = cb;
+  F.fb_bits = fb;
+  hipLaunchKernelGGL(k_fine, dim3(ncb), dim3(OVL_FINE_WAVES * 64), 0, s, F);
+  HIPC(hipGetLastError());
+  uint32_t hm[4];
+  HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  // P counted every window; windows holding an 'n' are not hashed (key_is_bad)
+  if (hm[0] > P) return fail(OVL_ERR_HIP, "index count %u exceeds bound %llu", hm[0],
+                             (unsigned long long)P);
+  uint32_t nbig = hm[1];
+  if (nbig) {
+    std::vector<uint32_t> bl(2 * nbig);
+    HIPC(hipMemcpy(bl.data(), big.p, 8ull * nbig, hipMemcpyDeviceToHost));
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < nbig; i++) mx = std::max(mx, bl[2 * i + 1]);
+    uint32_t n2 = 1;
+    while (n2 < mx) n2 <<= 1;
+    DBuf<uint64_t> sM, sP;
+    if (sM.alloc((size_t)n2 * nbig) || sP.alloc((size_t)n2 * nbig))
+      return fail(OVL_ERR_OOM, "big fine buckets");
+    hipLaunchKernelGGL(k_fine_big, dim3(nbig), dim3(1024), 0, s, c->d_tmpM2.p, c->d_occ.p,
+                       big.p, sM.p, sP.p, n2, misc.p + 2);
+    HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  }
+  uint32_t maxd = std::max<uint32_t>(hm[2], 1);
+  c->slice_bits = std::max<uint32_t>(1, ceil_log2(2ull * maxd));
+  c->tab_bits = cb + fb + c->slice_bits;
+  if (c->d_tab.alloc(1ull << c->tab_bits)) return fail(OVL_ERR_OOM, "table 2^%u", c->tab_bits);
+  TableArgs T;
+  T.M = c->d_tmpM2.p;
+  T.P = c->d_occ.p;
+  T.fstart = fstart.p;
+  T.fcnt = fcnt.p;
+  T.tab = c->d_tab.p;
+  T.nfine = nfine;
+  T.slice_bits = c->slice_bits;
+  T.tab_bits = c->tab_bits;
+  T.len = c->d_len.p;
+  T.rflags = c->d_flags.p;
+  T.first_iid = c->first_iid;
+  T.k = k;
+  uint32_t S = 1u << c->slice_bits;
+  uint32_t wpb = std::max<uint32_t>(1, std::min<uint32_t>(4, 65536u / (16u * S)));
+  size_t lds = (size_t)wpb * 16u * S;
+  if (lds > 65536) return fail(OVL_ERR_UNSUPPORTED, "k-mer slice too large (%u)", S);
+  hipLaunchKernelGGL(k_table, dim3((nfine + wpb - 1) / wpb), dim3(64 * wpb), lds, s, T);
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(c->ev[1], s));
+  HIPC(hipStreamSynchronize(s));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+  c->stats.ms_index = ms;
+  c->d_tmpM.release();
+  c->d_tmpP.release();
+  c->have_index = true;
+  return OVL_OK;
+}
+
+IndexDev index_dev(const ovl_ctx *c) {
+  IndexDev X;
+  X.tab = c->d_tab.p;
+  X.occ = c->d_occ.p;
+  X.tab_bits = c->tab_bits;
+  X.slice_bits = c->slice_bits;
+  X.k = c->P.kmer_len;
+  X.kmask = (1ull << (2 * c->P.kmer_len)) - 1;
+  return X;
+}
+
+int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  if (!c->have_index) return fail(OVL_ERR_STATE, "ovl_build_hash_index() first");
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const uint32_t k = c->P.kmer_len;
+  if (bgn < 1) bgn = 1;
+  if (bgn < c->first_iid) bgn = c->first_iid;
+  uint32_t last = c->first_iid + c->nreads - 1;
+  if (end > last) end = last;
+
+  // units: (query, FORWARD), (query, REVERSE) -- Process_Overlaps.C:124-128
+  std::vector<Unit> units;
+  std::vector<uint64_t> uwin;
+  for (uint32_t a = bgn; a <= end && a >= bgn; a++) {
+    uint32_t r = a - c->first_iid;
+    int32_t L = (int32_t)c->h_len[r];
+    if (L < c->P.min_olap_len || L < (int32_t)k) continue;
+    if (a >= c->hash_end_iid) continue;          // no hash read with a larger ID
+    units.push_back(Unit{r, 0});
+    units.push_back(Unit{r, 1});
+    uwin.push_back((uint64_t)(L - (int32_t)k + 1));
+    uwin.push_back((uint64_t)(L - (int32_t)k + 1));
+  }
+  ovl_stats keep_idx = c->stats;
+  memset(&c->stats, 0, sizeof(c->stats));
+  c->stats.ms_index = keep_idx.ms_index;
+  c->nout = 0;
+
+  // per-context device buffers, sized per batch
+  const uint64_t WIN_BUDGET = 192ull << 20;     // probe slots per batch (8 B each)
+  const uint64_t HIT_BUDGET = 320ull << 20;     // seed hits per batch
+  DBuf<Unit> d_units;
+  DBuf<uint64_t> d_rbase;
+  DBuf<Probe> d_probe;
+  DBuf<uint32_t> d_uhits, d_uflags, d_ctr, d_done;
+  DBuf<Node> d_pool, d_pnodes;
+  DBuf<PairRec> d_pairs;
+  DBuf<unsigned long long> d_stats;
+  if (d_ctr.alloc(16) || d_stats.alloc(8)) return fail(OVL_ERR_OOM, "counters");
+  HIPC(hipMemsetAsync(d_stats.p, 0, 64, s));
+
+  // extension scratch per wave
+  int32_t e_cap = c->h_error_bound[std::min<uint32_t>(c->max_len, AS_MAX_READLEN)] + 2;
+  uint64_t rows_cap = (uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64;
+  uint64_t per_wave = rows_cap * 4 + 8ull * (e_cap + 2) + 16ull * (e_cap + 8);
+  uint32_t ext_waves = 16u * c->n_cu;
+  uint64_t budget = 24ull << 30;
+  while (ext_waves > 256 && (uint64_t)ext_waves * per_wave > budget) ext_waves /= 2;
+  DBuf<int32_t> d_rows, d_rowdir, d_deltas;
+  if (d_rows.alloc(rows_cap * ext_waves) ||
+      d_rowdir.alloc((size_t)2 * (e_cap + 2) * ext_waves) ||
+      d_deltas.alloc((size_t)4 * (e_cap + 8) * ext_waves))
+    return fail(OVL_ERR_OOM, "extension scratch");
+  uint32_t chain_waves = 8u * c->n_cu;
+  const uint32_t DONE_CAP = 4096;
+  if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");
+
+  size_t out_cap = std::max<size_t>(1u << 20, units.size() * 8);
+  if (c->d_out.alloc(out_cap)) return fail(OVL_ERR_OOM, "output");
+
+  float ms_probe = 0, ms_chain = 0, ms_ext = 0;
+  uint64_t seed_hits = 0, npairs_tot = 0, probe_bytes = 0;
+  uint32_t nu = (uint32_t)units.size();
+  uint32_t u0 = 0;
+  while (u0 < nu) {
+    // batch by probe slots
+    uint32_t u1 = u0;
+    uint64_t wsum = 0;
+    while (u1 < nu && (wsum + uwin[u1] <= WIN_BUDGET || u1 == u0)) wsum += uwin[u1++];
+    uint32_t nb = u1 - u0;
+    std::vector<uint64_t> rbase(nb + 1);
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < nb; i++) { rbase[i] = acc; acc += uwin[u0 + i]; }
+    rbase[nb] = acc;
+    if (d_units.alloc(nb) || d_rbase.alloc(nb + 1) || d_probe.alloc(acc) ||
+        d_uhits.alloc(nb) || d_uflags.alloc(nb))
+      return fail(OVL_ERR_OOM, "probe buffers");
+    HIPC(hipMemcpyAsync(d_units.p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(d_rbase.p, rbase.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
+    ProbeArgs PA;
+    PA.R = c->reads();
+    PA.X = index_dev(c);
+    PA.units = d_units.p;
+    PA.rbase = d_rbase.p;
+    PA.nunits = nb;
+    PA.out = d_probe.p;
+    PA.unit_hits = d_uhits.p;
+    PA.unit_flags = d_uflags.p;
+    PA.k = k;
+    HIPC(hipEventRecord(c->ev[2], s));
+    hipLaunchKernelGGL(k_probe, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev[3], s));
+    std::vector<uint32_t> uh(nb);
+    HIPC(hipMemcpyAsync(uh.data(), d_uhits.p, 4ull * nb, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+    ms_probe += t;
+    probe_bytes += acc * 8;                          // see DESIGN.md for the full count
+    // shrink the batch to the hit budget (probe results stay valid for the prefix)
+    uint64_t hsum = 0;
+    uint32_t nc = 0;
+    while (nc < nb && (hsum + uh[nc] <= HIT_BUDGET || nc == 0)) hsum += uh[nc++];
+    seed_hits += hsum;
+
+    uint64_t pool_cap = hsum + (hsum / 4000 + chain_waves + 2) * (uint64_t)OVL_NODE_BLOCK + 8;
+    uint64_t pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * 256 + 1024);
+    if (pool_cap >= 0xFFFFFFF0ull) return fail(OVL_ERR_UNSUPPORTED, "node pool too large");
+    if (d_pool.alloc(pool_cap) || d_pnodes.alloc(hsum + 1) || d_pairs.alloc(pairs_cap))
+      return fail(OVL_ERR_OOM, "chain buffers (%llu hits)", (unsigned long long)hsum);
+    uint32_t ctr_init[16] = {0};
+    ctr_init[1] = 1;                                 // pool_next: node 0 is null
+    HIPC(hipMemcpyAsync(d_ctr.p, ctr_init, 64, hipMemcpyHostToDevice, s));
+    ChainArgs CA;
+    CA.R = c->reads();
+    CA.occ = c->d_occ.p;
+    CA.units = d_units.p;
+    CA.rbase = d_rbase.p;
+    CA.probes = d_probe.p;
+    CA.unit_flags = d_uflags.p;
+    CA.nunits = nc;
+    CA.k = k;
+    CA.unit_next = d_ctr.p + 0;
+    CA.pool = d_pool.p;
+    CA.pool_next = d_ctr.p + 1;
+    CA.pool_cap = (uint32_t)pool_cap;
+    CA.pnodes = d_pnodes.p;
+    CA.pnodes_next = d_ctr.p + 2;
+    CA.pnodes_cap = (uint32_t)(hsum + 1);
+    CA.pairs = d_pairs.p;
+    CA.npairs = d_ctr.p + 3;
+    CA.pairs_cap = (uint32_t)pairs_cap;
+    CA.overflow = d_ctr.p + 4;
+    CA.done_scratch = d_done.p;
+    CA.done_cap = DONE_CAP;
+    HIPC(hipEventRecord(c->ev[4], s));
+    hipLaunchKernelGGL(k_chain, dim3(chain_waves / 4), dim3(256), 0, s, CA);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev[5], s));
+    uint32_t hc[16];
+    HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    (void)hipEventElapsedTime(&t, c->ev[4], c->ev[5]);
+    ms_chain += t;
+    if (hc[4]) return fail(OVL_ERR_OOM, "chain capacity exceeded (flags %u)", hc[4]);
+    uint32_t npairs = hc[3];
+    npairs_tot += npairs;
+
+    ExtendArgs EA;
+    EA.R = c->reads();
+    EA.units = d_units.p;
+    EA.pairs = d_pairs.p;
+    EA.npairs = npairs;
+    EA.pnodes = d_pnodes.p;
+    EA.pair_next = d_ctr.p + 5;
+    EA.error_bound = c->d_error_bound.p;
+    EA.match_limit = c->d_match_limit.p;
+    EA.max_errors = c->max_errors;
+    EA.branch_match_value = c->branch_match_value;
+    EA.min_branch_tail_slope = c->min_branch_tail_slope;
+    EA.min_branch_end_dist = 20;
+    EA.partial = c->P.partial;
+    EA.unique = c->P.unique_olap_per_pair;
+    EA.min_olap_len = c->P.min_olap_len;
+    EA.use_hopeless = c->P.use_hopeless_check;
+    EA.k = (int32_t)k;
+    EA.filter_by_kmer_count = c->P.filter_by_kmer_count;
+    EA.minkmer_exp = exp(-1.0 * (double)k * c->P.max_erate);
+    EA.rows = d_rows.p;
+    EA.rows_cap = rows_cap;
+    EA.rowdir = d_rowdir.p;
+    EA.deltas = d_deltas.p;
+    EA.e_cap = e_cap;
+    // output capacity: grow if this batch could exceed it (<= 3 records per pair)
+    uint64_t need = c->nout + 3ull * npairs;
+    if (need > c->d_out.n) {
+      DBuf<Rec> bigger;
+      if (bigger.alloc(need + (need >> 2))) return fail(OVL_ERR_OOM, "output grow");
+      if (c->nout)
+        HIPC(hipMemcpyAsync(bigger.p, c->d_out.p, sizeof(Rec) * c->nout, hipMemcpyDeviceToDevice, s));
+      HIPC(hipStreamSynchronize(s));
+      std::swap(bigger.p, c->d_out.p);
+      std::swap(bigger.n, c->d_out.n);
+    }
+    uint32_t nout32 = (uint32_t)c->nout;
+    HIPC(hipMemcpyAsync(d_ctr.p + 6, &nout32, 4, hipMemcpyHostToDevice, s));
+    EA.out = c->d_out.p;
+    EA.nout = d_ctr.p + 6;
+    EA.out_cap = (uint32_t)std::min<uint64_t>(c->d_out.n, 0xFFFFFFF0ull);
+    EA.stats = d_stats.p;
+    EA.overflow = d_ctr.p + 7;
+    HIPC(hipEventRecord(c->ev[6], s));
+    if (npairs)
+      hipLaunchKernelGGL(k_extend, dim3(ext_waves / 4), dim3(256), 0, s, EA);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev[7], s));
+    HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    (void)hipEventElapsedTime(&t, c->ev[6], c->ev[7]);
+    ms_ext += t;
+    if (hc[7]) return fail(OVL_ERR_OOM, "extension capacity exceeded (flags %u)", hc[7]);
+    c->nout = hc[6];
+    u0 += nc;
+  }
+  unsigned long long hs[8];
+  HIPC(hipMemcpy(hs, d_stats.p, 64, hipMemcpyDeviceToHost));
+  c->stats.kmer_hits_without_olap = hs[0];
+  c->stats.kmer_hits_with_olap = hs[1];
+  c->stats.kmer_hits_skipped = hs[2];
+  c->stats.multi_overlaps = hs[3];
+  c->stats.total_overlaps = hs[4];
+  c->stats.contained_overlaps = hs[5];
+  c->stats.dovetail_overlaps = hs[6];
+  c->stats.seed_hits = seed_hits;
+  c->stats.pairs = npairs_tot;
+  c->stats.ms_seed = ms_probe + ms_chain;
+  c->stats.ms_extend = ms_ext;
+  c->stats.ms_probe_kernel = ms_probe;
+  c->stats.probe_bytes = probe_bytes;
+  *n_out = c->nout;
+  return OVL_OK;
+}
+
+int ovl_fetch_overlaps(ovl_ctx *c, ovl_record *out, uint64_t max_records, uint64_t *n_copied) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  HIPC(hipSetDevice(c->device));
+  std::vector<Rec> h(c->nout);
+  if (c->nout)
+    HIPC(hipMemcpy(h.data(), c->d_out.p, sizeof(Rec) * c->nout, hipMemcpyDeviceToHost));
+  std::sort(h.begin(), h.end(), [](const Rec &x, const Rec &y) {
+    if (x.a_iid != y.a_iid) return x.a_iid < y.a_iid;
+    if (x.b_iid != y.b_iid) return x.b_iid < y.b_iid;
+    if (x.w0 != y.w0) return x.w0 < y.w0;
+    return x.w1 < y.w1;
+  });
+  uint64_t n = std::min<uint64_t>(max_records, h.size());
+  for (uint64_t i = 0; i < n; i++) {
+    out[i].a_iid = h[i].a_iid;
+    out[i].b_iid = h[i].b_iid;
+    out[i].dat[0] = h[i].w0;
+    out[i].dat[1] = h[i].w1;
+  }
+  *n_copied = n;
+  return OVL_OK;
+}
+
+int ovl_get_stats(ovl_ctx *c, ovl_stats *out) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  *out = c->stats;
+  return OVL_OK;
+}
+
+}  // extern "C"

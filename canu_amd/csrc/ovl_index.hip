@@ -1,0 +1,427 @@
+// ovl_index.hip -- read packing and the k-mer index (Build_Hash_Index replacement).
+//
+// Reference: src/overlapInCore/overlapInCore-Build_Hash_Index.C
+//   Put_String_In_Hash (:360)  every window of k ACGT bases is an occurrence
+//   Hash_Insert        (:296)  occurrences of one k-mer are chained newest-first
+//   Mark_Skip_Kmers    (:235)  -k file k-mers become Empty entries; their occurrences
+//                              mark the reads' screened ends (Mark_Screened_Ends_Single)
+//
+// MI355X design: instead of a CPU bucket table filled one insert at a time, the index is a
+// two-level bucket sort of (mix(kmer), position) records:
+//   coarse pass  : 4096 buckets by the top 12 bits of mix(kmer); per-block LDS histograms,
+//                  one global atomic per (block, bucket) to claim space
+//   fine pass    : one workgroup per coarse bucket splits it into 2^FB fine buckets in LDS,
+//                  then each wave sorts one fine bucket in LDS (bitonic, by mix asc /
+//                  position desc = the reference's chain order)
+//   table pass   : each wave turns one sorted fine bucket into one slice of an open-
+//                  addressing table (16-B entries, the slice is the fine bucket's own range
+//                  of the table, so no two workgroups ever touch the same slots)
+// The occurrence array is the sorted position array itself.
+#include "ovl_common.h"
+
+namespace ovl {
+
+// ---------------------------------------------------------------------------------------
+// Packing: ASCII reads -> 2-bit strands + exception masks.  One block per read.
+// Accepts acgtn / ACGTN; anything else sets *err (the GPU path cannot represent it).
+__device__ __forceinline__ int base_code(uint8_t c, int *is_n, int *bad) {
+  switch (c | 0x20) {
+    case 'a': return 0;
+    case 'c': return 1;
+    case 'g': return 2;
+    case 't': return 3;
+    case 'n': *is_n = 1; return 0;
+    default:  *bad = 1; return 0;
+  }
+}
+
+__global__ void k_pack(const uint8_t *__restrict__ bases, const uint64_t *__restrict__ offs,
+                       const uint32_t *__restrict__ lens, const uint64_t *__restrict__ wofs,
+                       uint64_t *fwd, uint64_t *rc, uint32_t *fwdN, uint32_t *rcNul,
+                       uint32_t *flags, uint32_t *rcFirstNul, uint32_t *err, uint32_t k) {
+  uint32_t r = blockIdx.x;
+  uint32_t L = lens[r];
+  uint64_t o = offs[r], w0 = wofs[r];
+  uint32_t nw = (L + 31) / 32 + 1;        // + guard word
+  __shared__ int s_hasn;
+  __shared__ int s_lastn;
+  if (threadIdx.x == 0) { s_hasn = 0; s_lastn = -1; }
+  __syncthreads();
+  int bad = 0, anyn = 0, lastn = -1;
+  for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+    uint64_t f = 0, c = 0;
+    uint32_t fn = 0, cn = 0;
+    for (uint32_t i = 0; i < 32; i++) {
+      uint32_t p = w * 32 + i;
+      if (p < L) {
+        int isn = 0;
+        int code = base_code(bases[o + p], &isn, &bad);
+        f |= (uint64_t)code << (2 * i);
+        if (isn) {
+          fn |= 1u << i;
+          anyn = 1;
+          // only NULs at rc positions >= k can end the window scan (see below)
+          if (p + k <= L - 1 && (int)p > lastn) lastn = (int)p;
+        }
+      }
+      // rc base at position p comes from fwd base L-1-p
+      if (p < L) {
+        int isn2 = 0;
+        int code2 = base_code(bases[o + (L - 1 - p)], &isn2, &bad);
+        if (isn2) cn |= 1u << i;          // complement of 'n' is NUL
+        else      c |= (uint64_t)(3 - code2) << (2 * i);
+      }
+    }
+    fwd[w0 + w] = f;
+    rc[w0 + w] = c;
+    fwdN[w0 + w] = fn;
+    rcNul[w0 + w] = cn;
+  }
+  if (bad) atomicOr(err, 1u);
+  if (anyn) atomicOr(&s_hasn, 1);
+  if (lastn >= 0) atomicMax(&s_lastn, lastn);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flags[r] = s_hasn ? 1u : 0u;
+    // Find_Overlaps.C:341 tests `*P` only for the last base of windows 1, 2, ..., so a
+    // NUL ends the scan only from rc position k on: the first such NUL is the rc image of
+    // the last forward 'n' at or before L-1-k.
+    rcFirstNul[r] = (s_lastn >= 0) ? (L - 1 - (uint32_t)s_lastn) : L;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Index build
+
+struct BuildArgs {
+  ReadsDev R;
+  uint32_t h0, h1;           // local read range [h0, h1) of hash reads
+  uint32_t reads_per_block;
+  uint32_t k;
+  int32_t  min_len;          // G.Min_Olap_Len: shorter reads are not hashed
+  uint64_t kmask;
+  const uint64_t *skip;      // skip k-mers (both strands), may be null
+  uint32_t n_skip;
+  uint32_t cb_bits;          // coarse bucket bits
+  uint32_t fb_bits;          // fine bucket bits
+};
+
+#define OVL_CB_MAX 4096
+#define OVL_SKIP_POS 0xFFFFFFFFFFFFFFFFull
+
+template <typename F>
+__device__ __forceinline__ void for_block_windows(const BuildArgs &A, F &&fn) {
+  uint32_t rb = A.h0 + blockIdx.x * A.reads_per_block;
+  uint32_t re = rb + A.reads_per_block;
+  if (re > A.h1) re = A.h1;
+  for (uint32_t r = rb; r < re; r++) {
+    int32_t L = (int32_t)A.R.len[r];
+    if (L < A.min_len || L < (int32_t)A.k) continue;
+    uint64_t wo = A.R.wofs[r];
+    const uint64_t *w = A.R.fwd + wo;
+    const uint32_t *nm = (A.R.flags[r] & 1u) ? A.R.fwdN + wo : nullptr;
+    uint64_t iid = A.R.first_iid + r;
+    uint32_t kbits = (1u << A.k) - 1u;   // k <= 31
+    for (int32_t p = threadIdx.x; p + (int32_t)A.k <= L; p += blockDim.x) {
+      if (nm && (mask_at(nm, p) & kbits)) continue;          // key_is_bad
+      uint64_t kmer = bases_at(w, p) & A.kmask;
+      fn(kmer, (iid << 32) | (uint32_t)p);
+    }
+  }
+  // skip k-mers ride along as marker records, spread over the blocks
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n_skip;
+       i += gridDim.x * blockDim.x)
+    fn(A.skip[i], OVL_SKIP_POS);
+}
+
+__global__ void k_coarse_hist(BuildArgs A, uint32_t *hist) {
+  __shared__ uint32_t h[OVL_CB_MAX];
+  uint32_t nb = 1u << A.cb_bits;
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for_block_windows(A, [&](uint64_t kmer, uint64_t) {
+    atomicAdd(&h[mix64(kmer) >> (64 - A.cb_bits)], 1u);
+  });
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+__global__ void k_coarse_scatter(BuildArgs A, uint32_t *cursor, uint64_t *outM,
+                                 uint64_t *outP) {
+  __shared__ uint32_t h[OVL_CB_MAX];
+  __shared__ uint32_t base[OVL_CB_MAX];
+  uint32_t nb = 1u << A.cb_bits;
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for_block_windows(A, [&](uint64_t kmer, uint64_t) {
+    atomicAdd(&h[mix64(kmer) >> (64 - A.cb_bits)], 1u);
+  });
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+    base[i] = h[i] ? atomicAdd(&cursor[i], h[i]) : 0u;
+    h[i] = 0;
+  }
+  __syncthreads();
+  for_block_windows(A, [&](uint64_t kmer, uint64_t pos) {
+    uint64_t M = mix64(kmer);
+    uint32_t b = (uint32_t)(M >> (64 - A.cb_bits));
+    uint32_t slot = base[b] + atomicAdd(&h[b], 1u);
+    outM[slot] = M;
+    outP[slot] = pos;
+  });
+}
+
+// Sort order: M ascending, then position descending (chain order).
+__device__ __forceinline__ bool rec_less(uint64_t m1, uint64_t p1, uint64_t m2, uint64_t p2) {
+  return (m1 < m2) || (m1 == m2 && p1 > p2);
+}
+
+// Wave-level bitonic sort of n2 (power of 2) records in LDS.
+__device__ void wave_bitonic(uint64_t *sM, uint64_t *sP, uint32_t n2, uint32_t lane) {
+  for (uint32_t size = 2; size <= n2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = lane; t < n2 / 2; t += OVL_WAVE) {
+        uint32_t i = 2 * t - (t & (stride - 1));
+        uint32_t j = i + stride;
+        bool up = ((i & size) == 0);
+        uint64_t mi = sM[i], pi = sP[i], mj = sM[j], pj = sP[j];
+        bool sw = up ? rec_less(mj, pj, mi, pi) : rec_less(mi, pi, mj, pj);
+        if (sw) { sM[i] = mj; sP[i] = pj; sM[j] = mi; sP[j] = pi; }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+  }
+}
+
+#define OVL_FINE_WAVES  8
+#define OVL_FINE_CAP    1024      // records a wave sorts in LDS (16 KB)
+#define OVL_FB_MAX      4096
+
+struct FineArgs {
+  const uint64_t *inM, *inP;     // coarse-bucketed records
+  uint64_t *outM, *outP;         // fine-bucketed, sorted records
+  const uint32_t *cstart;        // coarse bucket start (exclusive scan of hist)
+  const uint32_t *ccnt;          // coarse bucket counts
+  uint32_t *fstart, *fcnt;       // fine bucket start / count (global index)
+  uint32_t *big_list, *big_n;    // fine buckets too large for LDS
+  uint32_t *max_distinct;
+  uint32_t cb_bits, fb_bits;
+};
+
+__global__ void __launch_bounds__(OVL_FINE_WAVES * 64)
+k_fine(FineArgs A) {
+  __shared__ uint32_t h[OVL_FB_MAX];
+  __shared__ uint32_t cur[OVL_FB_MAX];
+  __shared__ uint64_t sM[OVL_FINE_WAVES][OVL_FINE_CAP];
+  __shared__ uint64_t sP[OVL_FINE_WAVES][OVL_FINE_CAP];
+  uint32_t cb = blockIdx.x;
+  uint32_t nf = 1u << A.fb_bits;
+  uint32_t n = A.ccnt[cb], s0 = A.cstart[cb];
+  uint32_t shift = 64 - A.cb_bits - A.fb_bits;
+  for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    atomicAdd(&h[(uint32_t)(A.inM[s0 + i] >> shift) & (nf - 1)], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {                        // nf <= 4096: serial scan is cheap
+    uint32_t acc = 0;
+    for (uint32_t f = 0; f < nf; f++) { cur[f] = acc; acc += h[f]; }
+  }
+  __syncthreads();
+  for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) {
+    A.fstart[cb * nf + f] = s0 + cur[f];
+    A.fcnt[cb * nf + f] = h[f];
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    uint64_t M = A.inM[s0 + i];
+    uint32_t f = (uint32_t)(M >> shift) & (nf - 1);
+    uint32_t slot = atomicAdd(&cur[f], 1u);
+    A.outM[s0 + slot] = M;
+    A.outP[s0 + slot] = A.inP[s0 + i];
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t *wM = sM[wave], *wP = sP[wave];
+  for (uint32_t f = wave; f < nf; f += OVL_FINE_WAVES) {
+    uint32_t fn = h[f];
+    if (fn == 0) continue;
+    uint32_t fs = s0 + cur[f] - fn;              // cur[] now holds the fine bucket end
+    if (fn > OVL_FINE_CAP) {
+      if (lane == 0) {
+        uint32_t j = atomicAdd(A.big_n, 1u);
+        A.big_list[2 * j] = fs;
+        A.big_list[2 * j + 1] = fn;
+      }
+      continue;
+    }
+    uint32_t n2 = 1;
+    while (n2 < fn) n2 <<= 1;
+    for (uint32_t i = lane; i < n2; i += 64) {
+      if (i < fn) { wM[i] = A.outM[fs + i]; wP[i] = A.outP[fs + i]; }
+      else        { wM[i] = ~0ull;          wP[i] = 0; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (fn > 1) wave_bitonic(wM, wP, n2, lane);
+    uint32_t runs = 0;
+    for (uint32_t i = lane; i < fn; i += 64) {
+      A.outM[fs + i] = wM[i];
+      A.outP[fs + i] = wP[i];
+      runs += (i == 0 || wM[i] != wM[i - 1]) ? 1u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) runs += __shfl_xor(runs, o);
+    if (lane == 0) atomicMax(A.max_distinct, runs);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
+// Fine buckets larger than the LDS sort: one workgroup each, bitonic in global memory over
+// a power-of-two scratch copy.
+__global__ void k_fine_big(uint64_t *M, uint64_t *P, const uint32_t *big_list,
+                           uint64_t *scrM, uint64_t *scrP, uint32_t n2, uint32_t *max_distinct) {
+  uint32_t fs = big_list[2 * blockIdx.x], fn = big_list[2 * blockIdx.x + 1];
+  uint64_t *gM = scrM + (uint64_t)blockIdx.x * n2, *gP = scrP + (uint64_t)blockIdx.x * n2;
+  uint32_t m2 = 1;
+  while (m2 < fn) m2 <<= 1;
+  for (uint32_t i = threadIdx.x; i < m2; i += blockDim.x) {
+    if (i < fn) { gM[i] = M[fs + i]; gP[i] = P[fs + i]; }
+    else        { gM[i] = ~0ull;     gP[i] = 0; }
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (uint32_t size = 2; size <= m2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = threadIdx.x; t < m2 / 2; t += blockDim.x) {
+        uint32_t i = 2 * t - (t & (stride - 1));
+        uint32_t j = i + stride;
+        bool up = ((i & size) == 0);
+        uint64_t mi = gM[i], pi = gP[i], mj = gM[j], pj = gP[j];
+        bool sw = up ? rec_less(mj, pj, mi, pi) : rec_less(mi, pi, mj, pj);
+        if (sw) { gM[i] = mj; gP[i] = pj; gM[j] = mi; gP[j] = pi; }
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  __shared__ uint32_t s_runs;
+  if (threadIdx.x == 0) s_runs = 0;
+  __syncthreads();
+  uint32_t runs = 0;
+  for (uint32_t i = threadIdx.x; i < fn; i += blockDim.x) {
+    M[fs + i] = gM[i];
+    P[fs + i] = gP[i];
+    runs += (i == 0 || gM[i] != gM[i - 1]) ? 1u : 0u;
+  }
+  atomicAdd(&s_runs, runs);
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(max_distinct, s_runs);
+}
+
+struct TableArgs {
+  const uint64_t *M, *P;         // sorted records
+  const uint32_t *fstart, *fcnt;
+  TabEntry *tab;
+  uint32_t nfine;                // total fine buckets (2^(cb+fb))
+  uint32_t slice_bits;
+  uint32_t tab_bits;
+  // screened-end marking for skip k-mers (Mark_Screened_Ends_Single, :147)
+  const uint32_t *len;
+  uint32_t *rflags;              // bit1 lfrag_end_screened, bit2 rfrag_end_screened
+  uint32_t first_iid;
+  uint32_t k;
+};
+
+#define OVL_HOPELESS_MATCH 90
+
+// One wave per fine bucket -> one table slice.
+__global__ void __launch_bounds__(256) k_table(TableArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t f = blockIdx.x * (blockDim.x >> 6) + wave;
+  uint32_t S = 1u << A.slice_bits;
+  uint64_t *key = (uint64_t *)smem + (size_t)wave * S * 2;     // S keys then S (off,cnt)
+  uint32_t *oc = (uint32_t *)(key + S);
+  if (f >= A.nfine) return;
+  for (uint32_t i = lane; i < S; i += 64) { key[i] = 0; oc[2 * i] = 0; oc[2 * i + 1] = 0; }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t fs = A.fstart[f], fn = A.fcnt[f];
+  uint32_t pshift = 64 - A.tab_bits;
+  for (uint32_t i0 = 0; i0 < fn; i0 += 64) {
+    uint32_t i = i0 + lane;
+    bool start = false;
+    uint64_t M = 0;
+    if (i < fn) {
+      M = A.M[fs + i];
+      start = (i == 0) || (A.M[fs + i - 1] != M);
+    }
+    if (start) {
+      uint32_t e = i + 1;                      // run end
+      while (e < fn && A.M[fs + e] == M) e++;
+      uint32_t off = fs + i, cnt = e - i, flags = 0;
+      if (A.P[off] == OVL_SKIP_POS) {          // marker sorts first (position descending)
+        flags = OVL_FLAG_SKIP;
+        off++; cnt--;
+        for (uint32_t j = off; j < off + cnt; j++) {
+          uint64_t pos = A.P[j];
+          if (pos == OVL_SKIP_POS) continue;
+          uint32_t r = (uint32_t)(pos >> 32) - A.first_iid, o = (uint32_t)pos;
+          uint32_t bits = 0;
+          if (o < OVL_HOPELESS_MATCH) bits |= 2u;
+          if ((int64_t)A.len[r] - o - A.k + 1 < OVL_HOPELESS_MATCH) bits |= 4u;
+          if (bits) atomicOr(&A.rflags[r], bits);
+        }
+        while (cnt > 0 && A.P[off] == OVL_SKIP_POS) { off++; cnt--; }   // duplicate markers
+      }
+      uint32_t slot = (uint32_t)(M >> pshift) & (S - 1);
+      for (;;) {
+        uint32_t old = atomicCAS(&oc[2 * slot + 1], 0u, (cnt | flags | OVL_PRESENT));
+        if (old == 0) break;
+        slot = (slot + 1) & (S - 1);
+      }
+      key[slot] = M;
+      oc[2 * slot] = off;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  TabEntry *dst = A.tab + ((size_t)f << A.slice_bits);
+  for (uint32_t i = lane; i < S; i += 64) {
+    TabEntry e;
+    e.key = key[i];
+    e.off = oc[2 * i];
+    e.cnt = oc[2 * i + 1];
+    dst[i] = e;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Small utilities
+
+// Single-block exclusive scan, u32 in -> u32 out, any n.  Also writes the total.
+__global__ void k_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *total) {
+  __shared__ uint32_t part[1024];
+  uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+  uint32_t b = threadIdx.x * per, e = b + per;
+  if (e > n) e = n;
+  uint32_t s = 0;
+  for (uint32_t i = b; i < e; i++) s += in[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < blockDim.x; i++) { uint32_t v = part[i]; part[i] = acc; acc += v; }
+    if (total) *total = acc;
+  }
+  __syncthreads();
+  uint32_t acc = part[threadIdx.x];
+  for (uint32_t i = b; i < e; i++) { uint32_t v = in[i]; out[i] = acc; acc += v; }
+}
+
+}  // namespace ovl

@@ -1,0 +1,435 @@
+// ovl_seed.hip -- seed lookup and match chaining (Find_Overlaps replacement).
+//
+// Reference: src/overlapInCore/overlapInCore-Find_Overlaps.C
+//   Find_Overlaps (:284)  every k-window of the query (FORWARD, then its reverse
+//                          complement) is looked up; each occurrence in a read with a
+//                          larger ID than the query is passed to Add_Ref
+//   Add_Ref       (:158)  per-target bookkeeping (diag stats, consistent flag)
+//   Add_Match     (:79)   the ordered match list: extend the node whose next expected
+//                          window is this one on the same diagonal, else push a new node
+//
+// Two kernels:
+//   k_probe  one wave per (query, orientation) unit; lanes probe 64 windows at a time,
+//            write (list offset, qualifying count) per window -- the HBM-bound kernel
+//   k_chain  one wave per unit; per 64-window chunk the qualifying occurrences are staged
+//            in LDS (wave-level ordered compaction); every target read owns one lane, and
+//            that lane replays Add_Match for its target in reference order (window asc,
+//            chain order) -- all targets of the unit advance in parallel
+#include "ovl_common.h"
+
+namespace ovl {
+
+struct ProbeArgs {
+  ReadsDev R;
+  IndexDev X;
+  const Unit *units;
+  const uint64_t *rbase;        // per unit: first Probe slot
+  uint32_t nunits;
+  Probe *out;
+  uint32_t *unit_hits;          // per unit: qualifying occurrences
+  uint32_t *unit_flags;         // bit1 left_end_screened, bit2 right_end_screened
+  uint32_t k;
+};
+
+__device__ __forceinline__ uint32_t unit_windows(const ReadsDev &R, const Unit &u, uint32_t k) {
+  int32_t L = (int32_t)R.len[u.r];
+  int32_t lim = L;
+  if (u.dir) {
+    int32_t fn = (int32_t)R.rcFirstNul[u.r];
+    if (fn < lim) lim = fn;
+  }
+  // windows 0 .. lim-k; window 0 is always visited (it cannot match if it holds a NUL)
+  int32_t nw = lim - (int32_t)k + 1;
+  if (nw < 1) nw = 1;
+  return (uint32_t)nw;
+}
+
+// Number of leading entries of a descending occurrence list whose read iid > a.
+__device__ __forceinline__ uint32_t qualifying(const uint64_t *occ, uint32_t off, uint32_t cnt,
+                                               uint32_t a_iid) {
+  if (cnt <= 8) {
+    uint32_t q = 0;
+    while (q < cnt && (uint32_t)(occ[off + q] >> 32) > a_iid) q++;
+    return q;
+  }
+  uint32_t lo = 0, hi = cnt;           // first index with iid <= a
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(occ[off + mid] >> 32) > a_iid) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
+  uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t u = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (u >= A.nunits) return;
+  Unit un = A.units[u];
+  Strand S = un.dir ? strand_rc(A.R, un.r) : strand_fwd(A.R, un.r);
+  const uint32_t *bad = un.dir ? S.ex_nul : S.ex_wild;
+  uint32_t nw = unit_windows(A.R, un, A.k);
+  uint32_t a_iid = A.R.first_iid + un.r;
+  int32_t L = S.len;
+  uint32_t kbits = (1u << A.k) - 1u;
+  Probe *out = A.out + A.rbase[u];
+  uint32_t hits = 0, flags = 0;
+  for (uint32_t o = lane; o < nw; o += 64) {
+    Probe pr;
+    pr.off = 0;
+    pr.cnt = 0;
+    bool ok = (int32_t)(o + A.k) <= L;
+    if (ok && bad) ok = (mask_at(bad, (int32_t)o) & kbits) == 0;
+    if (ok) {
+      uint64_t kmer = bases_at(S.w, (int32_t)o) & A.X.kmask;
+      const TabEntry *e = index_find(A.X, kmer);
+      if (e) {
+        uint32_t c = e->cnt;
+        if (c & OVL_FLAG_SKIP) {
+          // Hash_Find found an Empty entry: hi_hits (Find_Overlaps.C:321-366)
+          if (o < 90) flags |= 2u;
+          if (o > 0 && L - (int32_t)o - (int32_t)A.k + 1 < 90) flags |= 4u;
+        } else {
+          pr.off = e->off;
+          pr.cnt = qualifying(A.X.occ, e->off, c & OVL_CNT_MASK, a_iid);
+          hits += pr.cnt;
+        }
+      }
+    }
+    out[o] = pr;
+  }
+  for (int s = 32; s > 0; s >>= 1) {
+    hits += __shfl_xor(hits, s);
+    flags |= __shfl_xor(flags, s);
+  }
+  if (lane == 0) {
+    A.unit_hits[u] = hits;
+    A.unit_flags[u] = flags;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+
+#define OVL_HCAP   1024          // staged occurrences per wave
+#define OVL_MAXT   128           // targets per pass (2 per lane)
+#define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
+
+struct ChainArgs {
+  ReadsDev R;
+  const uint64_t *occ;
+  const Unit *units;
+  const uint64_t *rbase;
+  const Probe *probes;
+  const uint32_t *unit_flags;
+  uint32_t nunits;
+  uint32_t k;
+  uint32_t *unit_next;          // work counter
+  Node *pool;                   // working node pool (index 0 = null)
+  uint32_t *pool_next;          // bump (starts at 1)
+  uint32_t pool_cap;
+  Node *pnodes;                 // per-pair node arrays, list order
+  uint32_t *pnodes_next;
+  uint32_t pnodes_cap;
+  PairRec *pairs;
+  uint32_t *npairs;
+  uint32_t pairs_cap;
+  uint32_t *overflow;           // set when a capacity is exceeded (host retries smaller)
+  uint32_t *done_scratch;       // per wave: targets finished in earlier passes
+  uint32_t done_cap;
+};
+
+struct SlotState {
+  uint32_t t;          // target iid (0 = none)
+  int32_t  head;
+  uint32_t nn;
+  int32_t  diag_ct, diag_bgn, diag_end;
+  uint32_t consistent;
+};
+
+__device__ __forceinline__ void slot_reset(SlotState &s) {
+  s.t = 0; s.head = 0; s.nn = 0; s.diag_ct = 0; s.diag_bgn = 0x7fffffff; s.diag_end = 0;
+  s.consistent = 1;
+}
+
+struct WaveAlloc {
+  uint32_t *cur;   // LDS: next free node
+  uint32_t *end;   // LDS: end of claimed block
+};
+
+// Node slots for the lanes active at the call; one LDS-held block per wave.
+__device__ __forceinline__ int32_t lane_alloc(WaveAlloc &W, const ChainArgs &A, uint32_t lane) {
+  uint64_t act = __ballot(1);
+  uint32_t leader = __builtin_ctzll(act);
+  uint32_t n = __builtin_popcountll(act);
+  uint32_t rank = __builtin_popcountll(act & ((1ull << lane) - 1));
+  uint32_t base = 0;
+  if (lane == leader) {
+    if (*W.cur + n > *W.end) {
+      uint32_t b = atomicAdd(A.pool_next, (uint32_t)OVL_NODE_BLOCK);
+      if (b + OVL_NODE_BLOCK > A.pool_cap) {
+        atomicOr(A.overflow, 1u);
+        b = 0xFFFFFFFFu;
+      }
+      *W.cur = b;
+      *W.end = b + OVL_NODE_BLOCK;
+    }
+    base = *W.cur;
+    if (base != 0xFFFFFFFFu) *W.cur = base + n;
+  }
+  base = __shfl(base, leader);
+  if (base == 0xFFFFFFFFu) return -1;
+  return (int32_t)(base + rank);
+}
+
+// Add_Match (Find_Overlaps.C:79) on the slot's list.  p = occurrence offset in the
+// target, o = window offset in the query.  Returns false if the node pool ran out.
+__device__ __forceinline__ void add_match(SlotState &s, int32_t p, int32_t o, int32_t k,
+                                          Node *pool, WaveAlloc &W, const ChainArgs &A,
+                                          uint32_t lane) {
+  int32_t new_diag = p - o;
+  int32_t diag = 0, expected_start = 0, num_checked = 0;
+  bool move_to_front = false;
+  int32_t prev = 0, cur = s.head;
+  bool done = false;
+  uint32_t guard = 0;
+  while (cur > 0 && guard++ <= s.nn) {
+    Node nd = pool[cur];
+    expected_start = nd.Start + nd.Len - k + 1;
+    diag = nd.Offset - nd.Start;
+    if (expected_start < o) break;
+    if (expected_start == o) {
+      if (new_diag == diag) {
+        pool[cur].Len = nd.Len + 1;
+        if (move_to_front) {
+          pool[prev].Next = nd.Next;
+          pool[cur].Next = s.head;
+          s.head = cur;
+        }
+        done = true;
+        break;
+      }
+      move_to_front = true;
+    }
+    num_checked++;
+    prev = cur;
+    cur = nd.Next;
+  }
+  if (!done) {
+    if (s.head != 0 && (num_checked > 0 || abs(diag - new_diag) > 3 ||
+                        o < expected_start + k - 2))
+      s.consistent = 0;
+    int32_t idx = lane_alloc(W, A, lane);
+    if (idx > 0) {
+      Node nn;
+      nn.Offset = p; nn.Len = k; nn.Start = o; nn.Next = s.head;
+      pool[idx] = nn;
+      s.head = idx;
+      s.nn++;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t thash(uint32_t t) {
+  t *= 0x9E3779B1u;
+  return t >> 25;                 // 7 bits -> 0..127
+}
+
+// Replay the occurrences of target s.t found in window j's staged segment [lo0, hi0).
+__device__ __forceinline__ void replay_window(SlotState &s, const uint64_t *hb, uint32_t lo0,
+                                              uint32_t hi0, int32_t o_j, int32_t k,
+                                              WaveAlloc &W, const ChainArgs &A,
+                                              uint32_t lane) {
+  if (s.t == 0) return;
+  uint32_t lo = lo0, hi = hi0;           // entries are iid-descending: first iid <= t
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(hb[mid] >> 32) > s.t) lo = mid + 1; else hi = mid;
+  }
+  while (lo < hi0 && (uint32_t)(hb[lo] >> 32) == s.t) {
+    int32_t pp = (int32_t)(uint32_t)hb[lo];
+    s.diag_ct++;                                        // Add_Ref (:203-206)
+    if (s.diag_bgn > o_j) s.diag_bgn = o_j;
+    if (s.diag_end < o_j) s.diag_end = o_j;
+    add_match(s, pp, o_j, k, A.pool, W, A, lane);
+    lo++;
+  }
+}
+
+// Walk the slot's list and store it in list order; write its PairRec.
+__device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32_t uflags,
+                                          const ChainArgs &A, uint32_t lane) {
+  bool has = s.t != 0 && s.nn > 0;
+  uint64_t m = __ballot(has);
+  uint32_t np = __builtin_popcountll(m);
+  if (np == 0) return;
+  uint32_t rank = __builtin_popcountll(m & ((1ull << lane) - 1));
+  uint32_t nn = has ? s.nn : 0;
+  uint32_t incl = nn;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t v = __shfl_up(incl, d);
+    if ((int)lane >= d) incl += v;
+  }
+  uint32_t totn = __shfl(incl, 63);
+  uint32_t pbase = 0, nbase = 0;
+  if (lane == 0) {
+    pbase = atomicAdd(A.npairs, np);
+    nbase = atomicAdd(A.pnodes_next, totn);
+    if (pbase + np > A.pairs_cap || nbase + totn > A.pnodes_cap) atomicOr(A.overflow, 2u);
+  }
+  pbase = __shfl(pbase, 0);
+  nbase = __shfl(nbase, 0);
+  if (has && pbase + rank < A.pairs_cap && nbase + incl <= A.pnodes_cap) {
+    uint32_t no = nbase + incl - nn;
+    uint32_t c = 0;
+    for (int32_t x = s.head; x > 0 && c < nn; c++) {
+      Node nd = A.pool[x];
+      A.pnodes[no + c] = nd;
+      x = nd.Next;
+    }
+    PairRec pr2;
+    pr2.unit = u;
+    pr2.tgt = s.t - A.R.first_iid;
+    pr2.node_off = no;
+    pr2.node_cnt = c;
+    pr2.diag_ct = s.diag_ct;
+    pr2.diag_bgn = s.diag_bgn;
+    pr2.diag_end = s.diag_end;
+    pr2.flags = (s.consistent ? 1u : 0u) | (uflags & 6u);
+    A.pairs[pbase + rank] = pr2;
+  }
+}
+
+#define WAVE_SYNC()                                          \
+  do {                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+    __builtin_amdgcn_wave_barrier();                         \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+  } while (0)
+
+__global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
+  __shared__ uint64_t s_hb[4][OVL_HCAP];
+  __shared__ uint32_t s_seg[4][65];
+  __shared__ uint32_t s_off[4][64];
+  __shared__ uint32_t s_tgt[4][OVL_MAXT];
+  __shared__ uint32_t s_alloc[4][2];
+  __shared__ uint32_t s_over[4];
+  uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t *hb = s_hb[wave];
+  uint32_t *seg = s_seg[wave];
+  uint32_t *soff = s_off[wave];
+  uint32_t *tgt = s_tgt[wave];
+  WaveAlloc W;
+  W.cur = &s_alloc[wave][0];
+  W.end = &s_alloc[wave][1];
+  if (lane == 0) { *W.cur = 0; *W.end = 0; }
+  const int32_t k = (int32_t)A.k;
+  uint32_t gw = blockIdx.x * 4 + wave;
+  uint32_t *done_list = A.done_scratch + (size_t)gw * A.done_cap;
+
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(A.unit_next, 1u);
+    u = __shfl(u, 0);
+    if (u >= A.nunits) break;
+    Unit un = A.units[u];
+    uint32_t nw = unit_windows(A.R, un, A.k);
+    const Probe *pr = A.probes + A.rbase[u];
+    uint32_t uflags = A.unit_flags[u];
+    uint32_t ndone = 0;
+
+    for (uint32_t pass = 0;; pass++) {
+      SlotState s0, s1;
+      slot_reset(s0);
+      slot_reset(s1);
+      for (uint32_t i = lane; i < OVL_MAXT; i += 64) tgt[i] = 0;
+      if (lane == 0) s_over[wave] = 0;
+      WAVE_SYNC();
+
+      for (uint32_t base = 0; base < nw; base += 64) {
+        uint32_t o = base + lane;
+        Probe p;
+        p.off = 0; p.cnt = 0;
+        if (o < nw) p = pr[o];
+        uint32_t incl = p.cnt;                       // wave inclusive scan
+        for (int d = 1; d < 64; d <<= 1) {
+          uint32_t v = __shfl_up(incl, d);
+          if ((int)lane >= d) incl += v;
+        }
+        uint32_t total = __shfl(incl, 63);
+        if (total == 0) continue;
+        seg[lane] = incl - p.cnt;
+        soff[lane] = p.off;
+        if (lane == 63) seg[64] = total;
+        WAVE_SYNC();
+
+        for (uint32_t p0 = 0; p0 < total; p0 += OVL_HCAP) {
+          uint32_t p1 = p0 + OVL_HCAP < total ? p0 + OVL_HCAP : total;
+          // stage occurrences p0..p1 of this chunk, in order (ordered compaction)
+          for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
+            uint32_t lo = 0, hi = 64;            // last j with seg[j] <= idx
+            while (hi - lo > 1) {
+              uint32_t mid = (lo + hi) >> 1;
+              if (seg[mid] <= idx) lo = mid; else hi = mid;
+            }
+            hb[idx - p0] = A.occ[soff[lo] + (idx - seg[lo])];
+          }
+          WAVE_SYNC();
+          // discover targets (LDS open-addressing set, 128 slots)
+          for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
+            uint32_t t = (uint32_t)(hb[idx - p0] >> 32);
+            bool skip = false;
+            for (uint32_t q = 0; q < ndone; q++)
+              if (done_list[q] == t) { skip = true; break; }
+            if (skip) continue;
+            uint32_t h = thash(t);
+            bool placed = false;
+            for (uint32_t probe = 0; probe < OVL_MAXT; probe++) {
+              uint32_t cur = tgt[h];
+              if (cur == t) { placed = true; break; }
+              if (cur == 0) {
+                uint32_t old = atomicCAS(&tgt[h], 0u, t);
+                if (old == 0 || old == t) { placed = true; break; }
+              }
+              h = (h + 1) & (OVL_MAXT - 1);
+            }
+            if (!placed) atomicOr(&s_over[wave], 1u);
+          }
+          WAVE_SYNC();
+          uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
+          if (t0 != s0.t) { slot_reset(s0); s0.t = t0; }
+          if (t1 != s1.t) { slot_reset(s1); s1.t = t1; }
+          // replay Add_Match per target, windows in order
+          for (uint32_t j = 0; j < 64; j++) {
+            uint32_t sj = seg[j], ej = seg[j + 1];
+            if (ej <= p0 || sj >= p1 || ej == sj) continue;
+            uint32_t lo0 = (sj > p0 ? sj : p0) - p0, hi0 = (ej < p1 ? ej : p1) - p0;
+            int32_t o_j = (int32_t)(base + j);
+            replay_window(s0, hb, lo0, hi0, o_j, k, W, A, lane);
+            replay_window(s1, hb, lo0, hi0, o_j, k, W, A, lane);
+          }
+          WAVE_SYNC();
+        }
+      }
+
+      emit_slot(s0, u, uflags, A, lane);
+      emit_slot(s1, u, uflags, A, lane);
+
+      bool over = s_over[wave] != 0;
+      if (!over) break;
+      // targets the 128-slot table could not hold: another pass over the unit
+      uint64_t m0 = __ballot(s0.t != 0), m1 = __ballot(s1.t != 0);
+      uint32_t c0 = __builtin_popcountll(m0), c1 = __builtin_popcountll(m1);
+      if (ndone + c0 + c1 > A.done_cap) {
+        if (lane == 0) atomicOr(A.overflow, 4u);
+        break;
+      }
+      if (s0.t) done_list[ndone + __builtin_popcountll(m0 & ((1ull << lane) - 1))] = s0.t;
+      if (s1.t) done_list[ndone + c0 + __builtin_popcountll(m1 & ((1ull << lane) - 1))] = s1.t;
+      ndone += c0 + c1;
+      __threadfence_block();
+      WAVE_SYNC();
+    }
+  }
+}
+
+}  // namespace ovl

@@ -1,0 +1,306 @@
+"""Host-side mirror of canu's overlapInCore interface over the MI355X C-ABI.
+
+Names follow the reference: `OicParameters` is oicParameters (overlapInCore.H:418) and
+`parse_overlapInCore_args` accepts overlapInCore's own options (overlapInCore.C:316-412).
+`OverlapInCore` drives what OverlapDriver() does (overlapInCore.C:190): load the reads,
+Build_Hash_Index over the -h range, search the -r range in both orientations, and hand
+back ovOverlap records.  Everything runs in libcanu_ovl.so on a gfx950 device; there is
+no CPU fallback -- a missing library or device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcanu_ovl.so")
+
+RECORD_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("w0", "<u8"), ("w1", "<u8")])
+
+OVL_STATUS = {0: "OVL_OK", -1: "OVL_ERR_NO_DEVICE", -2: "OVL_ERR_BAD_PARAM",
+              -3: "OVL_ERR_UNSUPPORTED", -4: "OVL_ERR_BAD_INPUT", -5: "OVL_ERR_HIP",
+              -6: "OVL_ERR_OOM", -7: "OVL_ERR_STATE"}
+
+UINT64_MAX = (1 << 64) - 1
+
+
+class OvlError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{OVL_STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("kmer_len", ctypes.c_uint32), ("max_erate", ctypes.c_double),
+                ("min_olap_len", ctypes.c_int32), ("partial", ctypes.c_int32),
+                ("unique_olap_per_pair", ctypes.c_int32), ("use_window_filter", ctypes.c_int32),
+                ("use_hopeless_check", ctypes.c_int32), ("frag_olap_limit", ctypes.c_uint64),
+                ("filter_by_kmer_count", ctypes.c_uint64)]
+
+
+class _Record(ctypes.Structure):
+    _fields_ = [("a_iid", ctypes.c_uint32), ("b_iid", ctypes.c_uint32),
+                ("dat", ctypes.c_uint64 * 2)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "kmer_hits_without_olap", "kmer_hits_with_olap", "kmer_hits_skipped", "multi_overlaps",
+        "total_overlaps", "contained_overlaps", "dovetail_overlaps", "seed_hits", "pairs")] + \
+        [("ms_index", ctypes.c_double), ("ms_seed", ctypes.c_double),
+         ("ms_extend", ctypes.c_double), ("ms_probe_kernel", ctypes.c_double),
+         ("probe_bytes", ctypes.c_uint64)]
+
+
+# Every symbol include/canu_ovl.h declares (tests check the library exports them all).
+EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_destroy",
+           "ovl_last_error", "ovl_abi_version", "ovl_load_reads", "ovl_load_reads_device",
+           "ovl_set_skip_kmers", "ovl_build_hash_index", "ovl_find_overlaps",
+           "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream"]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libcanu_ovl.so.  Raises if it was not built -- there is no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OvlError(-1, f"{path} missing: run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    lib.ovl_params_init.argtypes = [P(_Params)]
+    lib.ovl_params_finalize.argtypes = [P(_Params)]
+    lib.ovl_ctx_create.argtypes = [P(_Params), ctypes.c_int, P(ctypes.c_void_p)]
+    lib.ovl_ctx_destroy.argtypes = [ctypes.c_void_p]
+    lib.ovl_last_error.restype = ctypes.c_char_p
+    lib.ovl_load_reads.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+    lib.ovl_load_reads_device.argtypes = lib.ovl_load_reads.argtypes
+    lib.ovl_set_skip_kmers.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64]
+    lib.ovl_build_hash_index.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    lib.ovl_find_overlaps.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                      P(ctypes.c_uint64)]
+    lib.ovl_fetch_overlaps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                       P(ctypes.c_uint64)]
+    lib.ovl_get_stats.argtypes = [ctypes.c_void_p, P(_Stats)]
+    lib.ovl_ctx_stream.argtypes = [ctypes.c_void_p]
+    lib.ovl_ctx_stream.restype = ctypes.c_void_p
+    _lib = lib
+    return lib
+
+
+@dataclasses.dataclass
+class OicParameters:
+    """oicParameters (overlapInCore.H:418-530), the options this path honours."""
+    Kmer_Len: int = 0
+    maxErate: float = 0.06
+    Min_Olap_Len: int = 0
+    Doing_Partial_Overlaps: bool = False
+    Unique_Olap_Per_Pair: bool = True
+    Use_Window_Filter: bool = False
+    Use_Hopeless_Check: bool = True
+    Frag_Olap_Limit: int = UINT64_MAX
+    Filter_By_Kmer_Count: int = 0
+    bgnHashID: int = 1
+    endHashID: int = 0xFFFFFFFF
+    bgnRefID: int = 1
+    endRefID: int = 0xFFFFFFFF
+
+    def finalize(self) -> "OicParameters":
+        """main()'s fix-ups after option parsing (overlapInCore.C:416-421)."""
+        if self.maxErate > 0.06:
+            self.Use_Window_Filter = False
+            self.Use_Hopeless_Check = False
+        return self
+
+    def to_c(self) -> _Params:
+        return _Params(kmer_len=self.Kmer_Len, max_erate=self.maxErate,
+                       min_olap_len=self.Min_Olap_Len, partial=int(self.Doing_Partial_Overlaps),
+                       unique_olap_per_pair=int(self.Unique_Olap_Per_Pair),
+                       use_window_filter=int(self.Use_Window_Filter),
+                       use_hopeless_check=int(self.Use_Hopeless_Check),
+                       frag_olap_limit=self.Frag_Olap_Limit,
+                       filter_by_kmer_count=self.Filter_By_Kmer_Count)
+
+    def as_dict(self) -> dict:
+        return dict(kmer_len=self.Kmer_Len, max_erate=self.maxErate,
+                    min_olap_len=self.Min_Olap_Len, partial=int(self.Doing_Partial_Overlaps),
+                    unique_olap_per_pair=int(self.Unique_Olap_Per_Pair),
+                    use_window_filter=int(self.Use_Window_Filter),
+                    use_hopeless_check=int(self.Use_Hopeless_Check),
+                    frag_olap_limit=self.Frag_Olap_Limit,
+                    filter_by_kmer_count=self.Filter_By_Kmer_Count)
+
+
+def _decode_range(s: str) -> tuple[int, int]:
+    """AS_UTL_decodeRange: 'a-b' or 'a'."""
+    if "-" in s:
+        a, b = s.split("-", 1)
+        return int(a), int(b)
+    return int(s), int(s)
+
+
+def parse_overlapInCore_args(argv: list[str]) -> tuple[OicParameters, dict]:
+    """Parse overlapInCore's command line (overlapInCore.C:316-412) the way main() does:
+    --maxerate through strtof (a float), --minkmers evaluated where it appears."""
+    P = OicParameters()
+    extra = {"skip_file": None, "store": None, "output": None, "threads": 1}
+    i = 0
+    while i < len(argv):
+        a = argv[i]
+        if a == "-G":
+            P.Doing_Partial_Overlaps = True
+        elif a == "-h":
+            i += 1; P.bgnHashID, P.endHashID = _decode_range(argv[i])
+        elif a == "-r":
+            i += 1; P.bgnRefID, P.endRefID = _decode_range(argv[i])
+        elif a == "-k":
+            i += 1
+            v = argv[i]
+            if v.isdigit() and len(v) <= 2:
+                P.Kmer_Len = int(v)
+            else:
+                extra["skip_file"] = v
+        elif a == "-l":
+            i += 1
+            v = int(argv[i])
+            P.Frag_Olap_Limit = UINT64_MAX if v < 1 else v
+        elif a == "-m":
+            P.Unique_Olap_Per_Pair = False
+        elif a == "-u":
+            P.Unique_Olap_Per_Pair = True
+        elif a == "--minlength":
+            i += 1; P.Min_Olap_Len = int(argv[i])
+        elif a == "--minkmers":
+            P.Filter_By_Kmer_Count = int(np.floor(np.exp(-1.0 * P.Kmer_Len * P.maxErate) *
+                                                  (P.Min_Olap_Len - P.Kmer_Len + 1)))
+        elif a == "--maxerate":
+            i += 1; P.maxErate = float(np.float32(float(argv[i])))
+        elif a == "-w":
+            P.Use_Window_Filter = True
+        elif a == "-z":
+            P.Use_Hopeless_Check = False
+        elif a == "-o":
+            i += 1; extra["output"] = argv[i]
+        elif a == "-t":
+            i += 1; extra["threads"] = int(argv[i])
+        elif a in ("--hashbits", "--hashstrings", "--hashdatalen", "--hashload", "-s",
+                   "--maxreadlen", "-H", "-R"):
+            i += 1      # CPU hash-table sizing / stats options: not needed on this path
+        else:
+            extra["store"] = a
+        i += 1
+    P.finalize()
+    return P, extra
+
+
+def read_skip_fasta(path: str, k: int) -> list[str]:
+    """The -k <frequentMers.fasta> file: '>' line then one k-mer line (Mark_Skip_Kmers)."""
+    out = []
+    with open(path) as f:
+        lines = f.read().split("\n")
+    for j in range(0, len(lines) - 1, 2):
+        if not lines[j].startswith(">"):
+            raise ValueError(f"bad skip-kmer line {j + 1}")
+        km = lines[j + 1].strip()
+        if len(km) != k:
+            raise ValueError(f"bad skip-kmer line {j + 2}")
+        out.append(km)
+    return out
+
+
+class OverlapInCore:
+    """One overlapInCore job on one gfx950 device (one process per GPU)."""
+
+    def __init__(self, params: OicParameters, device: int = 0):
+        self.lib = load_library()
+        self.params = params
+        cp = params.to_c()
+        ctx = ctypes.c_void_p()
+        self._check(self.lib.ovl_ctx_create(ctypes.byref(cp), device, ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.first_iid = 1
+        self.nreads = 0
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise OvlError(rc, self.lib.ovl_last_error().decode())
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.ovl_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_reads(self, rs) -> None:
+        bases = np.ascontiguousarray(rs.bases, dtype=np.uint8)
+        offs = np.ascontiguousarray(rs.offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(rs.lengths, dtype=np.uint32)
+        self._check(self.lib.ovl_load_reads(self.ctx, rs.first_iid, rs.nreads,
+                                            bases.ctypes.data, offs.ctypes.data,
+                                            lens.ctypes.data, None))
+        self.first_iid = rs.first_iid
+        self.nreads = rs.nreads
+
+    def load_reads_device(self, first_iid: int, d_bases: int, d_offsets: int,
+                          lengths: np.ndarray) -> None:
+        """Reads already in HBM (device pointers, e.g. from torch tensors)."""
+        lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+        self._check(self.lib.ovl_load_reads_device(self.ctx, first_iid, lens.shape[0],
+                                                   d_bases, d_offsets, lens.ctypes.data, None))
+        self.first_iid = first_iid
+        self.nreads = int(lens.shape[0])
+
+    def set_skip_kmers(self, kmers: list[str]) -> None:
+        blob = "".join(kmers).encode()
+        self._check(self.lib.ovl_set_skip_kmers(self.ctx, blob, len(kmers)))
+
+    def build_hash_index(self, bgn: int | None = None, end: int | None = None) -> None:
+        bgn = self.params.bgnHashID if bgn is None else bgn
+        end = self.params.endHashID if end is None else end
+        self._check(self.lib.ovl_build_hash_index(self.ctx, bgn, min(end, 0xFFFFFFFF)))
+
+    def find_overlaps(self, bgn: int | None = None, end: int | None = None) -> int:
+        bgn = self.params.bgnRefID if bgn is None else bgn
+        end = self.params.endRefID if end is None else end
+        n = ctypes.c_uint64()
+        self._check(self.lib.ovl_find_overlaps(self.ctx, bgn, min(end, 0xFFFFFFFF),
+                                               ctypes.byref(n)))
+        return n.value
+
+    def fetch(self, n: int | None = None) -> np.ndarray:
+        if n is None:
+            n = self.stats()["total_overlaps"]
+        rec = np.zeros(max(n, 1), dtype=RECORD_DTYPE)
+        got = ctypes.c_uint64()
+        self._check(self.lib.ovl_fetch_overlaps(self.ctx, rec.ctypes.data, n,
+                                                ctypes.byref(got)))
+        return rec[:got.value]
+
+    def stats(self) -> dict:
+        s = _Stats()
+        self._check(self.lib.ovl_get_stats(self.ctx, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in _Stats._fields_}
+
+    def stream(self) -> int:
+        return self.lib.ovl_ctx_stream(self.ctx)
+
+    def run(self, rs, skip_kmers=None) -> np.ndarray:
+        """OverlapDriver() for one hash batch: load, index, search, fetch (sorted)."""
+        self.load_reads(rs)
+        if skip_kmers:
+            self.set_skip_kmers(skip_kmers)
+        self.build_hash_index()
+        n = self.find_overlaps()
+        return self.fetch(n)
