@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py -- overlapInCore on MI355X: overlaps/sec on 50k x 10 kb synthetic ONT reads.
+
+One step = one full overlapInCore job over the resident read set: Build_Hash_Index over
+all reads (-h 1-N) and Find_Overlaps for every query read in both orientations (-r), with
+seed extension and ovOverlap output (BASELINE configs[2]).  Reads are generated
+synthetically (no datasets here), packed into HBM before the timed region; records stay in
+HBM.  With --gpus N (torchrun, one process per GPU) every rank generates 1/N of the reads,
+the packed read store is all-gathered over RCCL, every rank builds the index and searches
+its own query range (ranges balanced by pair count), independent per-shard output.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "overlaps/sec + Gbp-vs-Gbp/sec, 50k×10kb ONT reads, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def query_shards(n: int, world: int) -> list[tuple[int, int]]:
+    """Split query IDs 1..n so every rank gets about the same number of (a, b>a) pairs:
+    read a pairs with the n-a reads after it."""
+    w = np.arange(n, 0, -1, dtype=np.float64) - 1.0     # weight of a = n - a
+    c = np.cumsum(w)
+    tot = c[-1] if n else 0.0
+    out, lo = [], 1
+    for r in range(world):
+        if r == world - 1:
+            hi = n
+        else:
+            hi = int(np.searchsorted(c, tot * (r + 1) / world)) + 1
+            hi = max(hi, lo - 1)
+        out.append((lo, hi))
+        lo = hi + 1
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=50_000)
+    ap.add_argument("--read-len", type=int, default=10_000)
+    ap.add_argument("--coverage", type=float, default=25.0)
+    ap.add_argument("--read-error", type=float, default=0.015)
+    ap.add_argument("--k", type=int, default=22)
+    ap.add_argument("--maxerate", type=float, default=0.06)
+    ap.add_argument("--minlength", type=int, default=500)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample-reads", type=int, default=1000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from canu_amd.synth import synth_reads, random_genome
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+
+    n = args.reads
+    genome_len = int(n * args.read_len / args.coverage)
+    gen_kw = dict(n_reads=n, read_len=args.read_len, genome_len=genome_len,
+                  error_rate=args.read_error, seed=args.seed)
+
+    # ---- setup: each rank generates its slice, then the read store is all-gathered ----
+    t_setup = time.time()
+    genome = random_genome(np.random.default_rng(args.seed), genome_len)
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    part = synth_reads(genome=genome, read_range=(lo, hi), **gen_kw)
+    dev = torch.device("cuda", local)
+    if world == 1:
+        bases = torch.from_numpy(part.bases).to(dev)
+        lengths = part.lengths
+    else:
+        mine = torch.from_numpy(part.bases).to(dev)
+        sizes = torch.tensor([mine.numel()], device=dev, dtype=torch.int64)
+        all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+        dist.all_gather(all_sizes, sizes)
+        mx = int(max(s.item() for s in all_sizes))
+        buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+        buf[:mine.numel()] = mine
+        gathered = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
+        dist.all_gather(gathered, buf)                          # RCCL over xGMI
+        bases = torch.cat([g[:int(s.item())] for g, s in zip(gathered, all_sizes)])
+        lens_t = torch.from_numpy(part.lengths.astype(np.int64)).to(dev)
+        nl = torch.tensor([lens_t.numel()], device=dev, dtype=torch.int64)
+        all_nl = [torch.zeros_like(nl) for _ in range(world)]
+        dist.all_gather(all_nl, nl)
+        mxl = int(max(v.item() for v in all_nl))
+        lb = torch.zeros(mxl, dtype=torch.int64, device=dev)
+        lb[:lens_t.numel()] = lens_t
+        gl = [torch.empty(mxl, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(gl, lb)
+        lengths = torch.cat([g[:int(v.item())] for g, v in zip(gl, all_nl)]).cpu().numpy()
+        lengths = lengths.astype(np.uint32)
+    offsets = np.zeros(n, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    d_offsets = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    total_bases = int(lengths.sum(dtype=np.uint64))
+
+    P = OicParameters(Kmer_Len=args.k, maxErate=float(np.float32(args.maxerate)),
+                      Min_Olap_Len=args.minlength).finalize()
+    oic = OverlapInCore(P, device=local)
+    oic.load_reads_device(1, bases.data_ptr(), d_offsets.data_ptr(), lengths)
+    torch.cuda.synchronize()
+    shards = query_shards(n, world)
+    q_lo, q_hi = shards[rank]
+    setup_s = time.time() - t_setup
+
+    def step() -> int:
+        oic.build_hash_index(1, n)
+        return oic.find_overlaps(q_lo, q_hi)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nrec = 0
+    for _ in range(args.steps):
+        nrec = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = oic.stats()
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    nr = torch.tensor([nrec], dtype=torch.int64, device=dev)
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(nr, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_ovl = int(nr.item())
+    value = total_ovl * args.steps / elapsed
+    ms_step = 1000.0 * elapsed / args.steps
+    gbp = total_bases / 1e9
+    gbp_vs_gbp = gbp * gbp / 2.0 * args.steps / elapsed    # all-vs-all, each pair once
+
+    roof = None
+    if st["ms_probe_kernel"] > 0:
+        achieved = st["probe_bytes"] / (st["ms_probe_kernel"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_probe", "algorithmic_bytes": st["probe_bytes"],
+                "ms": round(st["ms_probe_kernel"], 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "overlaps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 2),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u8/2-bit bases, int32 edit rows", "data": "synthetic",
+            "config": {"workload": "configs[2]: 50k synthetic ONT reads x 10 kb, full "
+                                   "overlapInCore (seed + banded extend), all-vs-all",
+                       "reads": n, "read_len": args.read_len, "coverage": args.coverage,
+                       "read_error": args.read_error, "k": args.k,
+                       "maxerate": P.maxErate, "minlength": args.minlength,
+                       "parallelism": f"query-shard{world}"},
+            "overlaps_per_step": total_ovl,
+            "gbp_vs_gbp_per_sec": round(gbp_vs_gbp, 4),
+            "breakdown_ms": {"index": round(st["ms_index"], 2), "seed": round(st["ms_seed"], 2),
+                             "extend": round(st["ms_extend"], 2)},
+            "seed_hits": st["seed_hits"], "pairs": st["pairs"],
+            "setup_s": round(setup_s, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    oic.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args) -> dict | None:
+    """The reference overlapInCore (oracle/_ref/oic_ref, built from its sources) on a
+    bounded sample of the same workload: fewer reads, same read length / error / coverage."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import oracle
+        from canu_amd.synth import synth_reads
+    except Exception:
+        return None
+    if not oracle.reference_available():
+        return None
+    ns = args.cpu_sample_reads
+    gl = int(ns * args.read_len / args.coverage)
+    rs = synth_reads(ns, args.read_len, gl, args.read_error, seed=args.seed + 1000)
+    p = oracle.default_params(kmer_len=args.k, max_erate=args.maxerate,
+                              min_olap_len=args.minlength)
+    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    rec, secs, wall = oracle.run_reference(rs, p, threads=threads, hash_bits=22, with_time=True)
+    return {"value": round(len(rec) / secs, 1), "unit": "overlaps/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"{ns} reads x {args.read_len} bp at {args.coverage:.0f}x "
+                      f"(genome {gl} bp), reference OverlapDriver() wall {secs:.2f}s, "
+                      f"{len(rec)} overlaps"}
+
+
+if __name__ == "__main__":
+    main()

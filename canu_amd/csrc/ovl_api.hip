@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -527,6 +528,8 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   return OVL_OK;
 }
 
+static unsigned long long *dbg_ptr_for_print = nullptr;
+
 IndexDev index_dev(const ovl_ctx *c) {
   IndexDev X;
   X.tab = c->d_tab.p;
@@ -573,7 +576,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   DBuf<Unit> d_units;
   DBuf<uint64_t> d_rbase;
   DBuf<Probe> d_probe;
-  DBuf<uint32_t> d_uhits, d_uflags, d_ctr, d_done;
+  DBuf<uint32_t> d_uhits, d_uflags, d_ctr, d_done, d_defer;
   DBuf<Node> d_pool, d_pnodes;
   DBuf<PairRec> d_pairs;
   DBuf<unsigned long long> d_stats;
@@ -592,7 +595,14 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
       d_rowdir.alloc((size_t)2 * (e_cap + 2) * ext_waves) ||
       d_deltas.alloc((size_t)4 * (e_cap + 8) * ext_waves))
     return fail(OVL_ERR_OOM, "extension scratch");
-  uint32_t chain_waves = 8u * c->n_cu;
+  // LDS per extension wave: two row buffers + the traceback window (ovl_extend.hip)
+  size_t ext_lds_wave = 4ull * (((4ull * OVL_SCAP_WORDS + 2ull * (2 * e_cap + 8) + TB_ROWS * TB_W +
+                                  OVL_LDCAP) + 3) & ~3ull);
+  uint32_t ext_wpb = (4 * ext_lds_wave <= 80 * 1024) ? 4 : (2 * ext_lds_wave <= 80 * 1024) ? 2 : 1;
+  if (ext_lds_wave > 160 * 1024)
+    return fail(OVL_ERR_UNSUPPORTED, "error limit %d needs more LDS than a CU has", e_cap);
+  ext_waves = (ext_waves / ext_wpb) * ext_wpb;
+  uint32_t chain_waves = 16u * c->n_cu;
   const uint32_t DONE_CAP = 4096;
   if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");
 
@@ -600,7 +610,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   if (c->d_out.alloc(out_cap)) return fail(OVL_ERR_OOM, "output");
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
-  uint64_t seed_hits = 0, npairs_tot = 0, probe_bytes = 0;
+  uint64_t npairs_tot = 0, probe_bytes = 0;
   uint32_t nu = (uint32_t)units.size();
   uint32_t u0 = 0;
   while (u0 < nu) {
@@ -643,7 +653,6 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     uint64_t hsum = 0;
     uint32_t nc = 0;
     while (nc < nb && (hsum + uh[nc] <= HIT_BUDGET || nc == 0)) hsum += uh[nc++];
-    seed_hits += hsum;
 
     uint64_t pool_cap = hsum + (hsum / 4000 + chain_waves + 2) * (uint64_t)OVL_NODE_BLOCK + 8;
     uint64_t pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * 256 + 1024);
@@ -675,6 +684,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     CA.overflow = d_ctr.p + 4;
     CA.done_scratch = d_done.p;
     CA.done_cap = DONE_CAP;
+    CA.seed_hits = (unsigned long long *)(d_stats.p + 7);
     HIPC(hipEventRecord(c->ev[4], s));
     hipLaunchKernelGGL(k_chain, dim3(chain_waves / 4), dim3(256), 0, s, CA);
     HIPC(hipGetLastError());
@@ -731,9 +741,42 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.out_cap = (uint32_t)std::min<uint64_t>(c->d_out.n, 0xFFFFFFF0ull);
     EA.stats = d_stats.p;
     EA.overflow = d_ctr.p + 7;
+    EA.dbg = nullptr;
+    if (getenv("OVL_DEBUG")) {
+      static DBuf<unsigned long long> dbgbuf;
+      if (!dbgbuf.p) { dbgbuf.alloc(16); (void)hipMemset(dbgbuf.p, 0, 128); }
+      EA.dbg = dbgbuf.p;
+      dbg_ptr_for_print = dbgbuf.p;
+    }
+    EA.list = nullptr;
+    EA.defer = nullptr;
+    EA.ndefer = d_ctr.p + 8;
     HIPC(hipEventRecord(c->ev[6], s));
-    if (npairs)
-      hipLaunchKernelGGL(k_extend, dim3(ext_waves / 4), dim3(256), 0, s, EA);
+    if (npairs) {
+      size_t lds = ext_lds_wave * ext_wpb + 4ull * (((e_cap + 2) + 3) & ~3);
+      if ((c->max_len + 31) / 32 + 1 <= OVL_SCAP_WORDS) {
+        // staged kernel for exception-free pairs; pairs touching an 'n' are deferred to
+        // the generic kernel below
+        if (d_defer.alloc(npairs)) return fail(OVL_ERR_OOM, "defer list");
+        EA.defer = d_defer.p;
+        hipLaunchKernelGGL(k_extend<true>, dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
+                           lds, s, EA);
+        HIPC(hipGetLastError());
+        uint32_t nd = 0;
+        HIPC(hipMemcpyAsync(&nd, d_ctr.p + 8, 4, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        if (nd) {
+          EA.list = d_defer.p;
+          EA.npairs = nd;
+          EA.pair_next = d_ctr.p + 9;
+          hipLaunchKernelGGL(k_extend<false>, dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
+                             lds, s, EA);
+        }
+      } else {
+        hipLaunchKernelGGL(k_extend<false>, dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
+                           lds, s, EA);
+      }
+    }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev[7], s));
     HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
@@ -746,6 +789,12 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   }
   unsigned long long hs[8];
   HIPC(hipMemcpy(hs, d_stats.p, 64, hipMemcpyDeviceToHost));
+  if (dbg_ptr_for_print) {
+    unsigned long long dd[16];
+    (void)hipMemcpy(dd, dbg_ptr_for_print, 128, hipMemcpyDeviceToHost);
+    fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu tb=%llu iters=%llu pedcyc=%llu tbcyc=%llu pairs=%llu maxrows=%llu\n",
+            dd[0], dd[1], dd[2], dd[4], dd[5], dd[6], dd[7], dd[8], dd[9]);
+  }
   c->stats.kmer_hits_without_olap = hs[0];
   c->stats.kmer_hits_with_olap = hs[1];
   c->stats.kmer_hits_skipped = hs[2];
@@ -753,7 +802,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   c->stats.total_overlaps = hs[4];
   c->stats.contained_overlaps = hs[5];
   c->stats.dovetail_overlaps = hs[6];
-  c->stats.seed_hits = seed_hits;
+  c->stats.seed_hits = hs[7];
   c->stats.pairs = npairs_tot;
   c->stats.ms_seed = ms_probe + ms_chain;
   c->stats.ms_extend = ms_ext;

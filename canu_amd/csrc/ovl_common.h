@@ -30,13 +30,28 @@ struct ReadsDev {
   uint32_t        nreads;
 };
 
-// One strand of one read as the extension sees it.
-struct Strand {
-  const uint64_t *w;
-  const uint32_t *ex_wild;  // bases that match anything ('n'), may be null
-  const uint32_t *ex_nul;   // bases that match nothing but a wildcard, may be null
+// One strand of one read as the extension sees it.  W is the pointer type of the packed
+// words: plain (global) or LDS (address space 3) when the strands are staged on chip.
+template <typename W>
+struct StrandT {
+  static constexpr bool kExc = true;
+  W               w;
+  const uint32_t *ex_wild;  // bases that match anything ('n'), may be null (global)
+  const uint32_t *ex_nul;   // bases that match nothing but a wildcard, may be null (global)
   int32_t         len;
 };
+// A strand without 'n' / NUL exceptions (the common case): no mask pointers at all.
+template <typename W>
+struct StrandP {
+  static constexpr bool kExc = false;
+  W       w;
+  int32_t len;
+};
+typedef StrandT<const uint64_t *> Strand;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+typedef StrandT<const lds_u64 *> StrandL;
+typedef StrandP<const lds_u64 *> StrandLP;
 
 __device__ __forceinline__ Strand strand_fwd(const ReadsDev &R, uint32_t r) {
   Strand s;
@@ -61,7 +76,8 @@ __device__ __forceinline__ Strand strand_rc(const ReadsDev &R, uint32_t r) {
 }
 
 // 32 bases starting at p (0 <= p < len); base i of the result in bits 2i..2i+1.
-__device__ __forceinline__ uint64_t bases_at(const uint64_t *w, int32_t p) {
+template <typename W>
+__device__ __forceinline__ uint64_t bases_at(W w, int32_t p) {
   uint32_t wi = (uint32_t)p >> 5, sh = ((uint32_t)p & 31u) * 2u;
   uint64_t v = w[wi] >> sh;
   if (sh) v |= w[wi + 1] << (64u - sh);
@@ -88,21 +104,25 @@ __device__ __forceinline__ uint64_t spread2(uint32_t m) {
 
 // Mismatch bits (bit 2i) between 32 bases of A at pa and of T at pt, both forward.
 // bases_match(a, b) = a == b || a == 'n' || b == 'n'   (forward.C:176)
-__device__ __forceinline__ uint64_t mismatch_fwd(const Strand &A, int32_t pa,
-                                                 const Strand &T, int32_t pt) {
+template <typename SA, typename ST>
+__device__ __forceinline__ uint64_t mismatch_fwd(const SA &A, int32_t pa, const ST &T,
+                                                 int32_t pt) {
   uint64_t x = bases_at(A.w, pa) ^ bases_at(T.w, pt);
   uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
-  if (A.ex_nul) mm |= spread2(mask_at(A.ex_nul, pa));
-  if (T.ex_nul) mm |= spread2(mask_at(T.ex_nul, pt));
-  uint32_t wild = 0;
-  if (A.ex_wild) wild |= mask_at(A.ex_wild, pa);
-  if (T.ex_wild) wild |= mask_at(T.ex_wild, pt);
-  if (wild) mm &= ~spread2(wild);
+  if constexpr (SA::kExc && ST::kExc) if (A.ex_nul || T.ex_nul || A.ex_wild || T.ex_wild) {
+    if (A.ex_nul) mm |= spread2(mask_at(A.ex_nul, pa));
+    if (T.ex_nul) mm |= spread2(mask_at(T.ex_nul, pt));
+    uint32_t wild = 0;
+    if (A.ex_wild) wild |= mask_at(A.ex_wild, pa);
+    if (T.ex_wild) wild |= mask_at(T.ex_wild, pt);
+    if (wild) mm &= ~spread2(wild);
+  }
   return mm;
 }
 
 // 32 bases ending at p, p-31 .. p (group 31 = base p).  p may be < 31.
-__device__ __forceinline__ uint64_t bases_end(const uint64_t *w, int32_t p) {
+template <typename W>
+__device__ __forceinline__ uint64_t bases_end(W w, int32_t p) {
   if (p >= 31) return bases_at(w, p - 31);
   return bases_at(w, 0) << (2 * (31 - p));
 }
@@ -111,22 +131,26 @@ __device__ __forceinline__ uint32_t mask_end(const uint32_t *m, int32_t p) {
   return mask_at(m, 0) << (31 - p);
 }
 
-__device__ __forceinline__ uint64_t mismatch_bwd(const Strand &A, int32_t pa,
-                                                 const Strand &T, int32_t pt) {
+template <typename SA, typename ST>
+__device__ __forceinline__ uint64_t mismatch_bwd(const SA &A, int32_t pa, const ST &T,
+                                                 int32_t pt) {
   uint64_t x = bases_end(A.w, pa) ^ bases_end(T.w, pt);
   uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
-  if (A.ex_nul) mm |= spread2(mask_end(A.ex_nul, pa));
-  if (T.ex_nul) mm |= spread2(mask_end(T.ex_nul, pt));
-  uint32_t wild = 0;
-  if (A.ex_wild) wild |= mask_end(A.ex_wild, pa);
-  if (T.ex_wild) wild |= mask_end(T.ex_wild, pt);
-  if (wild) mm &= ~spread2(wild);
+  if constexpr (SA::kExc && ST::kExc) if (A.ex_nul || T.ex_nul || A.ex_wild || T.ex_wild) {
+    if (A.ex_nul) mm |= spread2(mask_end(A.ex_nul, pa));
+    if (T.ex_nul) mm |= spread2(mask_end(T.ex_nul, pt));
+    uint32_t wild = 0;
+    if (A.ex_wild) wild |= mask_end(A.ex_wild, pa);
+    if (T.ex_wild) wild |= mask_end(T.ex_wild, pt);
+    if (wild) mm &= ~spread2(wild);
+  }
   return mm;
 }
 
 // How far A[ra..] and T[rt..] agree, going forward, at most lim bases.
-__device__ __forceinline__ int32_t slide_fwd(const Strand &A, int32_t ra, const Strand &T,
-                                             int32_t rt, int32_t lim) {
+template <typename SA, typename ST>
+__device__ __forceinline__ int32_t slide_fwd(const SA &A, int32_t ra, const ST &T, int32_t rt,
+                                             int32_t lim) {
   int32_t n = 0;
   while (n < lim) {
     uint64_t mm = mismatch_fwd(A, ra + n, T, rt + n);
@@ -138,8 +162,9 @@ __device__ __forceinline__ int32_t slide_fwd(const Strand &A, int32_t ra, const 
 }
 
 // How far A[ra], A[ra-1], .. and T[rt], T[rt-1], .. agree, at most lim bases.
-__device__ __forceinline__ int32_t slide_bwd(const Strand &A, int32_t ra, const Strand &T,
-                                             int32_t rt, int32_t lim) {
+template <typename SA, typename ST>
+__device__ __forceinline__ int32_t slide_bwd(const SA &A, int32_t ra, const ST &T, int32_t rt,
+                                             int32_t lim) {
   int32_t n = 0;
   while (n < lim) {
     uint64_t mm = mismatch_bwd(A, ra - n, T, rt - n);

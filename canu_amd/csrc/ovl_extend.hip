@@ -28,6 +28,9 @@ struct ExtendArgs {
   uint32_t npairs;
   Node *pnodes;                 // Len < 0 marks a node removed from its list
   uint32_t *pair_next;
+  const uint32_t *list;   // non-null: process pairs[list[0 .. npairs)] instead of pairs[0 .. npairs)
+  uint32_t *defer;        // staged kernel: pairs with 'n' bases go here for the generic kernel
+  uint32_t *ndefer;
   const int32_t *error_bound;   // ceil(i * maxErate), i <= AS_MAX_READLEN
   const int32_t *match_limit;   // Edit_Match_Limit[e]
   int32_t max_errors;
@@ -47,7 +50,11 @@ struct ExtendArgs {
   uint32_t out_cap;
   unsigned long long *stats;    // 0 without 1 with 2 skipped 3 multi 4 total 5 contained 6 dovetail
   uint32_t *overflow;
+  unsigned long long *dbg;      // optional counters (null: off)
 };
+
+// debug counters (dbg != null): 0 ped calls 1 rows 2 chunks 3 slide words 4 tb steps
+// 5 process iterations 6 ped cycles 7 tb cycles 8 pairs 9 max rows in one ped
 
 #define TB_ROWS 16
 #define TB_W    (2 * TB_ROWS + 3)
@@ -72,30 +79,81 @@ __device__ __forceinline__ void wave_argmax(int32_t &v, int32_t &d) {
   }
 }
 
+struct WaveMem {
+  int32_t *rows;      // global: band-compact log of every row (read by the traceback)
+  int32_t *rowdir;    // global: (offset, lo) per row
+  lds_i32 *lrow;      // LDS: two row buffers of wcap ints (previous / current row)
+  int32_t  wcap;
+  lds_i32 *tbw;       // LDS: traceback window
+  lds_i32 *ldc;       // LDS: Left_Delta cache for Lies_On_Alignment
+  int32_t  ldcap;
+  const lds_i32 *mlim;  // LDS: Edit_Match_Limit[0 .. e_cap+1], shared by the block
+};
+
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#define OVL_REG_CHUNKS 2      // row chunks (x64 diagonals) kept in registers
+
 // Greedy prefix edit distance of A against a prefix of T (m <= n).
 // DIR=+1: A[i] = A.w[a0+i], T[i] = T.w[t0+i]   (forward.C:103)
 // DIR=-1: A[i] = A.w[a0-i], T[i] = T.w[t0-i]   (reverse.C:119)
-// The traceback (Set_Right_Delta / Set_Left_Delta) writes the raw delta stack to dst.
-template <int DIR>
-__device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int32_t m,
-                           const Strand &T, int32_t t0, int32_t n, int32_t limit,
-                           int32_t *rows, int32_t *rowdir, int32_t *dst, int32_t *tbw,
-                           uint32_t lane) {
+// Row e (error level) is computed for all its diagonals at once, 64 per wave step; the
+// end test, the Edit_Match_Limit pruning (both sides) and the running longest row are
+// wave ballots / reductions over values that stay in registers.  The row is kept in LDS
+// for the next level and appended to a global log the traceback reads.
+template <int DIR, typename SS>
+__device__ __forceinline__ int32_t ped_slide(const SS &A, int32_t a0, int32_t m, const SS &T,
+                                             int32_t t0, int32_t n, int32_t r, int32_t d) {
+  int32_t lim = m - r;
+  int32_t l2 = n - r - d;
+  if (l2 < lim) lim = l2;
+  if (lim <= 0) return 0;
+  if (DIR > 0) return slide_fwd(A, a0 + r, T, t0 + r + d, lim);
+  return slide_bwd(A, a0 - r, T, t0 - r - d, lim);
+}
+
+// Max over the 64 lanes: DPP row shifts within 16-lane rows, then row broadcasts.
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+  const int32_t NEG = (int32_t)0x80000000;
+  int32_t t;
+  t = __builtin_amdgcn_update_dpp(NEG, v, 0x111, 0xf, 0xf, false); v = v > t ? v : t;
+  t = __builtin_amdgcn_update_dpp(NEG, v, 0x112, 0xf, 0xf, false); v = v > t ? v : t;
+  t = __builtin_amdgcn_update_dpp(NEG, v, 0x114, 0xf, 0xf, false); v = v > t ? v : t;
+  t = __builtin_amdgcn_update_dpp(NEG, v, 0x118, 0xf, 0xf, false); v = v > t ? v : t;
+  t = __builtin_amdgcn_update_dpp(NEG, v, 0x142, 0xa, 0xf, false); v = v > t ? v : t;
+  t = __builtin_amdgcn_update_dpp(NEG, v, 0x143, 0xc, 0xf, false); v = v > t ? v : t;
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
+template <int DIR, typename SS>
+__device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const SS &A, int32_t a0, int32_t m,
+                           const SS &T, int32_t t0, int32_t n, int32_t limit,
+                           const WaveMem &WM, int32_t *dst, uint32_t lane) {
+  int32_t *rows = WM.rows, *rowdir = WM.rowdir;
+  lds_i32 *tbw = WM.tbw;
+  const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;
   out.nd = 0;
-  auto slide = [&](int32_t r, int32_t d) -> int32_t {
-    int32_t lim = m - r;
-    int32_t l2 = n - r - d;
-    if (l2 < lim) lim = l2;
-    if (lim <= 0) return 0;
-    if (DIR > 0) return slide_fwd(A, a0 + r, T, t0 + r + d, lim);
-    return slide_bwd(A, a0 - r, T, t0 - r - d, lim);
-  };
+  unsigned long long dbg_rows = 0, dbg_chunks = 0;
+  unsigned long long t_start = X.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  // the scratch is sized for e_cap rows of width <= 2e+5 (ovl_api.hip), so the row loop
+  // needs no capacity checks
+  if (limit > X.e_cap - 2) {
+    if (lane == 0) atomicOr(X.overflow, 8u);
+    out.err = 0; out.a_len = 0; out.t_len = 0; out.mte = 0; out.nd = -1;
+    return out;
+  }
 
-  int32_t row0 = (m > 0) ? slide(0, 0) : 0;
-  if (lane == 0) { rowdir[0] = 0; rowdir[1] = -2; rows[2] = row0; }
-  int32_t cursor = 5;
+  int32_t row0 = (m > 0) ? ped_slide<DIR>(A, a0, m, T, t0, n, 0, 0) : 0;
+  row0 = __builtin_amdgcn_readfirstlane(row0);
+  lds_i32 *lbuf0 = WM.lrow, *lbuf1 = WM.lrow + WM.wcap;
+  if (lane == 0) { rowdir[0] = 0; rowdir[1] = -2; rows[2] = row0; lbuf0[2] = row0; }
+  lds_sync();
   if (row0 == m) {
     out.err = 0; out.a_len = m; out.t_len = m; out.mte = 1;
     out.leftover = m;          // reverse(): Leftover = m on an exact match
@@ -106,63 +164,78 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
   double  max_score = 0.0;
   int32_t max_score_len = 0, max_score_best_d = 0, max_score_best_e = 0;
   int32_t best_d = 0, best_e = 0, longest = 0;
-  int32_t left = 0, right = 0;
+  int32_t left = 0, right = 0, cursor = 5;
   int32_t prev_off = 0, prev_lo = -2;
   int32_t tb_e = -1, tb_d = 0;
   bool finished = false;
+  lds_i32 *lprev = lbuf0;
+  const double bmv = X.branch_match_value;
   const bool partial = X.partial != 0;
+  const int32_t mbed = X.min_branch_end_dist;
+  const double mbts = X.min_branch_tail_slope;
 
-  int32_t e;
-  for (e = 1; e <= limit; e++) {
+  for (int32_t e = 1; e <= limit; e++) {
+    const int32_t ML = WM.mlim[e];             // LDS: no global load in the row loop
     left = (left - 1 > -e) ? left - 1 : -e;
     right = (right + 1 < e) ? right + 1 : e;
-    int32_t *prev = rows + prev_off - prev_lo;
-    if (lane == 0) { prev[left] = -2; prev[left - 1] = -2; prev[right] = -2; prev[right + 1] = -2; }
-    int32_t lo = left - 2, width = right - left + 5;
-    int32_t off = cursor;
+    const int32_t lo = left - 2, width = right - left + 5, off = cursor;
     cursor += width;
-    if ((uint64_t)cursor > X.rows_cap || e > X.e_cap) {
-      if (lane == 0) atomicOr(X.overflow, 8u);
-      out.err = 0; out.a_len = 0; out.t_len = 0; out.mte = 0; out.nd = -1;
-      return out;
+    // sentinels around the new band in row e-1 (LDS copy and the traceback log)
+    if (lane < 4) {
+      int32_t d = (lane == 0) ? left : (lane == 1) ? left - 1 : (lane == 2) ? right : right + 1;
+      lprev[d - prev_lo] = -2;
+      rows[prev_off + d - prev_lo] = -2;
     }
     if (lane == 0) { rowdir[2 * e] = off; rowdir[2 * e + 1] = lo; }
-    int32_t *cur = rows + off - lo;
-    vm_sync();
+    lds_i32 *lcur = (e & 1) ? lbuf1 : lbuf0;
+    const lds_i32 *prev = lprev - prev_lo;      // index by diagonal
+    lds_i32 *cur = lcur - lo;
+    int32_t *glog = rows + off - lo;
+    lds_sync();
 
-    int32_t end_d = 0x7fffffff, end_row = 0;
+    // ---- the row: 64 diagonals per step ------------------------------------------
+    int32_t end_d = NONE, end_row = 0, nl = NONE, nr = NEG;
+    int32_t rv0 = NEG, rv1 = NEG;
+    int32_t nch = 0;
     for (int32_t c = left; c <= right; c += 64) {
-      int32_t d = c + (int32_t)lane;
-      bool act = d <= right;
-      int32_t r = 0;
-      if (act) {
-        r = 1 + prev[d];
-        int32_t j = prev[d - 1];
-        if (j > r) r = j;
-        j = 1 + prev[d + 1];
-        if (j > r) r = j;
-        if (r < m && r + d < n) r += slide(r, d);
-        cur[d] = r;
-      }
-      uint64_t endm = __ballot(act && (r == m || r + d == n));
+      const int32_t d = c + (int32_t)lane;
+      const bool act = d <= right;
+      const int32_t dd = act ? d : right;
+      int32_t r = 1 + prev[dd];
+      int32_t j = prev[dd - 1];
+      r = j > r ? j : r;
+      j = 1 + prev[dd + 1];
+      r = j > r ? j : r;
+      if (act && r < m && r + d < n) r += ped_slide<DIR>(A, a0, m, T, t0, n, r, d);
+      if (act) { cur[d] = r; glog[d] = r; }
+      if (nch == 0) rv0 = act ? r : NEG;
+      if (nch == 1) rv1 = act ? r : NEG;
+      nch++;
+      const uint64_t endm = __ballot(act && (r == m || r + d == n));
+      // pruning test (forward.C:236-252): left and right use the same predicate
+      const uint64_t km = __ballot(act && ((d < 0) ? !(r < ML) : !(r + d < ML)));
       if (endm) {
-        uint32_t l = __builtin_ctzll(endm);
-        end_d = c + (int32_t)l;
-        end_row = __shfl(r, l);
+        const int32_t l = (int32_t)__builtin_ctzll(endm);
+        end_d = c + l;
+        end_row = __builtin_amdgcn_readlane(r, l);
         break;
       }
+      if (km) {
+        if (nl == NONE) nl = c + (int32_t)__builtin_ctzll(km);
+        nr = c + 63 - (int32_t)__builtin_clzll(km);
+      }
     }
-    vm_sync();
+    dbg_rows++;
+    dbg_chunks += nch;
+    lds_sync();
 
-    if (end_d != 0x7fffffff) {
-      double  score = end_row * X.branch_match_value - e;
+    if (end_d != NONE) {
+      double  score = end_row * bmv - e;
       int32_t tail_len = end_row - max_score_len;
       double  slope = (double)(max_score - score) / tail_len;
       bool    abort_here = false;
       if (partial && score < max_score) abort_here = true;
-      if (e > X.min_branch_end_dist / 2 && tail_len >= X.min_branch_end_dist &&
-          slope >= X.min_branch_tail_slope)
-        abort_here = true;
+      if (e > mbed / 2 && tail_len >= mbed && slope >= mbts) abort_here = true;
       if (abort_here) {
         out.err = max_score_best_e;
         out.a_len = max_score_len;
@@ -174,8 +247,7 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
         // forward.C:212 -- force the last error to be a mismatch rather than an insertion
         if (DIR > 0 && end_row == m && 1 + prev[d + 1] == end_row && d < right) {
           d++;
-          if (lane == 0) cur[d] = end_row;
-          vm_sync();
+          if (lane == 0) { cur[d] = end_row; glog[d] = end_row; }
         }
         out.err = e;
         out.a_len = end_row;
@@ -187,45 +259,27 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
       break;
     }
 
-    // Edit_Match_Limit pruning (forward.C:236-252)
-    int32_t ML = X.match_limit[e];
-    int32_t nl = 0x7fffffff;
-    for (int32_t c = left; c <= right; c += 64) {
-      int32_t d = c + (int32_t)lane;
-      bool keep = false;
-      if (d <= right) {
-        int32_t v = cur[d];
-        keep = (d < 0) ? !(v < ML) : !(v + d < ML);
-      }
-      uint64_t km = __ballot(keep);
-      if (km) { nl = c + (int32_t)__builtin_ctzll(km); break; }
-    }
-    if (nl == 0x7fffffff) break;           // Left > Right
-    int32_t nr = nl;
-    for (int32_t c = right; c >= nl; c -= 64) {
-      int32_t d = c - (int32_t)lane;
-      bool keep = false;
-      if (d >= nl) {
-        int32_t v = cur[d];
-        keep = (d > 0) ? !(v + d < ML) : !(v < ML);
-      }
-      uint64_t km = __ballot(keep);
-      if (km) { nr = c - (int32_t)__builtin_ctzll(km); break; }
-    }
+    if (nl == NONE) break;                     // Left > Right
     left = nl;
     right = nr;
 
-    int32_t bv = -0x7fffffff, bd = 0x7fffffff;
-    for (int32_t c = left; c <= right; c += 64) {
-      int32_t d = c + (int32_t)lane;
-      if (d <= right) {
-        int32_t v = cur[d];
-        if (v > bv || (v == bv && d < bd)) { bv = v; bd = d; }
+    // longest row over the pruned band, first diagonal on ties (forward.C:256-261)
+    int32_t bv = NEG, bd = NONE;
+    for (int32_t ci = 0; ci < nch; ci++) {
+      const int32_t c = lo + 2 + 64 * ci;
+      if (c > right) break;
+      if (c + 63 < left) continue;
+      const int32_t d = c + (int32_t)lane;
+      int32_t v = (ci == 0) ? rv0 : (ci == 1) ? rv1 : cur[d <= right ? d : right];
+      v = (d >= left && d <= right) ? v : NEG;
+      const int32_t cm = wave_max(v);
+      if (cm > bv) {
+        bv = cm;
+        bd = c + (int32_t)__builtin_ctzll(__ballot(v == cm));
       }
     }
-    wave_argmax(bv, bd);
     if (bv > longest) { longest = bv; best_d = bd; best_e = e; }
-    double score = longest * X.branch_match_value - e;
+    double score = longest * bmv - e;
     if (score > max_score) {
       max_score = score;
       max_score_len = longest;
@@ -234,6 +288,7 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
     }
     prev_off = off;
     prev_lo = lo;
+    lprev = lcur;
   }
   if (!finished) {
     out.err = max_score_best_e;
@@ -243,7 +298,9 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
     tb_e = max_score_best_e; tb_d = max_score_best_d;
   }
 
+  unsigned long long t_mid = X.dbg ? __builtin_amdgcn_s_memtime() : 0;
   // ---- traceback (Set_Right_Delta / Set_Left_Delta loop), 16-row LDS windows ---------
+  vm_sync();                                  // the row log is complete
   int32_t d = tb_d;
   int32_t last;
   {
@@ -255,23 +312,20 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
     int32_t kl = kh - TB_ROWS + 1;
     if (kl < 1) kl = 1;
     int32_t dc = d;
-    // stage rows kl-1 .. kh-1, diagonals dc-(TB_ROWS+1) .. dc+(TB_ROWS+1)
     int32_t nrows = kh - kl + 1;
     for (int32_t i = lane; i < nrows * TB_W; i += 64) {
       int32_t rr = i / TB_W, w = i - rr * TB_W;
       int32_t row = kl - 1 + rr;
       int32_t ro = rowdir[2 * row], rl = rowdir[2 * row + 1];
-      int32_t width = rowdir[2 * (row + 1)] - ro;
+      int32_t rwidth = rowdir[2 * (row + 1)] - ro;
       int32_t dd = dc - (TB_ROWS + 1) + w;
       int32_t idx = dd - rl;
-      tbw[i] = (idx >= 0 && idx < width) ? rows[ro + idx] : -3;
+      tbw[i] = (idx >= 0 && idx < rwidth) ? rows[ro + idx] : -3;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    lds_sync();
     if (lane == 0) {
       for (int32_t kk = kh; kk >= kl; kk--) {
-        const int32_t *prow = tbw + (kk - 1 - (kl - 1)) * TB_W - (dc - (TB_ROWS + 1));
+        const lds_i32 *prow = tbw + (kk - 1 - (kl - 1)) * TB_W - (dc - (TB_ROWS + 1));
         int32_t from = d, mx = 1 + prow[d], j;
         if ((j = prow[d - 1]) > mx) { from = d - 1; mx = j; }
         if ((j = 1 + prow[d + 1]) > mx) { from = d + 1; mx = j; }
@@ -289,10 +343,20 @@ __device__ PedOut wave_ped(const ExtendArgs &X, const Strand &A, int32_t a0, int
     d = __shfl(d, 0);
     last = __shfl(last, 0);
     nd = __shfl(nd, 0);
-    __builtin_amdgcn_wave_barrier();
+    lds_sync();
   }
   out.leftover = last;
   out.nd = nd;
+  if (X.dbg && lane == 0) {
+    unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    atomicAdd(&X.dbg[0], 1ull);
+    atomicAdd(&X.dbg[1], dbg_rows);
+    atomicAdd(&X.dbg[2], dbg_chunks);
+    atomicAdd(&X.dbg[4], (unsigned long long)tb_e);
+    atomicAdd(&X.dbg[6], t_mid - t_start);
+    atomicAdd(&X.dbg[7], t_end - t_mid);
+    atomicMax(&X.dbg[9], dbg_rows);
+  }
   return out;
 }
 
@@ -311,10 +375,11 @@ struct ExtOut {
 };
 
 // Extend_Alignment (prefixEditDistance-extend.C:86).  Leaves the merged Left_Delta in LD.
-__device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const Strand &S,
-                                   int32_t S_Len, const Strand &T, int32_t T_Len,
-                                   int32_t *rows, int32_t *rowdir, int32_t *stk, int32_t *RD,
-                                   int32_t *LD, int32_t *tbw, uint32_t lane) {
+template <typename SS>
+__device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS &S,
+                                   int32_t S_Len, const SS &T, int32_t T_Len,
+                                   const WaveMem &WM, int32_t *stk, int32_t *RD,
+                                   int32_t *LD, uint32_t lane) {
   ExtOut r;
   int32_t right_errors = 0, left_errors = 0, leftover = 0;
   int32_t rmte = 1, lmte = 1;
@@ -332,13 +397,12 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const Str
     S_Hi = 0; T_Hi = 0; rmte = 1;
   } else {
     bool s_first = S_Right_Len <= T_Right_Len;
-    PedOut po;
-    if (s_first)
-      po = wave_ped<1>(X, S, S_Right_Begin, S_Right_Len, T, T_Right_Begin, T_Right_Len,
-                       error_limit, rows, rowdir, stk, tbw, lane);
-    else
-      po = wave_ped<1>(X, T, T_Right_Begin, T_Right_Len, S, S_Right_Begin, S_Right_Len,
-                       error_limit, rows, rowdir, stk, tbw, lane);
+    SS A = s_first ? S : T, B = s_first ? T : S;
+    int32_t a0 = s_first ? S_Right_Begin : T_Right_Begin;
+    int32_t b0 = s_first ? T_Right_Begin : S_Right_Begin;
+    int32_t am = s_first ? S_Right_Len : T_Right_Len;
+    int32_t bn = s_first ? T_Right_Len : S_Right_Len;
+    PedOut po = wave_ped<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
     right_errors = po.err;
     rmte = po.mte;
     if (s_first) { S_Hi = po.a_len; T_Hi = po.t_len; }
@@ -366,18 +430,15 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const Str
     S_Lo = 0; T_Lo = 0; lmte = 1;
   } else {
     bool s_first = S_Right_Begin <= T_Right_Begin;
-    PedOut po;
     int32_t lim = error_limit - right_errors;
-    if (s_first)
-      po = wave_ped<-1>(X, S, S_Left_Begin, S_Left_Begin + 1, T, T_Left_Begin, T_Left_Begin + 1,
-                        lim, rows, rowdir, LD, tbw, lane);
-    else
-      po = wave_ped<-1>(X, T, T_Left_Begin, T_Left_Begin + 1, S, S_Left_Begin, S_Left_Begin + 1,
-                        lim, rows, rowdir, LD, tbw, lane);
+    SS A = s_first ? S : T, B = s_first ? T : S;
+    int32_t a0 = s_first ? S_Left_Begin : T_Left_Begin;
+    int32_t b0 = s_first ? T_Left_Begin : S_Left_Begin;
+    PedOut po = wave_ped<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
     left_errors = po.err;
     lmte = po.mte;
     int32_t a_end = -po.a_len, t_end = -po.t_len;
-    int32_t n_t = s_first ? T_Left_Begin + 1 : S_Left_Begin + 1;     // reverse()'s n
+    int32_t n_t = b0 + 1;                                  // reverse()'s n
     leftover = po.leftover;
     if (po.nd >= 0) {
       ld_len = po.nd;
@@ -554,16 +615,214 @@ __device__ bool lies_on_alignment(int32_t start, int32_t offset, int32_t s_lo, i
   return abs(new_diag - diag) <= SHIFT_SLACK;
 }
 
+#define OVL_SCAP_WORDS 352          // LDS strand cache: up to 11,232 bases per strand
+#define OVL_LDCAP 512                 // LDS Left_Delta cache
+
+// Process_Matches (Process_String_Overlaps.C:400) for one pair, strands S (query, in its
+// orientation) and T (target, forward) -- global or LDS-staged.
+template <typename SS>
+__device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &un,
+                             const SS &S, const SS &T, const WaveMem &WM, int32_t *stk,
+                             int32_t *RD, int32_t *LD, unsigned long long *st, uint32_t lane) {
+  uint32_t S_ID = X.R.first_iid + un.r, T_ID = X.R.first_iid + P.tgt;
+  int32_t S_Len = S.len, t_len = T.len;
+  Node *nodes = X.pnodes + P.node_off;
+  int32_t nn = (int32_t)P.node_cnt;
+  uint32_t trf = X.R.flags[P.tgt];
+  bool consistent = P.flags & 1u;
+  bool lscr = P.flags & 2u, rscr = P.flags & 4u;
+
+  // computeMinimumKmers (Process_String_Overlaps.C:81), Process_String_Olaps:725
+  if (X.filter_by_kmer_count != 0) {
+    double ovl_len = (double)(P.diag_end - P.diag_bgn);
+    if (ovl_len < 0) ovl_len = -ovl_len;
+    uint64_t expct = 0;
+    if (!(ovl_len < (double)X.k))
+      expct = (uint64_t)(int)floor(X.minkmer_exp * (ovl_len - X.k + 1));
+    uint64_t mk = expct > X.filter_by_kmer_count ? expct : X.filter_by_kmer_count;
+    if (mk > (uint64_t)P.diag_ct) { st[2]++; return; }
+  }
+
+  // hopeless check (:433)
+  if (X.use_hopeless && nn == 1 && !X.partial) {
+    Node h = nodes[0];
+    int32_t s_head = h.Start, t_head = h.Offset;
+    bool hopeless = false;
+    if (s_head <= t_head) {
+      if (s_head > 90 && !lscr) hopeless = true;
+    } else {
+      if (t_head > 90 && !(trf & 2u)) hopeless = true;
+    }
+    int32_t s_tail = S_Len - s_head - h.Len + 1;
+    int32_t t_tail = t_len - t_head - h.Len + 1;
+    if (s_tail <= t_tail) {
+      if (s_tail > 90 && !rscr) hopeless = true;
+    } else {
+      if (t_tail > 90 && !(trf & 4u)) hopeless = true;
+    }
+    if (hopeless) { st[0]++; return; }
+  }
+  if (X.dbg && lane == 0) atomicAdd(&X.dbg[8], 1ull);
+
+  OlapInfo ol[MAX_DISTINCT_OLAPS];
+  int32_t ct = 0;
+  int32_t kind = K_NONE, S_Lo = 0, S_Hi = 0, T_Lo = 0, T_Hi = 0;
+  int32_t remaining = nn;
+  int32_t ld_len = 0;
+  while (remaining > 0) {
+    // longest remaining match, first in list order on ties (:473-480)
+    int32_t bv = -1, bi = 0x7fffffff;
+    for (int32_t i = lane; i < nn; i += 64) {
+      int32_t L = nodes[i].Len;
+      if (L > bv) { bv = L; bi = i; }
+    }
+    wave_argmax(bv, bi);
+    Node M = nodes[bi];
+    if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
+    ExtOut eo = extend_alignment(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+    kind = eo.kind;
+    S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
+    ld_len = eo.ld_len;
+    if (kind == K_DOVETAIL || X.partial) {
+      if (1 + S_Hi - S_Lo >= X.min_olap_len && 1 + T_Hi - T_Lo >= X.min_olap_len) {
+        int32_t olap_len = 1 + ((S_Hi - S_Lo) < (T_Hi - T_Lo) ? (S_Hi - S_Lo) : (T_Hi - T_Lo));
+        double quality = (double)eo.Errors / olap_len;
+        if (eo.Errors <= X.error_bound[olap_len])
+          add_overlap(X, S_Lo, S_Hi, T_Lo, T_Hi, quality, ld_len, ol, ct);
+      }
+    }
+    if (consistent) break;
+    // drop the longest match and every match on this alignment (:517-531)
+    const int32_t *ldp = LD;
+    if (ld_len <= WM.ldcap) {
+      for (int32_t i = lane; i < ld_len; i += 64) WM.ldc[i] = LD[i];
+      lds_sync();
+      ldp = (const int32_t *)WM.ldc;
+    }
+    int32_t removed = 0;
+    for (int32_t i = lane; i < nn; i += 64) {
+      Node nd = nodes[i];
+      if (nd.Len < 0) continue;
+      bool rm = (i == bi) ||
+                ((kind == K_DOVETAIL || X.partial) && S_Lo - SHIFT_SLACK <= nd.Start &&
+                 nd.Start + nd.Len <= (S_Hi + 1) + SHIFT_SLACK - 1 &&
+                 lies_on_alignment(nd.Start, nd.Offset, S_Lo, T_Lo, ldp, ld_len));
+      if (rm) { nodes[i].Len = -1; removed++; }
+    }
+    for (int s = 32; s > 0; s >>= 1) removed += __shfl_xor(removed, s);
+    remaining -= removed;
+    vm_sync();
+  }
+
+  int32_t outputs = 0;
+  if (ct > 0) {
+    bool del[MAX_DISTINCT_OLAPS] = {false, false, false};
+    if (X.partial) {
+      if (X.unique) {                       // Choose_Best_Partial (:336)
+        int32_t best = 0;
+        double mb0 = (1.0 - ol[0].quality) *
+                     (2 + ol[0].s_hi - ol[0].s_lo + ol[0].t_hi - ol[0].t_lo);
+        for (int32_t i = 1; i < ct; i++) {
+          double mb = (1.0 - ol[i].quality) *
+                      (2 + ol[i].s_hi - ol[i].s_lo + ol[i].t_hi - ol[i].t_lo);
+          if (mb0 < mb || (mb0 == mb && ol[i].quality < ol[best].quality)) best = i;
+        }
+        for (int32_t i = 0; i < ct; i++) del[i] = (i != best);
+      }
+    } else if (X.unique) {                  // Combine_Into_One_Olap (:95)
+      int32_t best = 0;
+      for (int32_t i = 1; i < ct; i++)
+        if (ol[i].quality < ol[best].quality) best = i;
+      for (int32_t i = 0; i < ct; i++) del[i] = (i != best);
+    } else {                                // Merge_Intersecting_Olaps (:153)
+      for (int32_t i = 0; i < ct - 1; i++)
+        for (int32_t j = i + 1; j < ct; j++) {
+          if (del[i] || del[j]) continue;
+          int32_t lo = ol[i].min_diag, hi = ol[i].max_diag;
+          if ((lo <= 0 && ol[j].min_diag > 0) || (lo > 0 && ol[j].min_diag <= 0)) continue;
+          if ((lo >= 0 && ol[j].trb - lo - ol[j].slb >= MIN_INTERSECTION) ||
+              (lo <= 0 && ol[j].srb + lo - ol[j].tlb >= MIN_INTERSECTION) ||
+              (hi >= 0 && ol[j].trb - hi - ol[j].slb >= MIN_INTERSECTION) ||
+              (hi <= 0 && ol[j].srb + hi - ol[j].tlb >= MIN_INTERSECTION)) {
+            int32_t keep, disc;
+            if (ol[i].quality < ol[j].quality) { keep = i; disc = j; del[j] = true; }
+            else                               { keep = j; disc = i; del[i] = true; }
+            if (ol[disc].min_diag < ol[keep].min_diag) ol[keep].min_diag = ol[disc].min_diag;
+            if (ol[disc].max_diag > ol[keep].max_diag) ol[keep].max_diag = ol[disc].max_diag;
+            if (ol[disc].slb < ol[keep].slb) ol[keep].slb = ol[disc].slb;
+            if (ol[disc].srb > ol[keep].srb) ol[keep].srb = ol[disc].srb;
+            if (ol[disc].tlb < ol[keep].tlb) ol[keep].tlb = ol[disc].tlb;
+            if (ol[disc].trb > ol[keep].trb) ol[keep].trb = ol[disc].trb;
+          }
+        }
+    }
+    for (int32_t i = 0; i < ct; i++) {
+      if (del[i]) continue;
+      Rec rec;
+      int32_t bhg = 0;
+      if (X.partial) rec = output_partial(S_ID, T_ID, un.dir, ol[i], S_Len, t_len);
+      else           rec = output_overlap(S_ID, S_Len, un.dir, T_ID, t_len, ol[i], &bhg);
+      if (lane == 0) {
+        uint32_t slot = atomicAdd(X.nout, 1u);
+        if (slot < X.out_cap) X.out[slot] = rec;
+        else atomicOr(X.overflow, 16u);
+      }
+      outputs++;
+      st[4]++;
+      if (!X.partial) {
+        if (bhg <= 0) st[5]++;
+        else          st[6]++;
+      }
+    }
+  }
+  if (outputs == 0) st[0]++;
+  else {
+    st[1]++;
+    if (outputs > 1) st[3]++;
+  }
+}
+
+// Copy a strand's packed words (and the guard) into LDS.  Only exception-free strands are
+// staged: the staged kernel defers pairs with 'n' bases to the generic kernel.
+__device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, uint32_t lane) {
+  int32_t nw = (G.len + 31) / 32 + 1;
+  for (int32_t i = lane; i < nw; i += 64) dst[i] = G.w[i];
+  StrandLP L;
+  L.w = dst;
+  L.len = G.len;
+  return L;
+}
+
+template <bool STAGE>
 __global__ void __launch_bounds__(256) k_extend(ExtendArgs X) {
-  __shared__ int32_t s_tb[4][TB_ROWS * TB_W];
+  extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t gw = blockIdx.x * 4 + wave;
-  int32_t *rows = X.rows + (size_t)gw * X.rows_cap;
-  int32_t *rowdir = X.rowdir + (size_t)gw * 2 * (X.e_cap + 2);
+  uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+  int32_t wcap = 2 * X.e_cap + 8;
+  int32_t mlsz = ((X.e_cap + 2) + 3) & ~3;
+  for (int32_t i = threadIdx.x; i < X.e_cap + 2; i += blockDim.x)
+    s_ext0[i] = (i <= X.max_errors) ? X.match_limit[i] : 0x7fffffff;
+  __syncthreads();
+  lds_i32 *l_ext0 = (lds_i32 *)s_ext0;
+  lds_i32 *s_ext = l_ext0 + mlsz;
+  // per wave: [S words | T words] (u64, 16-B aligned) then rows, traceback, delta cache
+  size_t wave_ints = 4 * OVL_SCAP_WORDS + 2 * wcap + TB_ROWS * TB_W + OVL_LDCAP;
+  wave_ints = (wave_ints + 3) & ~(size_t)3;
+  lds_i32 *wlds = s_ext + wave * (uint32_t)wave_ints;
+  lds_u64 *sw = (lds_u64 *)(wlds);
+  lds_u64 *tw = sw + OVL_SCAP_WORDS;
+  WaveMem WM;
+  WM.rows = X.rows + (size_t)gw * X.rows_cap;
+  WM.rowdir = X.rowdir + (size_t)gw * 2 * (X.e_cap + 2);
+  WM.lrow = wlds + 4 * OVL_SCAP_WORDS;
+  WM.wcap = wcap;
+  WM.tbw = WM.lrow + 2 * wcap;
+  WM.ldc = WM.tbw + TB_ROWS * TB_W;
+  WM.ldcap = OVL_LDCAP;
+  WM.mlim = l_ext0;
   int32_t *stk = X.deltas + (size_t)gw * 4 * (X.e_cap + 8);
   int32_t *RD = stk + (X.e_cap + 8);
   int32_t *LD = RD + (X.e_cap + 8);
-  int32_t *tbw = s_tb[wave];
   unsigned long long st[7] = {0, 0, 0, 0, 0, 0, 0};
 
   for (;;) {
@@ -571,168 +830,26 @@ __global__ void __launch_bounds__(256) k_extend(ExtendArgs X) {
     if (lane == 0) pi = atomicAdd(X.pair_next, 1u);
     pi = __shfl(pi, 0);
     if (pi >= X.npairs) break;
+    if (X.list) pi = X.list[pi];
     PairRec P = X.pairs[pi];
     Unit un = X.units[P.unit];
-    uint32_t S_ID = X.R.first_iid + un.r, T_ID = X.R.first_iid + P.tgt;
     Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
     Strand T = strand_fwd(X.R, P.tgt);
-    int32_t S_Len = S.len, t_len = T.len;
-    Node *nodes = X.pnodes + P.node_off;
-    int32_t nn = (int32_t)P.node_cnt;
-    uint32_t trf = X.R.flags[P.tgt];
-    bool consistent = P.flags & 1u;
-    bool lscr = P.flags & 2u, rscr = P.flags & 4u;
-
-    // computeMinimumKmers (Process_String_Overlaps.C:81), Process_String_Olaps:725
-    if (X.filter_by_kmer_count != 0) {
-      double ovl_len = (double)(P.diag_end - P.diag_bgn);
-      if (ovl_len < 0) ovl_len = -ovl_len;
-      uint64_t expct = 0;
-      if (!(ovl_len < (double)X.k))
-        expct = (uint64_t)(int)floor(X.minkmer_exp * (ovl_len - X.k + 1));
-      uint64_t mk = expct > X.filter_by_kmer_count ? expct : X.filter_by_kmer_count;
-      if (mk > (uint64_t)P.diag_ct) { st[2]++; continue; }
+    if constexpr (STAGE) {
+      // the host launches this variant only when every read fits the strand cache
+      if (S.ex_wild || S.ex_nul || T.ex_wild) {
+        if (lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
+        continue;
+      }
+      StrandLP SL = stage_strand(S, sw, lane);
+      StrandLP TL = stage_strand(T, tw, lane);
+      lds_sync();
+      process_pair(X, P, un, SL, TL, WM, stk, RD, LD, st, lane);
+    } else {
+      (void)sw; (void)tw;
+      process_pair(X, P, un, S, T, WM, stk, RD, LD, st, lane);
     }
-
-    // hopeless check (:433)
-    if (X.use_hopeless && nn == 1 && !X.partial) {
-      Node h = nodes[0];
-      int32_t s_head = h.Start, t_head = h.Offset;
-      bool hopeless = false;
-      if (s_head <= t_head) {
-        if (s_head > 90 && !lscr) hopeless = true;
-      } else {
-        if (t_head > 90 && !(trf & 2u)) hopeless = true;
-      }
-      int32_t s_tail = S_Len - s_head - h.Len + 1;
-      int32_t t_tail = t_len - t_head - h.Len + 1;
-      if (s_tail <= t_tail) {
-        if (s_tail > 90 && !rscr) hopeless = true;
-      } else {
-        if (t_tail > 90 && !(trf & 4u)) hopeless = true;
-      }
-      if (hopeless) { st[0]++; continue; }
-    }
-
-    OlapInfo ol[MAX_DISTINCT_OLAPS];
-    int32_t ct = 0;
-    int32_t kind = K_NONE, S_Lo = 0, S_Hi = 0, T_Lo = 0, T_Hi = 0;
-    int32_t remaining = nn;
-    int32_t ld_len = 0;
-    while (remaining > 0) {
-      // longest remaining match, first in list order on ties (:473-480)
-      int32_t bv = -1, bi = 0x7fffffff;
-      for (int32_t i = lane; i < nn; i += 64) {
-        int32_t L = nodes[i].Len;
-        if (L > bv) { bv = L; bi = i; }
-      }
-      wave_argmax(bv, bi);
-      Node M = nodes[bi];
-      ExtOut eo = extend_alignment(X, M, S, S_Len, T, t_len, rows, rowdir, stk, RD, LD, tbw,
-                                   lane);
-      kind = eo.kind;
-      S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
-      ld_len = eo.ld_len;
-      if (kind == K_DOVETAIL || X.partial) {
-        if (1 + S_Hi - S_Lo >= X.min_olap_len && 1 + T_Hi - T_Lo >= X.min_olap_len) {
-          int32_t olap_len = 1 + ((S_Hi - S_Lo) < (T_Hi - T_Lo) ? (S_Hi - S_Lo) : (T_Hi - T_Lo));
-          double quality = (double)eo.Errors / olap_len;
-          if (eo.Errors <= X.error_bound[olap_len])
-            add_overlap(X, S_Lo, S_Hi, T_Lo, T_Hi, quality, ld_len, ol, ct);
-        }
-      }
-      if (consistent) break;
-      // drop the longest match and every match on this alignment (:517-531)
-      int32_t removed = 0;
-      for (int32_t i = lane; i < nn; i += 64) {
-        Node nd = nodes[i];
-        if (nd.Len < 0) continue;
-        bool rm = (i == bi) ||
-                  ((kind == K_DOVETAIL || X.partial) && S_Lo - SHIFT_SLACK <= nd.Start &&
-                   nd.Start + nd.Len <= (S_Hi + 1) + SHIFT_SLACK - 1 &&
-                   lies_on_alignment(nd.Start, nd.Offset, S_Lo, T_Lo, LD, ld_len));
-        if (rm) { nodes[i].Len = -1; removed++; }
-      }
-      for (int s = 32; s > 0; s >>= 1) removed += __shfl_xor(removed, s);
-      remaining -= removed;
-      vm_sync();
-    }
-
-    int32_t outputs = 0;
-    if (ct > 0) {
-      bool del[MAX_DISTINCT_OLAPS] = {false, false, false};
-      if (X.partial) {
-        if (X.unique) {                       // Choose_Best_Partial (:336)
-          int32_t best = 0;
-          double mb0 = (1.0 - ol[0].quality) *
-                       (2 + ol[0].s_hi - ol[0].s_lo + ol[0].t_hi - ol[0].t_lo);
-          for (int32_t i = 1; i < ct; i++) {
-            double mb = (1.0 - ol[i].quality) *
-                        (2 + ol[i].s_hi - ol[i].s_lo + ol[i].t_hi - ol[i].t_lo);
-            if (mb0 < mb || (mb0 == mb && ol[i].quality < ol[best].quality)) best = i;
-          }
-          for (int32_t i = 0; i < ct; i++) del[i] = (i != best);
-        }
-      } else if (X.unique) {                  // Combine_Into_One_Olap (:95)
-        int32_t best = 0;
-        int32_t mnd = ol[0].min_diag, mxd = ol[0].max_diag;
-        int32_t slb = ol[0].slb, srb = ol[0].srb, tlb = ol[0].tlb, trb = ol[0].trb;
-        for (int32_t i = 1; i < ct; i++) {
-          if (ol[i].quality < ol[best].quality) best = i;
-          if (ol[i].min_diag < mnd) mnd = ol[i].min_diag;
-          if (ol[i].max_diag > mxd) mxd = ol[i].max_diag;
-          if (ol[i].slb < slb) slb = ol[i].slb;
-          if (ol[i].srb > srb) srb = ol[i].srb;
-          if (ol[i].tlb < tlb) tlb = ol[i].tlb;
-          if (ol[i].trb > trb) trb = ol[i].trb;
-        }
-        for (int32_t i = 0; i < ct; i++) del[i] = (i != best);
-      } else {                                // Merge_Intersecting_Olaps (:153)
-        for (int32_t i = 0; i < ct - 1; i++)
-          for (int32_t j = i + 1; j < ct; j++) {
-            if (del[i] || del[j]) continue;
-            int32_t lo = ol[i].min_diag, hi = ol[i].max_diag;
-            if ((lo <= 0 && ol[j].min_diag > 0) || (lo > 0 && ol[j].min_diag <= 0)) continue;
-            if ((lo >= 0 && ol[j].trb - lo - ol[j].slb >= MIN_INTERSECTION) ||
-                (lo <= 0 && ol[j].srb + lo - ol[j].tlb >= MIN_INTERSECTION) ||
-                (hi >= 0 && ol[j].trb - hi - ol[j].slb >= MIN_INTERSECTION) ||
-                (hi <= 0 && ol[j].srb + hi - ol[j].tlb >= MIN_INTERSECTION)) {
-              int32_t keep, disc;
-              if (ol[i].quality < ol[j].quality) { keep = i; disc = j; del[j] = true; }
-              else                               { keep = j; disc = i; del[i] = true; }
-              if (ol[disc].min_diag < ol[keep].min_diag) ol[keep].min_diag = ol[disc].min_diag;
-              if (ol[disc].max_diag > ol[keep].max_diag) ol[keep].max_diag = ol[disc].max_diag;
-              if (ol[disc].slb < ol[keep].slb) ol[keep].slb = ol[disc].slb;
-              if (ol[disc].srb > ol[keep].srb) ol[keep].srb = ol[disc].srb;
-              if (ol[disc].tlb < ol[keep].tlb) ol[keep].tlb = ol[disc].tlb;
-              if (ol[disc].trb > ol[keep].trb) ol[keep].trb = ol[disc].trb;
-            }
-          }
-      }
-      for (int32_t i = 0; i < ct; i++) {
-        if (del[i]) continue;
-        Rec rec;
-        int32_t bhg = 0;
-        if (X.partial) rec = output_partial(S_ID, T_ID, un.dir, ol[i], S_Len, t_len);
-        else           rec = output_overlap(S_ID, S_Len, un.dir, T_ID, t_len, ol[i], &bhg);
-        if (lane == 0) {
-          uint32_t slot = atomicAdd(X.nout, 1u);
-          if (slot < X.out_cap) X.out[slot] = rec;
-          else atomicOr(X.overflow, 16u);
-        }
-        outputs++;
-        st[4]++;
-        if (!X.partial) {
-          if (bhg <= 0) st[5]++;
-          else          st[6]++;
-        }
-      }
-    }
-    if (outputs == 0) st[0]++;
-    else {
-      st[1]++;
-      if (outputs > 1) st[3]++;
-    }
+    lds_sync();
   }
   if (lane == 0)
     for (int i = 0; i < 7; i++)

@@ -26,7 +26,7 @@ struct ProbeArgs {
   const uint64_t *rbase;        // per unit: first Probe slot
   uint32_t nunits;
   Probe *out;
-  uint32_t *unit_hits;          // per unit: qualifying occurrences
+  uint32_t *unit_hits;          // per unit: occurrences (upper bound of qualifying hits)
   uint32_t *unit_flags;         // bit1 left_end_screened, bit2 right_end_screened
   uint32_t k;
 };
@@ -90,8 +90,10 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
           if (o < 90) flags |= 2u;
           if (o > 0 && L - (int32_t)o - (int32_t)A.k + 1 < 90) flags |= 4u;
         } else {
+          // whole occurrence list; the chain kernel drops targets with iid <= query
+          // (the qualifying prefix, Find_Overlaps.C:328) as it stages them
           pr.off = e->off;
-          pr.cnt = qualifying(A.X.occ, e->off, c & OVL_CNT_MASK, a_iid);
+          pr.cnt = c & OVL_CNT_MASK;
           hits += pr.cnt;
         }
       }
@@ -136,11 +138,13 @@ struct ChainArgs {
   uint32_t *overflow;           // set when a capacity is exceeded (host retries smaller)
   uint32_t *done_scratch;       // per wave: targets finished in earlier passes
   uint32_t done_cap;
+  unsigned long long *seed_hits; // qualifying occurrences (Add_Ref calls)
 };
 
 struct SlotState {
   uint32_t t;          // target iid (0 = none)
-  int32_t  head;
+  int32_t  head;       // list head index (0 = empty list)
+  Node     hd;         // the head node itself; pool[head] is stale until flushed
   uint32_t nn;
   int32_t  diag_ct, diag_bgn, diag_end;
   uint32_t consistent;
@@ -149,6 +153,7 @@ struct SlotState {
 __device__ __forceinline__ void slot_reset(SlotState &s) {
   s.t = 0; s.head = 0; s.nn = 0; s.diag_ct = 0; s.diag_bgn = 0x7fffffff; s.diag_end = 0;
   s.consistent = 1;
+  s.hd.Offset = s.hd.Len = s.hd.Start = s.hd.Next = 0;
 }
 
 struct WaveAlloc {
@@ -182,50 +187,62 @@ __device__ __forceinline__ int32_t lane_alloc(WaveAlloc &W, const ChainArgs &A, 
 }
 
 // Add_Match (Find_Overlaps.C:79) on the slot's list.  p = occurrence offset in the
-// target, o = window offset in the query.  Returns false if the node pool ran out.
+// target, o = window offset in the query.  The head node lives in registers (s.hd): the
+// common case -- the next window on the head's diagonal -- touches no memory.
 __device__ __forceinline__ void add_match(SlotState &s, int32_t p, int32_t o, int32_t k,
                                           Node *pool, WaveAlloc &W, const ChainArgs &A,
                                           uint32_t lane) {
   int32_t new_diag = p - o;
   int32_t diag = 0, expected_start = 0, num_checked = 0;
-  bool move_to_front = false;
-  int32_t prev = 0, cur = s.head;
-  bool done = false;
-  uint32_t guard = 0;
-  while (cur > 0 && guard++ <= s.nn) {
-    Node nd = pool[cur];
-    expected_start = nd.Start + nd.Len - k + 1;
-    diag = nd.Offset - nd.Start;
-    if (expected_start < o) break;
-    if (expected_start == o) {
-      if (new_diag == diag) {
-        pool[cur].Len = nd.Len + 1;
-        if (move_to_front) {
-          pool[prev].Next = nd.Next;
-          pool[cur].Next = s.head;
-          s.head = cur;
+  if (s.head != 0) {
+    expected_start = s.hd.Start + s.hd.Len - k + 1;
+    diag = s.hd.Offset - s.hd.Start;
+    if (expected_start == o && new_diag == diag) {   // extend the head
+      s.hd.Len++;
+      return;
+    }
+    if (expected_start >= o) {
+      // walk past the head (repeats: several nodes end at this window)
+      bool move_to_front = (expected_start == o);
+      num_checked = 1;
+      int32_t prev = s.head, cur = s.hd.Next;
+      uint32_t guard = 0;
+      while (cur > 0 && guard++ <= s.nn) {
+        Node nd = pool[cur];
+        expected_start = nd.Start + nd.Len - k + 1;
+        diag = nd.Offset - nd.Start;
+        if (expected_start < o) break;
+        if (expected_start == o) {
+          if (new_diag == diag) {
+            nd.Len++;
+            if (move_to_front) {
+              if (prev == s.head) s.hd.Next = nd.Next;
+              else pool[prev].Next = nd.Next;
+              pool[s.head] = s.hd;                   // flush the old head
+              nd.Next = s.head;
+              s.hd = nd;
+              s.head = cur;
+            } else {
+              pool[cur].Len = nd.Len;
+            }
+            return;
+          }
+          move_to_front = true;
         }
-        done = true;
-        break;
+        num_checked++;
+        prev = cur;
+        cur = nd.Next;
       }
-      move_to_front = true;
     }
-    num_checked++;
-    prev = cur;
-    cur = nd.Next;
-  }
-  if (!done) {
-    if (s.head != 0 && (num_checked > 0 || abs(diag - new_diag) > 3 ||
-                        o < expected_start + k - 2))
+    if (num_checked > 0 || abs(diag - new_diag) > 3 || o < expected_start + k - 2)
       s.consistent = 0;
-    int32_t idx = lane_alloc(W, A, lane);
-    if (idx > 0) {
-      Node nn;
-      nn.Offset = p; nn.Len = k; nn.Start = o; nn.Next = s.head;
-      pool[idx] = nn;
-      s.head = idx;
-      s.nn++;
-    }
+  }
+  int32_t idx = lane_alloc(W, A, lane);
+  if (idx > 0) {
+    if (s.head != 0) pool[s.head] = s.hd;            // flush the old head
+    s.hd.Offset = p; s.hd.Len = k; s.hd.Start = o; s.hd.Next = s.head;
+    s.head = idx;
+    s.nn++;
   }
 }
 
@@ -281,7 +298,9 @@ __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32
   if (has && pbase + rank < A.pairs_cap && nbase + incl <= A.pnodes_cap) {
     uint32_t no = nbase + incl - nn;
     uint32_t c = 0;
-    for (int32_t x = s.head; x > 0 && c < nn; c++) {
+    A.pnodes[no] = s.hd;                               // the head, from registers
+    c = 1;
+    for (int32_t x = s.hd.Next; x > 0 && c < nn; c++) {
       Node nd = A.pool[x];
       A.pnodes[no + c] = nd;
       x = nd.Next;
@@ -325,6 +344,7 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
   const int32_t k = (int32_t)A.k;
   uint32_t gw = blockIdx.x * 4 + wave;
   uint32_t *done_list = A.done_scratch + (size_t)gw * A.done_cap;
+  unsigned long long nhits = 0;
 
   for (;;) {
     uint32_t u = 0;
@@ -336,6 +356,7 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
     const Probe *pr = A.probes + A.rbase[u];
     uint32_t uflags = A.unit_flags[u];
     uint32_t ndone = 0;
+    uint32_t a_iid = A.R.first_iid + un.r;
 
     for (uint32_t pass = 0;; pass++) {
       SlotState s0, s1;
@@ -377,6 +398,8 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
           // discover targets (LDS open-addressing set, 128 slots)
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
             uint32_t t = (uint32_t)(hb[idx - p0] >> 32);
+            if (t <= a_iid) continue;            // Find_Overlaps.C:328
+            if (pass == 0) nhits++;
             bool skip = false;
             for (uint32_t q = 0; q < ndone; q++)
               if (done_list[q] == t) { skip = true; break; }
@@ -430,6 +453,8 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
       WAVE_SYNC();
     }
   }
+  for (int d = 32; d > 0; d >>= 1) nhits += __shfl_xor(nhits, d);
+  if (lane == 0 && nhits) atomicAdd(A.seed_hits, nhits);
 }
 
 }  // namespace ovl

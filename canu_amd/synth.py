@@ -88,15 +88,20 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
                 seed: int = 1, sub_frac: float = 0.4, ins_frac: float = 0.3,
                 len_jitter: float = 0.0, n_rate: float = 0.0, n_repeats: int = 0,
                 repeat_len: int = 0, with_quals: bool = False,
-                genome: np.ndarray | None = None) -> ReadSet:
-    """Sample `n_reads` reads of about `read_len` bases from a random genome."""
-    rng = np.random.default_rng(seed)
+                genome: np.ndarray | None = None, read_range: tuple[int, int] | None = None
+                ) -> ReadSet:
+    """Sample `n_reads` reads of about `read_len` bases from a random genome.
+
+    Read i is drawn from its own stream (seed, i), so any sub-range [lo, hi) of the reads
+    can be generated on its own (read_range): ranks build their slice and all-gather."""
     if genome is None:
-        genome = random_genome(rng, genome_len, n_repeats, repeat_len)
+        genome = random_genome(np.random.default_rng(seed), genome_len, n_repeats, repeat_len)
     genome_len = genome.shape[0]
-    lengths = np.empty(n_reads, dtype=np.uint32)
+    lo, hi = read_range if read_range else (0, n_reads)
+    lengths = np.empty(hi - lo, dtype=np.uint32)
     chunks = []
-    for i in range(n_reads):
+    for i in range(lo, hi):
+        rng = np.random.default_rng([seed, i])
         L = read_len
         if len_jitter > 0:
             L = max(64, int(read_len * (1.0 + len_jitter * (2.0 * rng.random() - 1.0))))
@@ -112,15 +117,17 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
             rd = rd.copy()
             rd[m] = ord("N")
         chunks.append(rd)
-        lengths[i] = rd.shape[0]
+        lengths[i - lo] = rd.shape[0]
     bases = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
-    offsets = np.zeros(n_reads, dtype=np.uint64)
-    if n_reads > 1:
+    offsets = np.zeros(hi - lo, dtype=np.uint64)
+    if hi - lo > 1:
         offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
     quals = None
     if with_quals:
-        quals = rng.integers(2, 41, size=bases.shape[0]).astype(np.uint8)
-    return ReadSet(bases=bases, offsets=offsets, lengths=lengths, quals=quals)
+        quals = np.random.default_rng([seed, n_reads, 7]).integers(
+            2, 41, size=bases.shape[0]).astype(np.uint8)
+    return ReadSet(bases=bases, offsets=offsets, lengths=lengths, quals=quals,
+                   first_iid=1 + lo)
 
 
 def profile(name: str, seed: int = 1, **over) -> ReadSet:

@@ -383,6 +383,9 @@ typedef struct { int32_t Offset, Len, Start, Next; } match_node;
 
 enum { OLAP_NONE = 0, LEFT_BRANCH_PT, RIGHT_BRANCH_PT, DOVETAIL };
 
+static uint64_t dbg_extend_calls = 0;
+uint64_t oic_oracle_debug_extend_calls(void) { return dbg_extend_calls; }
+
 /* prefixEditDistance-extend.C:86 Extend_Alignment */
 static int extend_alignment(ped *p, const match_node *M, const char *S, int32_t S_Len,
                             const char *T, int32_t T_Len, int32_t *S_Lo, int32_t *S_Hi,
@@ -397,6 +400,7 @@ static int extend_alignment(ped *p, const match_node *M, const char *S, int32_t 
   int32_t total = (M->Start < M->Offset ? M->Start : M->Offset) + M->Len +
                   (S_Right_Len < T_Right_Len ? S_Right_Len : T_Right_Len);
   int32_t error_limit = t->error_bound[total];
+  dbg_extend_calls++;
 
   p->left_delta_len = 0;
   p->right_delta_len = 0;
