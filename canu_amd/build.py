@@ -26,18 +26,25 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
-        return OUT
+PROF_OUT = os.path.join(OUT_DIR, "libcanu_ovl_prof.so")
+
+
+def build(force: bool = False, verbose: bool = True, profile: bool = False) -> str:
+    """profile=True builds the instrumented variant (in-kernel cycle stamps, OVL_DEBUG=1
+    prints them) as libcanu_ovl_prof.so; load it with CANU_OVL_LIB."""
+    out = PROF_OUT if profile else OUT
+    if not force and not profile and not needs_build():
+        return out
     os.makedirs(OUT_DIR, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *HIPCC_FLAGS, "-o", OUT + ".tmp", os.path.join(CSRC, "ovl_api.hip")]
+    extra = ["-DOVL_PROFILE"] if profile else []
+    cmd = [hipcc, *HIPCC_FLAGS, *extra, "-o", out + ".tmp", os.path.join(CSRC, "ovl_api.hip")]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, profile="--profile" in sys.argv)

@@ -587,7 +587,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   int32_t e_cap = c->h_error_bound[std::min<uint32_t>(c->max_len, AS_MAX_READLEN)] + 2;
   uint64_t rows_cap = (uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64;
   uint64_t per_wave = rows_cap * 4 + 8ull * (e_cap + 2) + 16ull * (e_cap + 8);
-  uint32_t ext_waves = 16u * c->n_cu;
+  uint32_t ext_waves = 24u * c->n_cu;
   uint64_t budget = 24ull << 30;
   while (ext_waves > 256 && (uint64_t)ext_waves * per_wave > budget) ext_waves /= 2;
   DBuf<int32_t> d_rows, d_rowdir, d_deltas;
@@ -595,13 +595,18 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
       d_rowdir.alloc((size_t)2 * (e_cap + 2) * ext_waves) ||
       d_deltas.alloc((size_t)4 * (e_cap + 8) * ext_waves))
     return fail(OVL_ERR_OOM, "extension scratch");
-  // LDS per extension wave: two row buffers + the traceback window (ovl_extend.hip)
-  size_t ext_lds_wave = 4ull * (((4ull * OVL_SCAP_WORDS + 2ull * (2 * e_cap + 8) + TB_ROWS * TB_W +
-                                  OVL_LDCAP) + 3) & ~3ull);
-  uint32_t ext_wpb = (4 * ext_lds_wave <= 80 * 1024) ? 4 : (2 * ext_lds_wave <= 80 * 1024) ? 2 : 1;
-  if (ext_lds_wave > 160 * 1024)
+  // LDS per extension wave (ovl_extend.hip k_extend).  Generic kernel: two row buffers, the
+  // traceback window and the delta cache.  Staged kernel: both strands and a scratch.
+  const size_t ml_lds = 4ull * (((e_cap + 2) + 3) & ~3);
+  size_t gen_lds_wave = 4ull * ((2ull * (2 * e_cap + 8) + TB_ROWS * TB_W + OVL_LDCAP + 3) & ~3ull);
+  uint32_t gen_wpb = (4 * gen_lds_wave <= 80 * 1024) ? 4 : (2 * gen_lds_wave <= 80 * 1024) ? 2 : 1;
+  if (gen_lds_wave + ml_lds > 160 * 1024)
     return fail(OVL_ERR_UNSUPPORTED, "error limit %d needs more LDS than a CU has", e_cap);
-  ext_waves = (ext_waves / ext_wpb) * ext_wpb;
+  int32_t sw_words = (int32_t)((((uint64_t)c->max_len + 31) / 32 + 2) & ~1ull);
+  size_t stg_lds_wave = 4ull * (4ull * sw_words + OVL_SCR);
+  const uint32_t stg_wpb = 4;
+  bool staged = stg_lds_wave * stg_wpb + ml_lds <= 64 * 1024;
+  ext_waves = (ext_waves / 4) * 4;
   uint32_t chain_waves = 16u * c->n_cu;
   const uint32_t DONE_CAP = 4096;
   if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");
@@ -723,6 +728,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.rowdir = d_rowdir.p;
     EA.deltas = d_deltas.p;
     EA.e_cap = e_cap;
+    EA.sw_words = sw_words;
     // output capacity: grow if this batch could exceed it (<= 3 records per pair)
     uint64_t need = c->nout + 3ull * npairs;
     if (need > c->d_out.n) {
@@ -744,7 +750,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.dbg = nullptr;
     if (getenv("OVL_DEBUG")) {
       static DBuf<unsigned long long> dbgbuf;
-      if (!dbgbuf.p) { dbgbuf.alloc(16); (void)hipMemset(dbgbuf.p, 0, 128); }
+      if (!dbgbuf.p) { (void)dbgbuf.alloc(16); (void)hipMemset(dbgbuf.p, 0, 128); }
       EA.dbg = dbgbuf.p;
       dbg_ptr_for_print = dbgbuf.p;
     }
@@ -753,18 +759,20 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.ndefer = d_ctr.p + 8;
     HIPC(hipEventRecord(c->ev[6], s));
     if (npairs) {
-      size_t lds = ext_lds_wave * ext_wpb + 4ull * (((e_cap + 2) + 3) & ~3);
-      if ((c->max_len + 31) / 32 + 1 <= OVL_SCAP_WORDS) {
+      size_t lds = gen_lds_wave * gen_wpb + ml_lds;
+      const uint32_t ext_wpb = gen_wpb;
+      if (staged) {
         // staged kernel for exception-free pairs; pairs touching an 'n' are deferred to
         // the generic kernel below
         if (d_defer.alloc(npairs)) return fail(OVL_ERR_OOM, "defer list");
         EA.defer = d_defer.p;
-        hipLaunchKernelGGL(k_extend<true>, dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
-                           lds, s, EA);
+        hipLaunchKernelGGL(k_extend<true>, dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
+                           stg_lds_wave * stg_wpb + ml_lds, s, EA);
         HIPC(hipGetLastError());
         uint32_t nd = 0;
         HIPC(hipMemcpyAsync(&nd, d_ctr.p + 8, 4, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
+        if (getenv("OVL_DEBUG")) fprintf(stderr, "OVL_DEBUG deferred %u of %u pairs\n", nd, npairs);
         if (nd) {
           EA.list = d_defer.p;
           EA.npairs = nd;
@@ -792,8 +800,11 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   if (dbg_ptr_for_print) {
     unsigned long long dd[16];
     (void)hipMemcpy(dd, dbg_ptr_for_print, 128, hipMemcpyDeviceToHost);
-    fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu tb=%llu iters=%llu pedcyc=%llu tbcyc=%llu pairs=%llu maxrows=%llu\n",
-            dd[0], dd[1], dd[2], dd[4], dd[5], dd[6], dd[7], dd[8], dd[9]);
+    fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu slide_iters=%llu tb=%llu iters=%llu "
+            "cyc_chunks=%llu cyc_tb=%llu pairs=%llu maxrows=%llu cyc_rest=%llu cyc_ped=%llu "
+            "recenter=%llu cyc_pair=%llu\n",
+            dd[0], dd[1], dd[2], dd[3], dd[4], dd[5], dd[6], dd[7], dd[8], dd[9], dd[10], dd[11],
+            dd[12], dd[13]);
   }
   c->stats.kmer_hits_without_olap = hs[0];
   c->stats.kmer_hits_with_olap = hs[1];

@@ -45,6 +45,7 @@ struct ExtendArgs {
   int32_t *rowdir;              // per wave: (offset, lo) per error level
   int32_t *deltas;              // per wave: stack | right | left
   int32_t e_cap;                // error levels the scratch holds
+  int32_t sw_words;             // staged kernel: LDS words per strand (even)
   Rec *out;
   uint32_t *nout;
   uint32_t out_cap;
@@ -65,6 +66,7 @@ struct PedOut {
   int32_t leftover;
   int32_t mte;
   int32_t nd;              // deltas produced
+  int32_t ovf;             // register window overflow: the pair goes to the generic kernel
 };
 
 __device__ __forceinline__ void vm_sync() {
@@ -129,6 +131,63 @@ __device__ __forceinline__ int32_t wave_max(int32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// Set_Right_Delta / Set_Left_Delta walk (forward.C:51, reverse.C:49) over the row log:
+// rows are staged into LDS 16 at a time, lane 0 walks them.  Row e of the log holds the
+// values of diagonals [lo, lo + width) with width = next row's offset - this row's.
+__device__ __forceinline__ void ped_traceback(const WaveMem &WM, int32_t tb_e, int32_t tb_d,
+                                              int32_t *dst, uint32_t lane, int32_t &last_out,
+                                              int32_t &nd_out) {
+  int32_t *rows = WM.rows, *rowdir = WM.rowdir;
+  lds_i32 *tbw = WM.tbw;
+  vm_sync();                                  // the row log is complete
+  int32_t d = tb_d;
+  int32_t last;
+  {
+    int32_t o0 = rowdir[2 * tb_e], l0 = rowdir[2 * tb_e + 1];
+    last = rows[o0 + d - l0];
+  }
+  int32_t nd = 0;
+  for (int32_t kh = tb_e; kh >= 1; kh -= TB_ROWS) {
+    int32_t kl = kh - TB_ROWS + 1;
+    if (kl < 1) kl = 1;
+    int32_t dc = d;
+    int32_t nrows = kh - kl + 1;
+    for (int32_t i = lane; i < nrows * TB_W; i += 64) {
+      int32_t rr = i / TB_W, w = i - rr * TB_W;
+      int32_t row = kl - 1 + rr;
+      int32_t ro = rowdir[2 * row], rl = rowdir[2 * row + 1];
+      int32_t rwidth = rowdir[2 * (row + 1)] - ro;
+      int32_t dd = dc - (TB_ROWS + 1) + w;
+      int32_t idx = dd - rl;
+      tbw[i] = (idx >= 0 && idx < rwidth) ? rows[ro + idx] : -3;
+    }
+    lds_sync();
+    if (lane == 0) {
+      for (int32_t kk = kh; kk >= kl; kk--) {
+        const lds_i32 *prow = tbw + (kk - 1 - (kl - 1)) * TB_W - (dc - (TB_ROWS + 1));
+        int32_t from = d, mx = 1 + prow[d], j;
+        if ((j = prow[d - 1]) > mx) { from = d - 1; mx = j; }
+        if ((j = 1 + prow[d + 1]) > mx) { from = d + 1; mx = j; }
+        if (from == d - 1) {
+          dst[nd++] = mx - last - 1;
+          d--;
+          last = prow[from];
+        } else if (from == d + 1) {
+          dst[nd++] = last - (mx - 1);
+          d++;
+          last = prow[from];
+        }
+      }
+    }
+    d = __shfl(d, 0);
+    last = __shfl(last, 0);
+    nd = __shfl(nd, 0);
+    lds_sync();
+  }
+  last_out = last;
+  nd_out = nd;
+}
+
 template <int DIR, typename SS>
 __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const SS &A, int32_t a0, int32_t m,
                            const SS &T, int32_t t0, int32_t n, int32_t limit,
@@ -139,6 +198,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
   PedOut out;
   out.leftover = 0;
   out.nd = 0;
+  out.ovf = 0;
   unsigned long long dbg_rows = 0, dbg_chunks = 0;
   unsigned long long t_start = X.dbg ? __builtin_amdgcn_s_memtime() : 0;
   // the scratch is sized for e_cap rows of width <= 2e+5 (ovl_api.hip), so the row loop
@@ -299,52 +359,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
   }
 
   unsigned long long t_mid = X.dbg ? __builtin_amdgcn_s_memtime() : 0;
-  // ---- traceback (Set_Right_Delta / Set_Left_Delta loop), 16-row LDS windows ---------
-  vm_sync();                                  // the row log is complete
-  int32_t d = tb_d;
-  int32_t last;
-  {
-    int32_t o0 = rowdir[2 * tb_e], l0 = rowdir[2 * tb_e + 1];
-    last = rows[o0 + d - l0];
-  }
-  int32_t nd = 0;
-  for (int32_t kh = tb_e; kh >= 1; kh -= TB_ROWS) {
-    int32_t kl = kh - TB_ROWS + 1;
-    if (kl < 1) kl = 1;
-    int32_t dc = d;
-    int32_t nrows = kh - kl + 1;
-    for (int32_t i = lane; i < nrows * TB_W; i += 64) {
-      int32_t rr = i / TB_W, w = i - rr * TB_W;
-      int32_t row = kl - 1 + rr;
-      int32_t ro = rowdir[2 * row], rl = rowdir[2 * row + 1];
-      int32_t rwidth = rowdir[2 * (row + 1)] - ro;
-      int32_t dd = dc - (TB_ROWS + 1) + w;
-      int32_t idx = dd - rl;
-      tbw[i] = (idx >= 0 && idx < rwidth) ? rows[ro + idx] : -3;
-    }
-    lds_sync();
-    if (lane == 0) {
-      for (int32_t kk = kh; kk >= kl; kk--) {
-        const lds_i32 *prow = tbw + (kk - 1 - (kl - 1)) * TB_W - (dc - (TB_ROWS + 1));
-        int32_t from = d, mx = 1 + prow[d], j;
-        if ((j = prow[d - 1]) > mx) { from = d - 1; mx = j; }
-        if ((j = 1 + prow[d + 1]) > mx) { from = d + 1; mx = j; }
-        if (from == d - 1) {
-          dst[nd++] = mx - last - 1;
-          d--;
-          last = prow[from];
-        } else if (from == d + 1) {
-          dst[nd++] = last - (mx - 1);
-          d++;
-          last = prow[from];
-        }
-      }
-    }
-    d = __shfl(d, 0);
-    last = __shfl(last, 0);
-    nd = __shfl(nd, 0);
-    lds_sync();
-  }
+  int32_t last = 0, nd = 0;
+  ped_traceback(WM, tb_e, tb_d, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
   if (X.dbg && lane == 0) {
@@ -357,6 +373,367 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
     atomicAdd(&X.dbg[7], t_end - t_mid);
     atomicMax(&X.dbg[9], dbg_rows);
   }
+  return out;
+}
+
+// ---- register-resident rows (the staged kernel) -------------------------------------
+// Row e-1 lives in OVL_RJ registers per lane: lane l of chunk j holds diagonal B+64j+l, the
+// window [B, B + 64*OVL_RJ) is re-centred through LDS when the band drifts out of it (rare).
+// Every value outside the surviving band [pl, pr] is -2, which is exactly the sentinel
+// forward.C:170 writes around the band, so the neighbours d-1 / d+1 come from DPP wave
+// shifts with no LDS round trip.  Row e is logged band-compact as [nl-2, nr+2] (masked)
+// for the traceback.
+#define OVL_RJ 8
+
+#ifdef OVL_PROFILE
+#define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define PROF_T(v)
+#define PROF_ADD(acc, a, b)
+#endif
+
+// 32 bases of an LDS strand starting at p; p may be negative (the words before the strand
+// are other LDS data: those bases lie beyond the comparison limit and are never counted).
+__device__ __forceinline__ uint64_t lds_bases(const lds_u64 *w, int32_t p) {
+  int32_t wi = p >> 5;
+  uint32_t sh = ((uint32_t)p & 31u) * 2u;
+  uint64_t lo = w[wi], hi = w[wi + 1];
+  return (lo >> sh) | ((hi << 1) << (63u - sh));
+}
+
+// slide on exception-free LDS strands: DIR=+1 compares A[pa..], T[pt..]; DIR=-1 compares
+// A[pa], A[pa-1], .. with T[pt], T[pt-1], ..; at most lim (> 0) bases.
+template <int DIR>
+__device__ __forceinline__ int32_t slide_lds(const lds_u64 *a, int32_t pa, const lds_u64 *t,
+                                             int32_t pt, int32_t lim) {
+  int32_t k = 0;
+  for (;;) {
+    uint64_t x, mm;
+    int32_t run;
+    if (DIR > 0) {
+      x = lds_bases(a, pa + k) ^ lds_bases(t, pt + k);
+      mm = (x | (x >> 1)) & 0x5555555555555555ull;
+      run = mm ? (int32_t)(__builtin_ctzll(mm) >> 1) : 32;
+    } else {
+      x = lds_bases(a, pa - k - 31) ^ lds_bases(t, pt - k - 31);
+      mm = (x | (x >> 1)) & 0x5555555555555555ull;
+      run = mm ? (int32_t)(__builtin_clzll(mm) >> 1) : 32;
+    }
+    k += run;
+    if (run < 32 || k >= lim) break;
+  }
+  return k < lim ? k : lim;
+}
+
+// Matching bases (0..32) at the first step of a slide, no limit applied.
+template <int DIR>
+__device__ __forceinline__ int32_t first_run(const lds_u64 *a, int32_t pa, const lds_u64 *t,
+                                             int32_t pt) {
+  if (DIR > 0) {
+    const uint64_t x = lds_bases(a, pa) ^ lds_bases(t, pt);
+    const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
+    return mm ? (int32_t)(__builtin_ctzll(mm) >> 1) : 32;
+  } else {
+    const uint64_t x = lds_bases(a, pa - 31) ^ lds_bases(t, pt - 31);
+    const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
+    return mm ? (int32_t)(__builtin_clzll(mm) >> 1) : 32;
+  }
+}
+
+template <int DIR, typename SS>
+__device__ __forceinline__ int32_t slide_any(const SS &A, int32_t a0, const SS &T, int32_t t0,
+                                             int32_t r, int32_t d, int32_t lim) {
+  if constexpr (SS::kExc) {
+    if (DIR > 0) return slide_fwd(A, a0 + r, T, t0 + r + d, lim);
+    return slide_bwd(A, a0 - r, T, t0 - r - d, lim);
+  } else {
+    if (DIR > 0) return slide_lds<1>(A.w, a0 + r, T.w, t0 + r + d, lim);
+    return slide_lds<-1>(A.w, a0 - r, T.w, t0 - r - d, lim);
+  }
+}
+
+__device__ __forceinline__ int32_t dpp_from_lower(int32_t v, int32_t lane0) {   // lane l <- l-1
+  return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int32_t dpp_from_upper(int32_t v, int32_t lane63) {  // lane l <- l+1
+  return __builtin_amdgcn_update_dpp(lane63, v, 0x130, 0xf, 0xf, false);
+}
+
+template <int DIR, typename SS>
+__device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
+                                                         int32_t a0, int32_t m, const SS &T,
+                                                         int32_t t0, int32_t n, int32_t limit,
+                                                         const WaveMem &WM, int32_t *dst,
+                                                         uint32_t lane) {
+  constexpr int J = OVL_RJ;
+  static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
+  int32_t *rows = WM.rows, *rowdir = WM.rowdir;
+  const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
+  PedOut out;
+  out.leftover = 0;
+  out.nd = 0;
+  out.ovf = 0;
+  if (limit > X.e_cap - 2) {
+    if (lane == 0) atomicOr(X.overflow, 8u);
+    out.err = 0; out.a_len = 0; out.t_len = 0; out.mte = 0; out.nd = -1;
+    return out;
+  }
+  int32_t row0 = 0;
+  {
+    int32_t lim0 = m < n ? m : n;
+    if (lim0 > 0) row0 = slide_any<DIR>(A, a0, T, t0, 0, 0, lim0);
+    row0 = __builtin_amdgcn_readfirstlane(row0);
+  }
+  if (row0 == m) {
+    out.err = 0; out.a_len = m; out.t_len = m; out.mte = 1;
+    out.leftover = m;          // reverse(): Leftover = m on an exact match
+    out.nd = -1;               // no traceback
+    return out;
+  }
+  // row 0 log: diagonals [-2, 2] = (-2, -2, row0, -2, -2)
+  if (lane < 5) rows[lane] = (lane == 2) ? row0 : -2;
+  if (lane == 0) { rowdir[0] = 0; rowdir[1] = -2; }
+
+  int32_t R[J];
+#pragma unroll
+  for (int j = 0; j < J; j++) R[j] = -2;
+  int32_t B = -3;                              // window anchored: B <= pl-3 < B+64
+  if (lane == 3) R[0] = row0;
+
+  double  max_score = 0.0;
+  int32_t max_score_len = 0, max_score_best_d = 0, max_score_best_e = 0;
+  int32_t best_d = 0, best_e = 0, longest = 0;
+  int32_t pl = 0, pr = 0, cursor = 5;
+  int32_t tb_e = -1, tb_d = 0;
+  bool finished = false;
+  const double bmv = X.branch_match_value;
+  const bool partial = X.partial != 0;
+  const int32_t mbed = X.min_branch_end_dist;
+  const double mbts = X.min_branch_tail_slope;
+#ifdef OVL_PROFILE
+  unsigned long long pc_chunks = 0, pc_rest = 0, pc_rows = 0, pc_nch = 0, pc_slide = 0,
+                     pc_recenter = 0;
+  PROF_T(pt_begin);
+#endif
+
+  for (int32_t e = 1; e <= limit; e++) {
+    PROF_T(pt_row);
+    const int32_t ML = WM.mlim[e];
+    const int32_t left = pl - 1, right = pr + 1;
+    // The window is anchored at the band: B <= pl-3 < B+64, so the row's chunks are
+    // 0..jr.  It must also hold pr+3 (the reads of this row and the log of the next).
+    if (pl - 3 < B) {                          // pl moves down by at most 1 per row
+#pragma unroll
+      for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
+      R[0] = -2;
+      B -= 64;
+#ifdef OVL_PROFILE
+      pc_recenter++;
+#endif
+    }
+    while (pl - 3 >= B + 64) {                 // pruning can move it up by any amount
+#pragma unroll
+      for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
+      R[J - 1] = -2;
+      B += 64;
+#ifdef OVL_PROFILE
+      pc_recenter++;
+#endif
+    }
+    if (pr + 3 > B + 64 * J - 1) {
+      out.ovf = 1;
+      return out;
+    }
+    const int32_t jr = (right - B) >> 6;
+
+    // ---- the row.  A: neighbours from row e-1 for every chunk (DPP, no LDS).  B: the
+    // first 32-base slide step of every lane of every chunk, branch-free, so the strand
+    // loads of all chunks are in flight together; lanes that matched all 32 continue in a
+    // per-chunk loop.  C: end test and Edit_Match_Limit pruning, chunk by chunk in d order.
+    int32_t NR[J], LM[J];
+    {
+      int32_t carry = -2;                      // row e-1 at diagonal B+64j-1
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        if (j > jr) break;
+        const int32_t d = B + 64 * j + (int32_t)lane;
+        const int32_t p0 = R[j];
+        const int32_t nxt = (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
+        const int32_t pm = dpp_from_lower(p0, carry);
+        const int32_t pp = dpp_from_upper(p0, nxt);
+        carry = __builtin_amdgcn_readlane(p0, 63);
+        int32_t r = 1 + p0;
+        r = pm > r ? pm : r;
+        r = 1 + pp > r ? 1 + pp : r;
+        int32_t lim = m - r;
+        const int32_t l2 = n - r - d;
+        lim = l2 < lim ? l2 : lim;
+        NR[j] = r;
+        LM[j] = (d >= left && d <= right) ? lim : 0;
+      }
+    }
+    bool more = false;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      if (j > jr) break;
+      const int32_t d = B + 64 * j + (int32_t)lane;
+      const int32_t r = NR[j], lim = LM[j];
+      const int32_t pa = (DIR > 0) ? a0 + r : a0 - r;
+      const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d;
+      const int32_t run = first_run<DIR>(A.w, pa, T.w, pt);
+      int32_t k = run < lim ? run : lim;
+      NR[j] = r + (lim > 0 ? k : 0);
+      LM[j] = (run == 32 && lim > 32) ? lim - 32 : 0;
+      more = more || LM[j] > 0;
+    }
+#ifdef OVL_PROFILE
+    pc_nch += jr + 1;
+#endif
+    if (__ballot(more)) {
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        if (j > jr) break;
+        if (LM[j] > 0) {
+          const int32_t d = B + 64 * j + (int32_t)lane;
+          NR[j] += slide_any<DIR>(A, a0, T, t0, NR[j], d, LM[j]);
+        }
+#ifdef OVL_PROFILE
+        pc_slide++;
+#endif
+      }
+    }
+    int32_t nl = NONE, nr = NEG;
+    bool ended = false;
+    int32_t end_d = 0, end_row = 0, end_pp = 0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      if (j > jr) break;
+      const int32_t c = B + 64 * j;
+      const int32_t d = c + (int32_t)lane;
+      const bool act = d >= left && d <= right;
+      const int32_t r = NR[j];
+      const uint64_t endm = __ballot(act && (r == m || r + d == n));
+      if (endm) {
+        const int32_t l = (int32_t)__builtin_ctzll(endm);
+        end_d = c + l;
+        end_row = __builtin_amdgcn_readlane(r, l);
+        // row e-1 at d+1 (R still holds row e-1 from chunk j on)
+        end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
+               : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
+        ended = true;
+        break;
+      }
+      const uint64_t km = __ballot(act && (((d < 0) ? r : r + d) >= ML));
+      if (km) {
+        if (nl == NONE) nl = c + (int32_t)__builtin_ctzll(km);
+        nr = c + 63 - (int32_t)__builtin_clzll(km);
+      }
+      R[j] = act ? r : -2;
+    }
+
+    PROF_T(pt_chunks);
+    PROF_ADD(pc_chunks, pt_row, pt_chunks);
+#ifdef OVL_PROFILE
+    pc_rows++;
+#endif
+    if (ended) {
+      double  score = end_row * bmv - e;
+      int32_t tail_len = end_row - max_score_len;
+      double  slope = (double)(max_score - score) / tail_len;
+      bool    abort_here = false;
+      if (partial && score < max_score) abort_here = true;
+      if (e > mbed / 2 && tail_len >= mbed && slope >= mbts) abort_here = true;
+      if (abort_here) {
+        out.err = max_score_best_e;
+        out.a_len = max_score_len;
+        out.t_len = max_score_len + max_score_best_d;
+        out.mte = 0;
+        tb_e = max_score_best_e; tb_d = max_score_best_d;
+      } else {
+        int32_t d = end_d;
+        // forward.C:212 -- force the last error to be a mismatch rather than an insertion
+        if (DIR > 0 && end_row == m && 1 + end_pp == end_row && d < right) d++;
+        out.err = e;
+        out.a_len = end_row;
+        out.t_len = end_row + d;
+        out.mte = 1;
+        tb_e = e; tb_d = d;
+        // the traceback reads row e only at d
+        if (lane == 0) { rows[cursor] = end_row; rowdir[2 * e] = cursor; rowdir[2 * e + 1] = d; }
+      }
+      finished = true;
+      break;
+    }
+    if (nl == NONE) break;                     // Left > Right
+
+    // prune to [nl, nr] (the rest becomes the -2 sentinel), log row e as [nl-2, nr+2],
+    // longest row with the first d on ties
+    const int32_t lo = nl - 2, hi = nr + 2, off = cursor;
+    const int32_t jrr = ((hi > right ? hi : right) - B) >> 6;
+    int32_t *glog = rows + off - lo;
+    int32_t mx = NEG;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      if (j > jrr) break;
+      const int32_t d = B + 64 * j + (int32_t)lane;
+      const int32_t v = (d >= nl && d <= nr) ? R[j] : -2;
+      R[j] = v;
+      mx = v > mx ? v : mx;
+      if (d >= lo && d <= hi) glog[d] = v;
+    }
+    if (lane == 0) { rowdir[2 * e] = off; rowdir[2 * e + 1] = lo; }
+    cursor += hi - lo + 1;
+    const int32_t M = wave_max(mx);
+    if (M > longest) {
+      int32_t bd = NONE;
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        if (j > jrr) break;
+        const uint64_t b = __ballot(R[j] == M);
+        if (b) { bd = B + 64 * j + (int32_t)__builtin_ctzll(b); break; }
+      }
+      longest = M; best_d = bd; best_e = e;
+    }
+    double score = longest * bmv - e;
+    if (score > max_score) {
+      max_score = score;
+      max_score_len = longest;
+      max_score_best_d = best_d;
+      max_score_best_e = best_e;
+    }
+    pl = nl;
+    pr = nr;
+    PROF_T(pt_rest);
+    PROF_ADD(pc_rest, pt_chunks, pt_rest);
+  }
+  if (!finished) {
+    out.err = max_score_best_e;
+    out.a_len = max_score_len;
+    out.t_len = max_score_len + max_score_best_d;
+    out.mte = 0;
+    tb_e = max_score_best_e; tb_d = max_score_best_d;
+  }
+  int32_t last = 0, nd = 0;
+  PROF_T(pt_tb0);
+  ped_traceback(WM, tb_e, tb_d, dst, lane, last, nd);
+  out.leftover = last;
+  out.nd = nd;
+#ifdef OVL_PROFILE
+  PROF_T(pt_tb1);
+  if (X.dbg && lane == 0) {
+    atomicAdd(&X.dbg[0], 1ull);
+    atomicAdd(&X.dbg[1], pc_rows);
+    atomicAdd(&X.dbg[2], pc_nch);
+    atomicAdd(&X.dbg[3], pc_slide);
+    atomicAdd(&X.dbg[4], (unsigned long long)(tb_e > 0 ? tb_e : 0));
+    atomicAdd(&X.dbg[6], pc_chunks);
+    atomicAdd(&X.dbg[7], pt_tb1 - pt_tb0);
+    atomicAdd(&X.dbg[10], pc_rest);
+    atomicAdd(&X.dbg[11], pt_tb1 - pt_begin);
+    atomicAdd(&X.dbg[12], pc_recenter);
+  }
+#endif
   return out;
 }
 
@@ -375,7 +752,7 @@ struct ExtOut {
 };
 
 // Extend_Alignment (prefixEditDistance-extend.C:86).  Leaves the merged Left_Delta in LD.
-template <typename SS>
+template <bool FAST, typename SS>
 __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS &S,
                                    int32_t S_Len, const SS &T, int32_t T_Len,
                                    const WaveMem &WM, int32_t *stk, int32_t *RD,
@@ -402,7 +779,10 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     int32_t b0 = s_first ? T_Right_Begin : S_Right_Begin;
     int32_t am = s_first ? S_Right_Len : T_Right_Len;
     int32_t bn = s_first ? T_Right_Len : S_Right_Len;
-    PedOut po = wave_ped<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    PedOut po;
+    if constexpr (FAST) po = wave_ped_reg<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    else                po = wave_ped<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    if (po.ovf) { r.kind = -1; return r; }
     right_errors = po.err;
     rmte = po.mte;
     if (s_first) { S_Hi = po.a_len; T_Hi = po.t_len; }
@@ -434,7 +814,10 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     SS A = s_first ? S : T, B = s_first ? T : S;
     int32_t a0 = s_first ? S_Left_Begin : T_Left_Begin;
     int32_t b0 = s_first ? T_Left_Begin : S_Left_Begin;
-    PedOut po = wave_ped<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    PedOut po;
+    if constexpr (FAST) po = wave_ped_reg<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    else                po = wave_ped<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    if (po.ovf) { r.kind = -1; return r; }
     left_errors = po.err;
     lmte = po.mte;
     int32_t a_end = -po.a_len, t_end = -po.t_len;
@@ -620,8 +1003,11 @@ __device__ bool lies_on_alignment(int32_t start, int32_t offset, int32_t s_lo, i
 
 // Process_Matches (Process_String_Overlaps.C:400) for one pair, strands S (query, in its
 // orientation) and T (target, forward) -- global or LDS-staged.
-template <typename SS>
-__device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &un,
+// Returns false when the pair must be redone by the generic kernel (register window
+// overflow); nothing has been output for it then, and removed nodes are marked ~Len so the
+// generic kernel can restore them.
+template <bool FAST, typename SS>
+__device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &un,
                              const SS &S, const SS &T, const WaveMem &WM, int32_t *stk,
                              int32_t *RD, int32_t *LD, unsigned long long *st, uint32_t lane) {
   uint32_t S_ID = X.R.first_iid + un.r, T_ID = X.R.first_iid + P.tgt;
@@ -640,7 +1026,7 @@ __device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     if (!(ovl_len < (double)X.k))
       expct = (uint64_t)(int)floor(X.minkmer_exp * (ovl_len - X.k + 1));
     uint64_t mk = expct > X.filter_by_kmer_count ? expct : X.filter_by_kmer_count;
-    if (mk > (uint64_t)P.diag_ct) { st[2]++; return; }
+    if (mk > (uint64_t)P.diag_ct) { st[2]++; return true; }
   }
 
   // hopeless check (:433)
@@ -660,7 +1046,7 @@ __device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     } else {
       if (t_tail > 90 && !(trf & 4u)) hopeless = true;
     }
-    if (hopeless) { st[0]++; return; }
+    if (hopeless) { st[0]++; return true; }
   }
   if (X.dbg && lane == 0) atomicAdd(&X.dbg[8], 1ull);
 
@@ -679,7 +1065,8 @@ __device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     wave_argmax(bv, bi);
     Node M = nodes[bi];
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
-    ExtOut eo = extend_alignment(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+    ExtOut eo = extend_alignment<FAST>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+    if (FAST && eo.kind < 0) return false;
     kind = eo.kind;
     S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
     ld_len = eo.ld_len;
@@ -707,7 +1094,7 @@ __device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
                 ((kind == K_DOVETAIL || X.partial) && S_Lo - SHIFT_SLACK <= nd.Start &&
                  nd.Start + nd.Len <= (S_Hi + 1) + SHIFT_SLACK - 1 &&
                  lies_on_alignment(nd.Start, nd.Offset, S_Lo, T_Lo, ldp, ld_len));
-      if (rm) { nodes[i].Len = -1; removed++; }
+      if (rm) { nodes[i].Len = ~nd.Len; removed++; }
     }
     for (int s = 32; s > 0; s >>= 1) removed += __shfl_xor(removed, s);
     remaining -= removed;
@@ -780,6 +1167,7 @@ __device__ void process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     st[1]++;
     if (outputs > 1) st[3]++;
   }
+  return true;
 }
 
 // Copy a strand's packed words (and the guard) into LDS.  Only exception-free strands are
@@ -793,33 +1181,51 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
   return L;
 }
 
+#define OVL_SCR 560              // staged kernel: per-wave LDS scratch ints (traceback window,
+                                 // window re-centring, Left_Delta cache), >= TB_ROWS * TB_W
+static_assert(OVL_SCR >= TB_ROWS * TB_W && OVL_SCR >= 64 * OVL_RJ, "scratch too small");
+
+// STAGE = true: exception-free pairs, strands staged in LDS, rows in registers; pairs with
+// 'n' bases or a band wider than the register window are deferred to the generic kernel.
+// STAGE = false: the generic kernel (global strands with exception masks, rows in LDS).
 template <bool STAGE>
-__global__ void __launch_bounds__(256) k_extend(ExtendArgs X) {
+__global__ void __launch_bounds__(256, 4) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-  int32_t wcap = 2 * X.e_cap + 8;
   int32_t mlsz = ((X.e_cap + 2) + 3) & ~3;
   for (int32_t i = threadIdx.x; i < X.e_cap + 2; i += blockDim.x)
     s_ext0[i] = (i <= X.max_errors) ? X.match_limit[i] : 0x7fffffff;
   __syncthreads();
   lds_i32 *l_ext0 = (lds_i32 *)s_ext0;
   lds_i32 *s_ext = l_ext0 + mlsz;
-  // per wave: [S words | T words] (u64, 16-B aligned) then rows, traceback, delta cache
-  size_t wave_ints = 4 * OVL_SCAP_WORDS + 2 * wcap + TB_ROWS * TB_W + OVL_LDCAP;
-  wave_ints = (wave_ints + 3) & ~(size_t)3;
-  lds_i32 *wlds = s_ext + wave * (uint32_t)wave_ints;
-  lds_u64 *sw = (lds_u64 *)(wlds);
-  lds_u64 *tw = sw + OVL_SCAP_WORDS;
   WaveMem WM;
   WM.rows = X.rows + (size_t)gw * X.rows_cap;
   WM.rowdir = X.rowdir + (size_t)gw * 2 * (X.e_cap + 2);
-  WM.lrow = wlds + 4 * OVL_SCAP_WORDS;
-  WM.wcap = wcap;
-  WM.tbw = WM.lrow + 2 * wcap;
-  WM.ldc = WM.tbw + TB_ROWS * TB_W;
-  WM.ldcap = OVL_LDCAP;
   WM.mlim = l_ext0;
+  lds_u64 *sw = nullptr, *tw = nullptr;
+  if constexpr (STAGE) {
+    // per wave: [S words | T words] (u64) then the scratch
+    uint32_t wave_ints = 4 * (uint32_t)X.sw_words + OVL_SCR;
+    lds_i32 *wlds = s_ext + wave * wave_ints;
+    sw = (lds_u64 *)wlds;
+    tw = sw + X.sw_words;
+    WM.lrow = nullptr;
+    WM.wcap = 0;
+    WM.tbw = wlds + 4 * X.sw_words;
+    WM.ldc = WM.tbw;
+    WM.ldcap = OVL_SCR;
+  } else {
+    // per wave: row buffers, traceback window, delta cache
+    int32_t wcap = 2 * X.e_cap + 8;
+    uint32_t wave_ints = (2 * wcap + TB_ROWS * TB_W + OVL_LDCAP + 3) & ~3u;
+    lds_i32 *wlds = s_ext + wave * wave_ints;
+    WM.lrow = wlds;
+    WM.wcap = wcap;
+    WM.tbw = WM.lrow + 2 * wcap;
+    WM.ldc = WM.tbw + TB_ROWS * TB_W;
+    WM.ldcap = OVL_LDCAP;
+  }
   int32_t *stk = X.deltas + (size_t)gw * 4 * (X.e_cap + 8);
   int32_t *RD = stk + (X.e_cap + 8);
   int32_t *LD = RD + (X.e_cap + 8);
@@ -836,18 +1242,28 @@ __global__ void __launch_bounds__(256) k_extend(ExtendArgs X) {
     Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
     Strand T = strand_fwd(X.R, P.tgt);
     if constexpr (STAGE) {
-      // the host launches this variant only when every read fits the strand cache
-      if (S.ex_wild || S.ex_nul || T.ex_wild) {
-        if (lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
-        continue;
+      bool ok = false;
+      if (!(S.ex_wild || S.ex_nul || T.ex_wild)) {
+        StrandLP SL = stage_strand(S, sw, lane);
+        StrandLP TL = stage_strand(T, tw, lane);
+        lds_sync();
+        PROF_T(pp0);
+        ok = process_pair<true>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane);
+#ifdef OVL_PROFILE
+        PROF_T(pp1);
+        if (X.dbg && lane == 0) atomicAdd(&X.dbg[13], pp1 - pp0);
+#endif
       }
-      StrandLP SL = stage_strand(S, sw, lane);
-      StrandLP TL = stage_strand(T, tw, lane);
-      lds_sync();
-      process_pair(X, P, un, SL, TL, WM, stk, RD, LD, st, lane);
+      if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
     } else {
-      (void)sw; (void)tw;
-      process_pair(X, P, un, S, T, WM, stk, RD, LD, st, lane);
+      if (X.list) {
+        // a deferred pair may have had nodes removed (~Len) before it overflowed
+        Node *nodes = X.pnodes + P.node_off;
+        for (uint32_t i = lane; i < P.node_cnt; i += 64)
+          if (nodes[i].Len < 0) nodes[i].Len = ~nodes[i].Len;
+        vm_sync();
+      }
+      process_pair<false>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
     }
     lds_sync();
   }

@@ -64,11 +64,13 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libcanu_ovl.so.  Raises if it was not built -- there is no fallback."""
+def load_library(path: str | None = None):
+    """Load libcanu_ovl.so.  Raises if it was not built -- there is no fallback.
+    CANU_OVL_LIB names another build of the same library (e.g. the profiling build)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("CANU_OVL_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise OvlError(-1, f"{path} missing: run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
