@@ -586,13 +586,13 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   // extension scratch per wave
   int32_t e_cap = c->h_error_bound[std::min<uint32_t>(c->max_len, AS_MAX_READLEN)] + 2;
   uint64_t rows_cap = (uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64;
-  uint64_t per_wave = rows_cap * 4 + 8ull * (e_cap + 2) + 16ull * (e_cap + 8);
+  uint64_t per_wave = rows_cap * 4 + 16ull * (e_cap + 2) + 16ull * (e_cap + 8);
   uint32_t ext_waves = 24u * c->n_cu;
   uint64_t budget = 24ull << 30;
   while (ext_waves > 256 && (uint64_t)ext_waves * per_wave > budget) ext_waves /= 2;
   DBuf<int32_t> d_rows, d_rowdir, d_deltas;
   if (d_rows.alloc(rows_cap * ext_waves) ||
-      d_rowdir.alloc((size_t)2 * (e_cap + 2) * ext_waves) ||
+      d_rowdir.alloc((size_t)4 * (e_cap + 2) * ext_waves) ||
       d_deltas.alloc((size_t)4 * (e_cap + 8) * ext_waves))
     return fail(OVL_ERR_OOM, "extension scratch");
   // LDS per extension wave (ovl_extend.hip k_extend).  Generic kernel: two row buffers, the

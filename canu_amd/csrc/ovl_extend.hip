@@ -460,6 +460,68 @@ __device__ __forceinline__ int32_t dpp_from_upper(int32_t v, int32_t lane63) {  
   return __builtin_amdgcn_update_dpp(lane63, v, 0x130, 0xf, 0xf, false);
 }
 
+// Set_Right_Delta / Set_Left_Delta over the code log of wave_ped_reg: cell (k, d) holds
+// (r << 2 | code), r = max(1 + L[k-1][d], L[k-1][d-1], 1 + L[k-1][d+1]) and code = which
+// one won (0: d, 1: d-1, 2: d+1) with the reference's tie order.  16 rows at a time are
+// loaded into registers (lane = diagonal offset -16..16 from the walk's position), and the
+// walk is scalar: one readlane per row.
+typedef __attribute__((address_space(1))) const int32_t g_ci32;
+typedef __attribute__((address_space(1))) const uint64_t g_cu64;
+
+__device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t tb_e,
+                                                    int32_t tb_d, int32_t last, int32_t *dst,
+                                                    uint32_t lane, int32_t &last_out,
+                                                    int32_t &nd_out) {
+  g_ci32 *rows = (g_ci32 *)WM.rows;
+  g_cu64 *rdir = (g_cu64 *)WM.rowdir;          // per row: (offset - left, left | right << 16)
+  vm_sync();                                  // the log is complete
+  int32_t d = __builtin_amdgcn_readfirstlane(tb_d);
+  last = __builtin_amdgcn_readfirstlane(last);
+  tb_e = __builtin_amdgcn_readfirstlane(tb_e);
+  int32_t nd = 0;
+  for (int32_t kh = tb_e; kh >= 1; kh -= 16) {
+    const int32_t dc = d;
+    const int32_t diag = dc - 16 + (int32_t)lane;
+    uint64_t rd[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) rd[i] = rdir[kh - i < 1 ? 1 : kh - i];
+    int32_t V[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int32_t base = (int32_t)(uint32_t)rd[i], lr = (int32_t)(rd[i] >> 32);
+      const int32_t lo = (int32_t)(int16_t)(lr & 0xffff), hi = lr >> 16;
+      const bool ok = (lane <= 32) & (diag >= lo) & (diag <= hi);
+      V[i] = rows[base + (ok ? diag : lo)];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int32_t lr = (int32_t)(rd[i] >> 32);
+      const int32_t lo = (int32_t)(int16_t)(lr & 0xffff), hi = lr >> 16;
+      const bool ok = (lane <= 32) & (diag >= lo) & (diag <= hi);
+      V[i] = ok ? V[i] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      if (kh - i < 1) break;
+      const int32_t p = __builtin_amdgcn_readlane(V[i], 16 + d - dc);
+      const int32_t code = p & 3, val = p >> 2;
+      if (code == 1) {
+        if (lane == 0) dst[nd] = val - last - 1;
+        nd++;
+        last = val;
+        d--;
+      } else if (code == 2) {
+        if (lane == 0) dst[nd] = last - val + 1;
+        nd++;
+        last = val - 1;
+        d++;
+      }
+    }
+  }
+  last_out = last;
+  nd_out = nd;
+}
+
 template <int DIR, typename SS>
 __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
                                                          int32_t a0, int32_t m, const SS &T,
@@ -491,9 +553,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     out.nd = -1;               // no traceback
     return out;
   }
-  // row 0 log: diagonals [-2, 2] = (-2, -2, row0, -2, -2)
-  if (lane < 5) rows[lane] = (lane == 2) ? row0 : -2;
-  if (lane == 0) { rowdir[0] = 0; rowdir[1] = -2; }
 
   int32_t R[J];
 #pragma unroll
@@ -504,8 +563,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   double  max_score = 0.0;
   int32_t max_score_len = 0, max_score_best_d = 0, max_score_best_e = 0;
   int32_t best_d = 0, best_e = 0, longest = 0;
-  int32_t pl = 0, pr = 0, cursor = 5;
-  int32_t tb_e = -1, tb_d = 0;
+  int32_t pl = 0, pr = 0, cursor = 0;
+  int32_t tb_e = -1, tb_d = 0, tb_last = 0;
   bool finished = false;
   const double bmv = X.branch_match_value;
   const bool partial = X.partial != 0;
@@ -546,6 +605,12 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       return out;
     }
     const int32_t jr = (right - B) >> 6;
+    // row e's traceback codes cover [left, right]: rowdir[e] = (offset - left, left | right << 16)
+    int32_t *glog = rows + cursor - left;
+    if (lane == 0)
+      ((uint64_t *)rowdir)[e] = (uint32_t)(cursor - left) |
+                                ((uint64_t)(uint32_t)((left & 0xffff) | (right << 16)) << 32);
+    cursor += right - left + 1;
 
     // ---- the row.  A: neighbours from row e-1 for every chunk (DPP, no LDS).  B: the
     // first 32-base slide step of every lane of every chunk, branch-free, so the strand
@@ -563,14 +628,17 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         const int32_t pm = dpp_from_lower(p0, carry);
         const int32_t pp = dpp_from_upper(p0, nxt);
         carry = __builtin_amdgcn_readlane(p0, 63);
-        int32_t r = 1 + p0;
-        r = pm > r ? pm : r;
-        r = 1 + pp > r ? 1 + pp : r;
+        // the traceback's choice (forward.C:62-70): d, then d-1, then d+1, strict >
+        int32_t r = 1 + p0, code = 0;
+        if (pm > r) { r = pm; code = 1; }
+        if (1 + pp > r) { r = 1 + pp; code = 2; }
         int32_t lim = m - r;
         const int32_t l2 = n - r - d;
         lim = l2 < lim ? l2 : lim;
         NR[j] = r;
-        LM[j] = (d >= left && d <= right) ? lim : 0;
+        const bool act = d >= left && d <= right;
+        LM[j] = act ? lim : 0;
+        if (act) glog[d] = (r << 2) | code;
       }
     }
     bool more = false;
@@ -658,38 +726,29 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         out.a_len = end_row;
         out.t_len = end_row + d;
         out.mte = 1;
-        tb_e = e; tb_d = d;
-        // the traceback reads row e only at d
-        if (lane == 0) { rows[cursor] = end_row; rowdir[2 * e] = cursor; rowdir[2 * e + 1] = d; }
+        tb_e = e; tb_d = d; tb_last = end_row;
       }
       finished = true;
       break;
     }
     if (nl == NONE) break;                     // Left > Right
 
-    // prune to [nl, nr] (the rest becomes the -2 sentinel), log row e as [nl-2, nr+2],
-    // longest row with the first d on ties
-    const int32_t lo = nl - 2, hi = nr + 2, off = cursor;
-    const int32_t jrr = ((hi > right ? hi : right) - B) >> 6;
-    int32_t *glog = rows + off - lo;
+    // prune to [nl, nr] (the rest becomes the -2 sentinel), longest row, first d on ties
     int32_t mx = NEG;
 #pragma unroll
     for (int j = 0; j < J; j++) {
-      if (j > jrr) break;
+      if (j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t v = (d >= nl && d <= nr) ? R[j] : -2;
       R[j] = v;
       mx = v > mx ? v : mx;
-      if (d >= lo && d <= hi) glog[d] = v;
     }
-    if (lane == 0) { rowdir[2 * e] = off; rowdir[2 * e + 1] = lo; }
-    cursor += hi - lo + 1;
     const int32_t M = wave_max(mx);
     if (M > longest) {
       int32_t bd = NONE;
 #pragma unroll
       for (int j = 0; j < J; j++) {
-        if (j > jrr) break;
+        if (j > jr) break;
         const uint64_t b = __ballot(R[j] == M);
         if (b) { bd = B + 64 * j + (int32_t)__builtin_ctzll(b); break; }
       }
@@ -714,9 +773,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     out.mte = 0;
     tb_e = max_score_best_e; tb_d = max_score_best_d;
   }
+  if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
-  ped_traceback(WM, tb_e, tb_d, dst, lane, last, nd);
+  ped_traceback_codes(WM, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
 #ifdef OVL_PROFILE
@@ -1201,7 +1261,7 @@ __global__ void __launch_bounds__(256, 4) k_extend(ExtendArgs X) {
   lds_i32 *s_ext = l_ext0 + mlsz;
   WaveMem WM;
   WM.rows = X.rows + (size_t)gw * X.rows_cap;
-  WM.rowdir = X.rowdir + (size_t)gw * 2 * (X.e_cap + 2);
+  WM.rowdir = X.rowdir + (size_t)gw * 4 * (X.e_cap + 2);
   WM.mlim = l_ext0;
   lds_u64 *sw = nullptr, *tw = nullptr;
   if constexpr (STAGE) {
