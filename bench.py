@@ -28,24 +28,6 @@ METRIC = "overlaps/sec + Gbp-vs-Gbp/sec, 50k×10kb ONT reads, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def query_shards(n: int, world: int) -> list[tuple[int, int]]:
-    """Split query IDs 1..n so every rank gets about the same number of (a, b>a) pairs:
-    read a pairs with the n-a reads after it."""
-    w = np.arange(n, 0, -1, dtype=np.float64) - 1.0     # weight of a = n - a
-    c = np.cumsum(w)
-    tot = c[-1] if n else 0.0
-    out, lo = [], 1
-    for r in range(world):
-        if r == world - 1:
-            hi = n
-        else:
-            hi = int(np.searchsorted(c, tot * (r + 1) / world)) + 1
-            hi = max(hi, lo - 1)
-        out.append((lo, hi))
-        lo = hi + 1
-    return out
-
-
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +59,7 @@ def main() -> None:
 
     from canu_amd.synth import synth_reads, random_genome
     from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    from canu_amd.dist import gather_read_store, query_shards
 
     n = args.reads
     genome_len = int(n * args.read_len / args.coverage)
@@ -94,27 +77,8 @@ def main() -> None:
         bases = torch.from_numpy(part.bases).to(dev)
         lengths = part.lengths
     else:
-        mine = torch.from_numpy(part.bases).to(dev)
-        sizes = torch.tensor([mine.numel()], device=dev, dtype=torch.int64)
-        all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-        dist.all_gather(all_sizes, sizes)
-        mx = int(max(s.item() for s in all_sizes))
-        buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-        buf[:mine.numel()] = mine
-        gathered = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
-        dist.all_gather(gathered, buf)                          # RCCL over xGMI
-        bases = torch.cat([g[:int(s.item())] for g, s in zip(gathered, all_sizes)])
-        lens_t = torch.from_numpy(part.lengths.astype(np.int64)).to(dev)
-        nl = torch.tensor([lens_t.numel()], device=dev, dtype=torch.int64)
-        all_nl = [torch.zeros_like(nl) for _ in range(world)]
-        dist.all_gather(all_nl, nl)
-        mxl = int(max(v.item() for v in all_nl))
-        lb = torch.zeros(mxl, dtype=torch.int64, device=dev)
-        lb[:lens_t.numel()] = lens_t
-        gl = [torch.empty(mxl, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(gl, lb)
-        lengths = torch.cat([g[:int(v.item())] for g, v in zip(gl, all_nl)]).cpu().numpy()
-        lengths = lengths.astype(np.uint32)
+        bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(dev), part.lengths,
+                                           dist, dev)          # RCCL over xGMI
     offsets = np.zeros(n, dtype=np.uint64)
     offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
     d_offsets = torch.from_numpy(offsets.view(np.int64)).to(dev)
@@ -162,13 +126,31 @@ def main() -> None:
     gbp = total_bases / 1e9
     gbp_vs_gbp = gbp * gbp / 2.0 * args.steps / elapsed    # all-vs-all, each pair once
 
+    traffic = load_traffic()
+    # Dominant kernel: k_extend (the banded edit-distance extension).  Its algorithmic HBM
+    # bytes per pair are the two packed strands it stages (2 bits/base + guard word each),
+    # the pair's seed-match nodes (16 B each) and its output records (24 B each).
+    avg_len = total_bases / max(n, 1)
+    strand = 8.0 * (np.ceil(avg_len / 32.0) + 1.0)
+    ext_bytes = st["pairs"] * 2 * strand + st["seed_hits"] * 16 + st["total_overlaps"] * 24
     roof = None
+    if st["ms_extend"] > 0:
+        achieved = ext_bytes / (st["ms_extend"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": _traffic(traffic, "k_extend"), "kernel": "k_extend",
+                "limiter": "integer issue/latency (greedy O(ND) rows, no MFMA shape)",
+                "algorithmic_bytes": int(ext_bytes), "ms": round(st["ms_extend"], 2)}
+    # The north star's roofline target: the hash-probe kernel (one 16-B table entry and one
+    # 8-B probe record per query window, plus the 2-bit query).
+    probe_roof = None
     if st["ms_probe_kernel"] > 0:
         achieved = st["probe_bytes"] / (st["ms_probe_kernel"] * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_probe", "algorithmic_bytes": st["probe_bytes"],
-                "ms": round(st["ms_probe_kernel"], 3)}
+        probe_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                      "traffic": _traffic(traffic, "k_probe"), "kernel": "k_probe",
+                      "algorithmic_bytes": st["probe_bytes"],
+                      "ms": round(st["ms_probe_kernel"], 3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -193,12 +175,31 @@ def main() -> None:
             "seed_hits": st["seed_hits"], "pairs": st["pairs"],
             "setup_s": round(setup_s, 1),
             "roofline": roof,
+            "probe_roofline": probe_roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     oic.close()
     if dist:
         dist.destroy_process_group()
+
+
+def _traffic(t: dict, k: str):
+    """HBM bytes per step of kernel k (same unit as algorithmic_bytes), or None."""
+    v = t.get(k)
+    return None if v is None else v.get("hbm_bytes_per_step")
+
+
+def load_traffic() -> dict:
+    """Per-kernel HBM traffic of one default bench step from the committed rocprofv3 PMC
+    passes (profiles/traffic.json, tools/pmc_traffic.py): (2 x FETCH_SIZE + WRITE_SIZE) KiB,
+    the x2 being the gfx950 FETCH_SIZE correction.  Empty when absent."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
 
 
 def cpu_baseline(args) -> dict | None:

@@ -155,6 +155,19 @@ struct ovl_ctx {
   DBuf<TabEntry> d_tab;
   uint32_t tab_bits = 0, slice_bits = 0;
 
+  // find_overlaps working buffers: kept across calls (grow-only), hipMalloc of tens of
+  // GB per call would cost seconds
+  struct {
+    DBuf<Unit> units;
+    DBuf<uint64_t> rbase;
+    DBuf<Probe> probe;
+    DBuf<uint32_t> uhits, uflags, ctr, done, defer;
+    DBuf<Node> pool, pnodes;
+    DBuf<PairRec> pairs;
+    DBuf<unsigned long long> stats;
+    DBuf<int32_t> rows, rowdir, deltas;
+  } fb;
+
   // results
   DBuf<Rec> d_out;
   uint64_t nout = 0;
@@ -571,15 +584,23 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   c->nout = 0;
 
   // per-context device buffers, sized per batch
-  const uint64_t WIN_BUDGET = 192ull << 20;     // probe slots per batch (8 B each)
-  const uint64_t HIT_BUDGET = 320ull << 20;     // seed hits per batch
-  DBuf<Unit> d_units;
-  DBuf<uint64_t> d_rbase;
-  DBuf<Probe> d_probe;
-  DBuf<uint32_t> d_uhits, d_uflags, d_ctr, d_done, d_defer;
-  DBuf<Node> d_pool, d_pnodes;
-  DBuf<PairRec> d_pairs;
-  DBuf<unsigned long long> d_stats;
+  // A batch is sized by seed hits (node pool + list-ordered copy: 32 B per hit); the probe
+  // window budget adapts to the hits-per-window ratio seen so far so that a batch's probe
+  // results are all consumed (units beyond the hit budget would otherwise be re-probed).
+  const uint64_t HIT_BUDGET = 1280ull << 20;    // seed hits per batch
+  uint64_t WIN_BUDGET = 256ull << 20;           // probe slots per batch (8 B each)
+  auto &d_units = c->fb.units;
+  auto &d_rbase = c->fb.rbase;
+  auto &d_probe = c->fb.probe;
+  auto &d_uhits = c->fb.uhits;
+  auto &d_uflags = c->fb.uflags;
+  auto &d_ctr = c->fb.ctr;
+  auto &d_done = c->fb.done;
+  auto &d_defer = c->fb.defer;
+  auto &d_pool = c->fb.pool;
+  auto &d_pnodes = c->fb.pnodes;
+  auto &d_pairs = c->fb.pairs;
+  auto &d_stats = c->fb.stats;
   if (d_ctr.alloc(16) || d_stats.alloc(8)) return fail(OVL_ERR_OOM, "counters");
   HIPC(hipMemsetAsync(d_stats.p, 0, 64, s));
 
@@ -590,7 +611,9 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   uint32_t ext_waves = 24u * c->n_cu;
   uint64_t budget = 24ull << 30;
   while (ext_waves > 256 && (uint64_t)ext_waves * per_wave > budget) ext_waves /= 2;
-  DBuf<int32_t> d_rows, d_rowdir, d_deltas;
+  auto &d_rows = c->fb.rows;
+  auto &d_rowdir = c->fb.rowdir;
+  auto &d_deltas = c->fb.deltas;
   if (d_rows.alloc(rows_cap * ext_waves) ||
       d_rowdir.alloc((size_t)4 * (e_cap + 2) * ext_waves) ||
       d_deltas.alloc((size_t)4 * (e_cap + 8) * ext_waves))
@@ -653,11 +676,18 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     float t = 0;
     (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
     ms_probe += t;
-    probe_bytes += acc * 8;                          // see DESIGN.md for the full count
+    // algorithmic bytes: per window one 16-B table entry and one 8-B Probe record, plus the
+    // packed query (2 bits per base); see DESIGN.md
+    probe_bytes += acc * 24 + acc / 4;
     // shrink the batch to the hit budget (probe results stay valid for the prefix)
     uint64_t hsum = 0;
     uint32_t nc = 0;
     while (nc < nb && (hsum + uh[nc] <= HIT_BUDGET || nc == 0)) hsum += uh[nc++];
+    {
+      double ratio = (double)hsum / (double)std::max<uint64_t>(1, rbase[nc]);
+      double wb = (double)HIT_BUDGET / std::max(ratio, 1e-3) * 1.05;
+      WIN_BUDGET = (uint64_t)std::min(std::max(wb, 64.0 * (1 << 20)), 1536.0 * (1 << 20));
+    }
 
     uint64_t pool_cap = hsum + (hsum / 4000 + chain_waves + 2) * (uint64_t)OVL_NODE_BLOCK + 8;
     uint64_t pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * 256 + 1024);

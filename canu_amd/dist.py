@@ -1,0 +1,62 @@
+"""Multi-GPU layout of one overlapInCore job: one process per GPU.
+
+The reference splits an all-vs-all job into independent overlapInCore runs, each over a
+hash range (-h) and a query range (-r), scheduled by overlapInCorePartition
+(src/overlapInCore/overlapInCorePartition.C).  Here every rank holds the whole read store
+in HBM (288 GB holds any realistic batch), builds the same index over -h, and searches its
+own query shard of -r: shards are independent, so the data path has no collective.  The
+only exchange is at setup, when the ranks that each generated (or read) a slice of the
+store all-gather it -- over RCCL/xGMI on the GPUs, over gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def query_shards(n: int, world: int, first: int = 1) -> list[tuple[int, int]]:
+    """Split query IDs first..first+n-1 so every rank gets about the same number of (a, b>a)
+    pairs: read a is paired with the n-a reads after it.  Ranges are inclusive and may be
+    empty (lo > hi) when world > n."""
+    w = np.arange(n, 0, -1, dtype=np.float64) - 1.0
+    c = np.cumsum(w)
+    tot = c[-1] if n else 0.0
+    out, lo = [], 1
+    for r in range(world):
+        if r == world - 1:
+            hi = n
+        else:
+            hi = int(np.searchsorted(c, tot * (r + 1) / world)) + 1
+            hi = max(hi, lo - 1)
+            hi = min(hi, n)
+        out.append((first - 1 + lo, first - 1 + hi))
+        lo = hi + 1
+    return out
+
+
+def gather_read_store(bases_local, lengths_local: np.ndarray, dist, device):
+    """All-gather every rank's slice of the read store (rank order = read order).
+
+    bases_local: 1-D uint8 torch tensor on `device`; lengths_local: uint32 numpy array.
+    Returns (bases, lengths): the whole store as a uint8 tensor on `device` and a uint32
+    numpy array of read lengths."""
+    import torch
+    world = dist.get_world_size()
+    n_b = torch.tensor([bases_local.numel()], device=device, dtype=torch.int64)
+    n_l = torch.tensor([lengths_local.shape[0]], device=device, dtype=torch.int64)
+    all_nb = [torch.zeros_like(n_b) for _ in range(world)]
+    all_nl = [torch.zeros_like(n_l) for _ in range(world)]
+    dist.all_gather(all_nb, n_b)
+    dist.all_gather(all_nl, n_l)
+    nbs = [int(x.item()) for x in all_nb]
+    nls = [int(x.item()) for x in all_nl]
+    buf = torch.zeros(max(nbs), dtype=torch.uint8, device=device)
+    buf[:bases_local.numel()] = bases_local
+    got = [torch.empty(max(nbs), dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(got, buf)
+    bases = torch.cat([g[:k] for g, k in zip(got, nbs)])
+    lb = torch.zeros(max(nls), dtype=torch.int64, device=device)
+    lb[:lengths_local.shape[0]] = torch.from_numpy(lengths_local.astype(np.int64)).to(device)
+    gl = [torch.empty(max(nls), dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(gl, lb)
+    lengths = torch.cat([g[:k] for g, k in zip(gl, nls)]).cpu().numpy().astype(np.uint32)
+    return bases, lengths

@@ -1,0 +1,94 @@
+"""The drop-in boundary: libcanu_ovl.so loads, exports exactly what include/canu_ovl.h
+declares, and behaves on the host without a GPU (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from canu_amd import overlap_in_core as oic
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "canu_ovl.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ovl_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_python_exports():
+    assert declared_functions() == sorted(oic.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(built):
+    lib = oic.load_library()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_abi_version(built):
+    assert oic.load_library().ovl_abi_version() == 1
+
+
+def test_params_init_matches_reference_defaults(built):
+    """ovl_params_init = oicParameters::initialize() (overlapInCore.H:425)."""
+    lib = oic.load_library()
+    p = oic._Params()
+    lib.ovl_params_init(ctypes.byref(p))
+    assert p.kmer_len == 0
+    assert p.min_olap_len == 0
+    assert p.partial == 0 and p.unique_olap_per_pair == 1
+    assert p.use_window_filter == 0 and p.use_hopeless_check == 1
+    assert p.frag_olap_limit == (1 << 64) - 1 and p.filter_by_kmer_count == 0
+    assert abs(p.max_erate - 0.06) < 1e-12
+
+
+def test_params_finalize_erate_fixups(built):
+    """main(): maxErate > 0.06 turns off the window filter and the hopeless check."""
+    lib = oic.load_library()
+    p = oic._Params()
+    lib.ovl_params_init(ctypes.byref(p))
+    p.kmer_len = 16
+    p.max_erate = 0.144
+    p.use_window_filter = 1
+    lib.ovl_params_finalize(ctypes.byref(p))
+    assert p.use_window_filter == 0 and p.use_hopeless_check == 0
+
+
+def test_ctx_create_fails_loudly_without_gpu(built):
+    """No silent CPU fallback: without a gfx950 device the context cannot be created."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    lib = oic.load_library()
+    cp = oic.OicParameters(Kmer_Len=22).to_c()
+    ctx = ctypes.c_void_p()
+    rc = lib.ovl_ctx_create(ctypes.byref(cp), 0, ctypes.byref(ctx))
+    assert rc == -1 and not ctx.value
+    assert b"device" in lib.ovl_last_error()
+    with pytest.raises(oic.OvlError):
+        oic.OverlapInCore(oic.OicParameters(Kmer_Len=22), device=0)
+
+
+def test_ctx_create_rejects_bad_params(built):
+    lib = oic.load_library()
+    cp = oic.OicParameters(Kmer_Len=0).to_c()
+    ctx = ctypes.c_void_p()
+    assert lib.ovl_ctx_create(ctypes.byref(cp), 0, ctypes.byref(ctx)) == -2
+
+
+def test_missing_library_raises(tmp_path, monkeypatch):
+    monkeypatch.setattr(oic, "_lib", None)
+    with pytest.raises(oic.OvlError):
+        oic.load_library(str(tmp_path / "nope.so"))
+
+
+def test_record_layout():
+    """ovl_record = {uint32 a_iid, uint32 b_iid, uint64 dat[2]} (ovOverlap.H:270)."""
+    assert ctypes.sizeof(oic._Record) == 24
+    assert oic.RECORD_DTYPE.itemsize == 24
+    r = np.zeros(1, dtype=oic.RECORD_DTYPE)
+    assert r.dtype.names == ("a", "b", "w0", "w1")

@@ -1,0 +1,68 @@
+"""Multi-process path on CPU (gloo, world_size 2): the setup all-gather of the read store
+that bench.py does over RCCL, and independent query shards whose union is the whole job."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle
+    from canu_amd.dist import gather_read_store, query_shards
+    from canu_amd.synth import ReadSet, random_genome, synth_reads
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, L, G = 50, 1800, 9000
+    genome = random_genome(np.random.default_rng(5), G)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    part = synth_reads(n, L, G, 0.02, seed=5, genome=genome, read_range=(lo, hi))
+    bases, lengths = gather_read_store(torch.from_numpy(part.bases), part.lengths, dist,
+                                       torch.device("cpu"))
+    offsets = np.zeros(n, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    rs = ReadSet(bases=bases.numpy(), offsets=offsets, lengths=lengths)
+    p = oracle.default_params(kmer_len=22, max_erate=0.06, min_olap_len=200)
+    q_lo, q_hi = query_shards(n, world)[rank]
+    mine = oracle.run_oracle(rs, p, ref_range=(q_lo, q_hi))
+    counts = [None] * world
+    dist.all_gather_object(counts, mine.tobytes())
+    if rank == 0:
+        whole = synth_reads(n, L, G, 0.02, seed=5, genome=genome)
+        ok_store = (np.array_equal(rs.bases, whole.bases) and
+                    np.array_equal(rs.lengths, whole.lengths))
+        union = np.concatenate([np.frombuffer(b, dtype=oracle.RECORD_DTYPE) for b in counts])
+        ok_union = np.array_equal(oracle.sort_records(union), oracle.run_oracle(whole, p))
+        q.put((ok_store, ok_union, len(union)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_and_shards():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok_store, ok_union, n = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert ok_store and ok_union and n > 0

@@ -1,0 +1,79 @@
+"""GPU path against the REFERENCE's own output (tests/golden, made by tools/make_golden.py
+from overlapInCore compiled from its sources), plus size-independent properties at the
+benchmark's read length."""
+import numpy as np
+import pytest
+
+import oracle
+from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+from canu_amd.synth import synth_reads
+from test_oracle import INDEX, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _P(p):
+    P = OicParameters(Kmer_Len=p["kmer_len"], maxErate=p["max_erate"],
+                      Min_Olap_Len=p["min_olap_len"],
+                      Doing_Partial_Overlaps=bool(p["partial"]),
+                      Unique_Olap_Per_Pair=bool(p["unique_olap_per_pair"]),
+                      Use_Window_Filter=bool(p["use_window_filter"]),
+                      Use_Hopeless_Check=bool(p["use_hopeless_check"]),
+                      Frag_Olap_Limit=int(p["frag_olap_limit"]),
+                      Filter_By_Kmer_Count=int(p["filter_by_kmer_count"]))
+    return P
+
+
+@pytest.mark.parametrize("name", sorted(INDEX))
+def test_golden_gpu(built, name):
+    rs, p, skip, want = load_golden(name)
+    oic = OverlapInCore(_P(p), device=0)
+    got = oic.run(rs, skip_kmers=skip or None)
+    oic.close()
+    assert got.shape == want.shape
+    assert np.array_equal(got, want)
+
+
+def _run(rs, P, ref=None):
+    oic = OverlapInCore(P, device=0)
+    oic.load_reads(rs)
+    oic.build_hash_index(1, rs.nreads)
+    n = oic.find_overlaps(*(ref or (1, rs.nreads)))
+    rec = oic.fetch(n)
+    oic.close()
+    return rec
+
+
+@pytest.fixture(scope="module")
+def ont():
+    # the benchmark's read length / error / coverage, 2k reads (the 50k job is 25x this)
+    return synth_reads(2000, 10_000, 800_000, 0.015, seed=21)
+
+
+def test_ont_query_subset_vs_oracle(built, ont):
+    """Bit-exact at 10 kb reads: a query sub-range against the oracle over the full index."""
+    P = OicParameters(Kmer_Len=22, maxErate=float(np.float32(0.06)), Min_Olap_Len=500)
+    got = _run(ont, P, ref=(900, 960))
+    want = oracle.run_oracle(ont, P.as_dict(), ref_range=(900, 960))
+    assert len(want) > 500
+    assert np.array_equal(got, want)
+
+
+def test_ont_shards_union_and_determinism(built, ont):
+    P = OicParameters(Kmer_Len=22, maxErate=float(np.float32(0.06)), Min_Olap_Len=500)
+    whole = _run(ont, P)
+    again = _run(ont, P)
+    assert np.array_equal(whole, again)
+    from canu_amd.dist import query_shards
+    parts = [_run(ont, P, ref=r) for r in query_shards(ont.nreads, 4)]
+    assert np.array_equal(oracle.sort_records(np.concatenate(parts)), whole)
+    # record invariants: hangs within the reads, span positive, evalue in range
+    L = ont.lengths.astype(np.int64)
+    a, b = whole["a"].astype(np.int64) - 1, whole["b"].astype(np.int64) - 1
+    w0, w1 = whole["w0"], whole["w1"]
+    ahg5, ahg3 = (w0 & 0x1FFFFF).astype(np.int64), ((w0 >> 21) & 0x1FFFFF).astype(np.int64)
+    bhg5, bhg3 = (w1 & 0x1FFFFF).astype(np.int64), ((w1 >> 21) & 0x1FFFFF).astype(np.int64)
+    span = (w1 >> 42) & 0x1FFFFF
+    assert np.all(span > 0) and np.all(((w0 >> 42) & 0xFFF) <= 4095)
+    assert np.all(ahg5 + ahg3 < L[a]) and np.all(bhg5 + bhg3 < L[b])
+    assert np.all(a != b)

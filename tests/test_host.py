@@ -1,0 +1,66 @@
+"""Host-side logic: the overlapInCore command line, the -k skip file, query sharding and
+the synthetic read generator."""
+import numpy as np
+import pytest
+
+from canu_amd.dist import query_shards
+from canu_amd.overlap_in_core import (UINT64_MAX, OicParameters, parse_overlapInCore_args,
+                                      read_skip_fasta)
+from canu_amd.synth import synth_reads
+
+
+def test_parse_defaults_and_options():
+    P, extra = parse_overlapInCore_args(
+        ["-G", "-h", "1-500", "-r", "20-300", "-k", "22", "--maxerate", "0.1", "-m",
+         "--minlength", "500", "-w", "-z", "-l", "7", "-t", "8", "-o", "out.ovb",
+         "--hashbits", "24", "seq.gkpStore"])
+    assert P.Doing_Partial_Overlaps and not P.Unique_Olap_Per_Pair
+    assert (P.bgnHashID, P.endHashID, P.bgnRefID, P.endRefID) == (1, 500, 20, 300)
+    assert P.Kmer_Len == 22 and P.Min_Olap_Len == 500 and P.Frag_Olap_Limit == 7
+    # strtof: the float value of 0.1, not the double
+    assert P.maxErate == float(np.float32(0.1))
+    # maxErate > 0.06 turns off the window filter and the hopeless check (main() fix-up)
+    assert not P.Use_Window_Filter and not P.Use_Hopeless_Check
+    assert extra == {"skip_file": None, "store": "seq.gkpStore", "output": "out.ovb",
+                     "threads": 8}
+
+
+def test_parse_k_file_and_minkmers_order():
+    P, extra = parse_overlapInCore_args(["-k", "mers.fasta", "-k", "18", "--minlength", "100",
+                                         "--maxerate", "0.05", "--minkmers", "-l", "0"])
+    assert extra["skip_file"] == "mers.fasta" and P.Kmer_Len == 18
+    # --minkmers is evaluated where it appears, with the values parsed so far
+    want = int(np.floor(np.exp(-18 * float(np.float32(0.05))) * (100 - 18 + 1)))
+    assert P.Filter_By_Kmer_Count == want
+    assert P.Frag_Olap_Limit == UINT64_MAX          # -l < 1 means no limit
+    assert P.Use_Hopeless_Check                      # 0.05 <= 0.06: untouched
+
+
+def test_read_skip_fasta(tmp_path):
+    f = tmp_path / "m.fasta"
+    f.write_text(">1\nACGTACGTAC\n>2\nTTTTTTTTTT\n")
+    assert read_skip_fasta(str(f), 10) == ["ACGTACGTAC", "TTTTTTTTTT"]
+    with pytest.raises(ValueError):
+        read_skip_fasta(str(f), 11)
+
+
+@pytest.mark.parametrize("n,world", [(1, 1), (10, 3), (1000, 8), (50000, 8), (3, 8)])
+def test_query_shards_cover_and_balance(n, world):
+    sh = query_shards(n, world)
+    assert len(sh) == world
+    ids = [i for lo, hi in sh for i in range(lo, hi + 1)]
+    assert ids == list(range(1, n + 1))
+    if n >= 1000:
+        pairs = [sum(n - a for a in range(lo, hi + 1)) for lo, hi in sh]
+        assert max(pairs) / (sum(pairs) / world) < 1.01
+
+
+def test_synth_slices_match_whole():
+    whole = synth_reads(40, 1500, 10_000, 0.02, seed=9, len_jitter=0.3, n_rate=0.001)
+    a = synth_reads(40, 1500, 10_000, 0.02, seed=9, len_jitter=0.3, n_rate=0.001,
+                    read_range=(0, 17))
+    b = synth_reads(40, 1500, 10_000, 0.02, seed=9, len_jitter=0.3, n_rate=0.001,
+                    read_range=(17, 40))
+    assert b.first_iid == 18
+    assert np.array_equal(np.concatenate([a.bases, b.bases]), whole.bases)
+    assert np.array_equal(np.concatenate([a.lengths, b.lengths]), whole.lengths)

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Summarise tools/prof_traffic.sh output into profiles/:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
+  profiles/<tag>_traffic.csv        per kernel: launches, avg ns, HBM bytes per launch
+  profiles/traffic.json             {kernel: {hbm_bytes_per_step, launches_per_step}} for
+                                    bench.py (the profiled run is one step, no warmup)
+HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and on
+gfx950 FETCH_SIZE reports half the bytes of a coalesced read (MI355X_MICROARCH.md, HBM).
+
+    python tools/pmc_traffic.py <tag>
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+SHORT = {"k_extend": "k_extend", "k_probe": "k_probe", "k_chain": "k_chain",
+         "k_fine": "k_fine", "k_table": "k_table", "k_coarse_scatter": "k_coarse_scatter",
+         "k_coarse_hist": "k_coarse_hist", "k_pack": "k_pack"}
+
+
+def short(name):
+    for k in SHORT:
+        if k + "(" in name or k + "<" in name:
+            return k
+    return None
+
+
+def counters(tag, what):
+    f = glob.glob(os.path.join(OUT, f"{tag}_{what}", "**", "*counter_collection.csv"),
+                  recursive=True)
+    tot, calls = defaultdict(float), defaultdict(set)
+    for path in f:
+        for row in csv.DictReader(open(path)):
+            k = short(row["Kernel_Name"])
+            if k:
+                tot[k] += float(row["Counter_Value"])
+                calls[k].add(row["Dispatch_Id"])
+    return tot, {k: len(v) for k, v in calls.items()}
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    os.makedirs(PROF, exist_ok=True)
+    stats = glob.glob(os.path.join(OUT, f"{tag}_kt", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    fetch, nf = counters(tag, "fetch")
+    write, nw = counters(tag, "write")
+    avg_ns = {}
+    if stats:
+        for row in csv.DictReader(open(stats[0])):
+            k = short(row["Name"])
+            if k:
+                avg_ns[k] = float(row["AverageNs"])
+    traffic = {}
+    with open(os.path.join(PROF, f"{tag}_traffic.csv"), "w") as f:
+        f.write("kernel,launches,avg_ns,fetch_kib_per_launch,write_kib_per_launch,"
+                "hbm_bytes_per_launch\n")
+        for k in sorted(set(fetch) | set(write)):
+            n = max(nf.get(k, 0), nw.get(k, 0), 1)
+            fk, wk = fetch.get(k, 0.0) / n, write.get(k, 0.0) / n
+            b = (2.0 * fk + wk) * 1024.0
+            traffic[k] = {"hbm_bytes_per_step": int(b * n), "launches_per_step": n,
+                          "hbm_bytes_per_launch": int(b)}
+            f.write(f"{k},{n},{avg_ns.get(k, 0):.0f},{fk:.1f},{wk:.1f},{b:.0f}\n")
+    with open(os.path.join(PROF, "traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
