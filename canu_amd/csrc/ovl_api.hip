@@ -606,7 +606,9 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
 
   // extension scratch per wave
   int32_t e_cap = c->h_error_bound[std::min<uint32_t>(c->max_len, AS_MAX_READLEN)] + 2;
-  uint64_t rows_cap = (uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64;
+  // generic kernel: band-compact rows, <= (e_cap+2)^2; staged kernel: 64*OVL_RJ cells per row
+  uint64_t rows_cap = std::max<uint64_t>((uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64,
+                                         (uint64_t)(e_cap + 2) * 64 * OVL_RJ);
   uint64_t per_wave = rows_cap * 4 + 16ull * (e_cap + 2) + 16ull * (e_cap + 8);
   uint32_t ext_waves = 24u * c->n_cu;
   uint64_t budget = 24ull << 30;
@@ -796,8 +798,13 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
         // the generic kernel below
         if (d_defer.alloc(npairs)) return fail(OVL_ERR_OOM, "defer list");
         EA.defer = d_defer.p;
-        hipLaunchKernelGGL(k_extend<true>, dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
-                           stg_lds_wave * stg_wpb + ml_lds, s, EA);
+        // 16-bit traceback cells hold (r << 2 | code) when every r < 2^14
+        if (c->max_len < 16384)
+          hipLaunchKernelGGL((k_extend<true, true>), dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
+                             stg_lds_wave * stg_wpb + ml_lds, s, EA);
+        else
+          hipLaunchKernelGGL((k_extend<true, false>), dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
+                             stg_lds_wave * stg_wpb + ml_lds, s, EA);
         HIPC(hipGetLastError());
         uint32_t nd = 0;
         HIPC(hipMemcpyAsync(&nd, d_ctr.p + 8, 4, hipMemcpyDeviceToHost, s));
@@ -807,11 +814,11 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
           EA.list = d_defer.p;
           EA.npairs = nd;
           EA.pair_next = d_ctr.p + 9;
-          hipLaunchKernelGGL(k_extend<false>, dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
+          hipLaunchKernelGGL((k_extend<false, false>), dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
                              lds, s, EA);
         }
       } else {
-        hipLaunchKernelGGL(k_extend<false>, dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
+        hipLaunchKernelGGL((k_extend<false, false>), dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
                            lds, s, EA);
       }
     }

@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #define OVL_WAVE 64
 

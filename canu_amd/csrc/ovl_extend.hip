@@ -466,14 +466,18 @@ __device__ __forceinline__ int32_t dpp_from_upper(int32_t v, int32_t lane63) {  
 // loaded into registers (lane = diagonal offset -16..16 from the walk's position), and the
 // walk is scalar: one readlane per row.
 typedef __attribute__((address_space(1))) const int32_t g_ci32;
+typedef __attribute__((address_space(1))) const uint16_t g_cu16;
 typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 
+template <bool L16>
 __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t tb_e,
                                                     int32_t tb_d, int32_t last, int32_t *dst,
                                                     uint32_t lane, int32_t &last_out,
                                                     int32_t &nd_out) {
+  constexpr int W = 64 * OVL_RJ;               // cells per logged row
   g_ci32 *rows = (g_ci32 *)WM.rows;
-  g_cu64 *rdir = (g_cu64 *)WM.rowdir;          // per row: (offset - left, left | right << 16)
+  g_cu16 *rows16 = (g_cu16 *)WM.rows;
+  g_ci32 *rdir = (g_ci32 *)WM.rowdir;         // per row: B, the diagonal of cell 0
   vm_sync();                                  // the log is complete
   int32_t d = __builtin_amdgcn_readfirstlane(tb_d);
   last = __builtin_amdgcn_readfirstlane(last);
@@ -481,24 +485,18 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
   int32_t nd = 0;
   for (int32_t kh = tb_e; kh >= 1; kh -= 16) {
     const int32_t dc = d;
-    const int32_t diag = dc - 16 + (int32_t)lane;
-    uint64_t rd[16];
+    const int32_t diag = dc - 16 + (int32_t)(lane <= 32 ? lane : 32);
+    int32_t b[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) rd[i] = rdir[kh - i < 1 ? 1 : kh - i];
+    for (int i = 0; i < 16; i++) b[i] = rdir[kh - i < 1 ? 1 : kh - i];
     int32_t V[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      const int32_t base = (int32_t)(uint32_t)rd[i], lr = (int32_t)(rd[i] >> 32);
-      const int32_t lo = (int32_t)(int16_t)(lr & 0xffff), hi = lr >> 16;
-      const bool ok = (lane <= 32) & (diag >= lo) & (diag <= hi);
-      V[i] = rows[base + (ok ? diag : lo)];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int32_t lr = (int32_t)(rd[i] >> 32);
-      const int32_t lo = (int32_t)(int16_t)(lr & 0xffff), hi = lr >> 16;
-      const bool ok = (lane <= 32) & (diag >= lo) & (diag <= hi);
-      V[i] = ok ? V[i] : 0;
+      const int32_t kk = kh - i < 1 ? 1 : kh - i;
+      int32_t cell = diag - b[i];
+      cell = cell < 0 ? 0 : cell >= W ? W - 1 : cell;   // the walk only reads in-band cells
+      if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
+      else               V[i] = rows[(size_t)kk * W + cell];
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
@@ -522,7 +520,7 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
   nd_out = nd;
 }
 
-template <int DIR, typename SS>
+template <int DIR, typename SS, bool L16>
 __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
                                                          int32_t a0, int32_t m, const SS &T,
                                                          int32_t t0, int32_t n, int32_t limit,
@@ -563,7 +561,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   double  max_score = 0.0;
   int32_t max_score_len = 0, max_score_best_d = 0, max_score_best_e = 0;
   int32_t best_d = 0, best_e = 0, longest = 0;
-  int32_t pl = 0, pr = 0, cursor = 0;
+  int32_t pl = 0, pr = 0;
   int32_t tb_e = -1, tb_d = 0, tb_last = 0;
   bool finished = false;
   const double bmv = X.branch_match_value;
@@ -575,6 +573,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
                      pc_recenter = 0;
   PROF_T(pt_begin);
 #endif
+
+  // code log: row e is a fixed 64*J-cell stripe at e * 64J, cell = d - B_e; rowdir[e] = B_e
+  typedef typename std::conditional<L16, uint16_t, int32_t>::type cell_t;
+  cell_t *clog = (cell_t *)rows;
 
   for (int32_t e = 1; e <= limit; e++) {
     PROF_T(pt_row);
@@ -605,17 +607,12 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       return out;
     }
     const int32_t jr = (right - B) >> 6;
-    // row e's traceback codes cover [left, right]: rowdir[e] = (offset - left, left | right << 16)
-    int32_t *glog = rows + cursor - left;
-    if (lane == 0)
-      ((uint64_t *)rowdir)[e] = (uint32_t)(cursor - left) |
-                                ((uint64_t)(uint32_t)((left & 0xffff) | (right << 16)) << 32);
-    cursor += right - left + 1;
+    const uint32_t span = (uint32_t)(right - left);
+    cell_t *crow = clog + (size_t)e * (64 * J) + lane;
+    if (lane == 0) rowdir[e] = B;
 
-    // ---- the row.  A: neighbours from row e-1 for every chunk (DPP, no LDS).  B: the
-    // first 32-base slide step of every lane of every chunk, branch-free, so the strand
-    // loads of all chunks are in flight together; lanes that matched all 32 continue in a
-    // per-chunk loop.  C: end test and Edit_Match_Limit pruning, chunk by chunk in d order.
+    // ---- A: neighbours from row e-1 for every chunk (DPP, no LDS), max3 with the
+    // traceback's choice (forward.C:62-70: d, then d-1, then d+1, strict >) ------------
     int32_t NR[J], LM[J];
     {
       int32_t carry = -2;                      // row e-1 at diagonal B+64j-1
@@ -628,32 +625,57 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         const int32_t pm = dpp_from_lower(p0, carry);
         const int32_t pp = dpp_from_upper(p0, nxt);
         carry = __builtin_amdgcn_readlane(p0, 63);
-        // the traceback's choice (forward.C:62-70): d, then d-1, then d+1, strict >
-        int32_t r = 1 + p0, code = 0;
-        if (pm > r) { r = pm; code = 1; }
-        if (1 + pp > r) { r = 1 + pp; code = 2; }
-        int32_t lim = m - r;
-        const int32_t l2 = n - r - d;
-        lim = l2 < lim ? l2 : lim;
+        const int32_t r0 = 1 + p0, r2 = 1 + pp;
+        const int32_t r01 = pm > r0 ? pm : r0;
+        const int32_t r = r2 > r01 ? r2 : r01;
+        const int32_t code = (r2 > r01) ? 2 : (pm > r0) ? 1 : 0;
+        crow[64 * j] = (cell_t)((r << 2) | code);
+        const bool act = (uint32_t)(d - left) <= span;
+        const int32_t l1 = m - r, l2 = n - r - d;
         NR[j] = r;
-        const bool act = d >= left && d <= right;
-        LM[j] = act ? lim : 0;
-        if (act) glog[d] = (r << 2) | code;
+        LM[j] = act ? (l1 < l2 ? l1 : l2) : 0;
       }
     }
+
+    // ---- B: first 32-base slide step, per group of 4 chunks all strand loads first ----
     bool more = false;
 #pragma unroll
-    for (int j = 0; j < J; j++) {
-      if (j > jr) break;
-      const int32_t d = B + 64 * j + (int32_t)lane;
-      const int32_t r = NR[j], lim = LM[j];
-      const int32_t pa = (DIR > 0) ? a0 + r : a0 - r;
-      const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d;
-      const int32_t run = first_run<DIR>(A.w, pa, T.w, pt);
-      int32_t k = run < lim ? run : lim;
-      NR[j] = r + (lim > 0 ? k : 0);
-      LM[j] = (run == 32 && lim > 32) ? lim - 32 : 0;
-      more = more || LM[j] > 0;
+    for (int g = 0; g < J; g += 4) {
+      if (g > jr) break;
+      uint64_t wa0[4], wa1[4], wt0[4], wt1[4];
+      uint32_t sha[4], sht[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int j = g + q;
+        if (j <= jr) {
+          const int32_t d = B + 64 * j + (int32_t)lane;
+          const int32_t r = NR[j];
+          const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
+          const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
+          const int32_t ia = pa >> 5, it = pt >> 5;
+          sha[q] = ((uint32_t)pa & 31u) * 2u;
+          sht[q] = ((uint32_t)pt & 31u) * 2u;
+          wa0[q] = A.w[ia]; wa1[q] = A.w[ia + 1];
+          wt0[q] = T.w[it]; wt1[q] = T.w[it + 1];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int j = g + q;
+        if (j > jr) break;
+        const int32_t r = NR[j], lim = LM[j];
+        const uint64_t xa = (wa0[q] >> sha[q]) | ((wa1[q] << 1) << (63u - sha[q]));
+        const uint64_t xt = (wt0[q] >> sht[q]) | ((wt1[q] << 1) << (63u - sht[q]));
+        const uint64_t x = xa ^ xt;
+        const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
+        int32_t run;
+        if (DIR > 0) run = mm ? (int32_t)(__builtin_ctzll(mm) >> 1) : 32;
+        else         run = mm ? (int32_t)(__builtin_clzll(mm) >> 1) : 32;
+        const int32_t k = run < lim ? run : lim;
+        NR[j] = r + (lim > 0 ? k : 0);
+        LM[j] = ((run == 32) & (lim > 32)) ? lim - 32 : 0;
+        more = more | (LM[j] > 0);
+      }
     }
 #ifdef OVL_PROFILE
     pc_nch += jr + 1;
@@ -671,6 +693,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #endif
       }
     }
+
+    // ---- C: end test (first d in order) and Edit_Match_Limit pruning -----------------
     int32_t nl = NONE, nr = NEG;
     bool ended = false;
     int32_t end_d = 0, end_row = 0, end_pp = 0;
@@ -679,25 +703,24 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       if (j > jr) break;
       const int32_t c = B + 64 * j;
       const int32_t d = c + (int32_t)lane;
-      const bool act = d >= left && d <= right;
+      const bool act = (uint32_t)(d - left) <= span;
       const int32_t r = NR[j];
-      const uint64_t endm = __ballot(act && (r == m || r + d == n));
+      const uint64_t endm = __ballot(act & ((r == m) | (r + d == n)));
       if (endm) {
         const int32_t l = (int32_t)__builtin_ctzll(endm);
         end_d = c + l;
         end_row = __builtin_amdgcn_readlane(r, l);
-        // row e-1 at d+1 (R still holds row e-1 from chunk j on)
+        // row e-1 at d+1 (R still holds row e-1)
         end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
                : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
         ended = true;
         break;
       }
-      const uint64_t km = __ballot(act && (((d < 0) ? r : r + d) >= ML));
-      if (km) {
-        if (nl == NONE) nl = c + (int32_t)__builtin_ctzll(km);
-        nr = c + 63 - (int32_t)__builtin_clzll(km);
-      }
-      R[j] = act ? r : -2;
+      const uint64_t km = __ballot(act & (r + (d > 0 ? d : 0) >= ML));
+      const int32_t f = c + (int32_t)__builtin_ctzll(km);
+      const int32_t h = c + 63 - (int32_t)__builtin_clzll(km);
+      nl = (km != 0 && nl == NONE) ? f : nl;
+      nr = (km != 0) ? h : nr;
     }
 
     PROF_T(pt_chunks);
@@ -735,11 +758,12 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 
     // prune to [nl, nr] (the rest becomes the -2 sentinel), longest row, first d on ties
     int32_t mx = NEG;
+    const uint32_t kspan = (uint32_t)(nr - nl);
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
-      const int32_t v = (d >= nl && d <= nr) ? R[j] : -2;
+      const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
       R[j] = v;
       mx = v > mx ? v : mx;
     }
@@ -776,7 +800,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
-  ped_traceback_codes(WM, tb_e, tb_d, tb_last, dst, lane, last, nd);
+  ped_traceback_codes<L16>(WM, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
 #ifdef OVL_PROFILE
@@ -812,7 +836,7 @@ struct ExtOut {
 };
 
 // Extend_Alignment (prefixEditDistance-extend.C:86).  Leaves the merged Left_Delta in LD.
-template <bool FAST, typename SS>
+template <bool FAST, bool L16, typename SS>
 __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS &S,
                                    int32_t S_Len, const SS &T, int32_t T_Len,
                                    const WaveMem &WM, int32_t *stk, int32_t *RD,
@@ -840,7 +864,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     int32_t am = s_first ? S_Right_Len : T_Right_Len;
     int32_t bn = s_first ? T_Right_Len : S_Right_Len;
     PedOut po;
-    if constexpr (FAST) po = wave_ped_reg<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    if constexpr (FAST) po = wave_ped_reg<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
     else                po = wave_ped<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
     if (po.ovf) { r.kind = -1; return r; }
     right_errors = po.err;
@@ -875,7 +899,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     int32_t a0 = s_first ? S_Left_Begin : T_Left_Begin;
     int32_t b0 = s_first ? T_Left_Begin : S_Left_Begin;
     PedOut po;
-    if constexpr (FAST) po = wave_ped_reg<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    if constexpr (FAST) po = wave_ped_reg<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
     else                po = wave_ped<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
     if (po.ovf) { r.kind = -1; return r; }
     left_errors = po.err;
@@ -1066,7 +1090,7 @@ __device__ bool lies_on_alignment(int32_t start, int32_t offset, int32_t s_lo, i
 // Returns false when the pair must be redone by the generic kernel (register window
 // overflow); nothing has been output for it then, and removed nodes are marked ~Len so the
 // generic kernel can restore them.
-template <bool FAST, typename SS>
+template <bool FAST, bool L16, typename SS>
 __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &un,
                              const SS &S, const SS &T, const WaveMem &WM, int32_t *stk,
                              int32_t *RD, int32_t *LD, unsigned long long *st, uint32_t lane) {
@@ -1125,7 +1149,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     wave_argmax(bv, bi);
     Node M = nodes[bi];
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
-    ExtOut eo = extend_alignment<FAST>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+    ExtOut eo = extend_alignment<FAST, L16>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
     if (FAST && eo.kind < 0) return false;
     kind = eo.kind;
     S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
@@ -1248,7 +1272,8 @@ static_assert(OVL_SCR >= TB_ROWS * TB_W && OVL_SCR >= 64 * OVL_RJ, "scratch too 
 // STAGE = true: exception-free pairs, strands staged in LDS, rows in registers; pairs with
 // 'n' bases or a band wider than the register window are deferred to the generic kernel.
 // STAGE = false: the generic kernel (global strands with exception masks, rows in LDS).
-template <bool STAGE>
+// L16: every read < 16384 bases, so the traceback code log holds 16-bit cells
+template <bool STAGE, bool L16>
 __global__ void __launch_bounds__(256, 4) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1308,7 +1333,7 @@ __global__ void __launch_bounds__(256, 4) k_extend(ExtendArgs X) {
         StrandLP TL = stage_strand(T, tw, lane);
         lds_sync();
         PROF_T(pp0);
-        ok = process_pair<true>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane);
+        ok = process_pair<true, L16>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane);
 #ifdef OVL_PROFILE
         PROF_T(pp1);
         if (X.dbg && lane == 0) atomicAdd(&X.dbg[13], pp1 - pp0);
@@ -1323,7 +1348,7 @@ __global__ void __launch_bounds__(256, 4) k_extend(ExtendArgs X) {
           if (nodes[i].Len < 0) nodes[i].Len = ~nodes[i].Len;
         vm_sync();
       }
-      process_pair<false>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
+      process_pair<false, false>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
     }
     lds_sync();
   }
