@@ -393,52 +393,55 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #define PROF_ADD(acc, a, b)
 #endif
 
-// 32 bases of an LDS strand starting at p; p may be negative (the words before the strand
-// are other LDS data: those bases lie beyond the comparison limit and are never counted).
-__device__ __forceinline__ uint64_t lds_bases(const lds_u64 *w, int32_t p) {
-  int32_t wi = p >> 5;
-  uint32_t sh = ((uint32_t)p & 31u) * 2u;
-  uint64_t lo = w[wi], hi = w[wi + 1];
-  return (lo >> sh) | ((hi << 1) << (63u - sh));
+// Staged strands are kept in LDS as BIT PLANES: word w holds bases 32w..32w+31 as
+// (plane0 = low code bits) | (plane1 = high code bits) << 32, so 32 bases at any offset are
+// two v_alignbit_b32 per strand and a mismatch mask is 32 bits wide.
+__device__ __forceinline__ uint32_t compact_even(uint64_t x) {   // bits 0,2,..,62 -> 0..31
+  x &= 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+  return (uint32_t)x;
 }
 
-// slide on exception-free LDS strands: DIR=+1 compares A[pa..], T[pt..]; DIR=-1 compares
-// A[pa], A[pa-1], .. with T[pt], T[pt-1], ..; at most lim (> 0) bases.
+// Mismatch mask of the 32 bases at a[pa..pa+31] vs t[pt..pt+31] (bit i = base i); pa, pt
+// may be negative (the words before a strand are other LDS data: those bases lie beyond
+// the comparison limit and are never counted).
+__device__ __forceinline__ uint32_t plane_mismatch(const lds_u64 *a, int32_t pa,
+                                                   const lds_u64 *t, int32_t pt) {
+  const int32_t ia = pa >> 5, it = pt >> 5;
+  const uint64_t a0 = a[ia], a1 = a[ia + 1], t0 = t[it], t1 = t[it + 1];
+  const uint32_t sa = (uint32_t)pa & 31u, st = (uint32_t)pt & 31u;
+  const uint32_t xa0 = __builtin_amdgcn_alignbit((uint32_t)a1, (uint32_t)a0, sa);
+  const uint32_t xa1 = __builtin_amdgcn_alignbit((uint32_t)(a1 >> 32), (uint32_t)(a0 >> 32), sa);
+  const uint32_t xt0 = __builtin_amdgcn_alignbit((uint32_t)t1, (uint32_t)t0, st);
+  const uint32_t xt1 = __builtin_amdgcn_alignbit((uint32_t)(t1 >> 32), (uint32_t)(t0 >> 32), st);
+  return (xa0 ^ xt0) | (xa1 ^ xt1);
+}
+
+__device__ __forceinline__ int32_t run_fwd(uint32_t mm) {   // matches from bit 0 up
+  return mm ? (int32_t)__builtin_ctz(mm) : 32;
+}
+__device__ __forceinline__ int32_t run_bwd(uint32_t mm) {   // matches from bit 31 down
+  return mm ? (int32_t)__builtin_clz(mm) : 32;
+}
+
+// slide on exception-free LDS plane strands: DIR=+1 compares A[pa..], T[pt..]; DIR=-1
+// compares A[pa], A[pa-1], .. with T[pt], T[pt-1], ..; at most lim (> 0) bases.
 template <int DIR>
 __device__ __forceinline__ int32_t slide_lds(const lds_u64 *a, int32_t pa, const lds_u64 *t,
                                              int32_t pt, int32_t lim) {
   int32_t k = 0;
   for (;;) {
-    uint64_t x, mm;
     int32_t run;
-    if (DIR > 0) {
-      x = lds_bases(a, pa + k) ^ lds_bases(t, pt + k);
-      mm = (x | (x >> 1)) & 0x5555555555555555ull;
-      run = mm ? (int32_t)(__builtin_ctzll(mm) >> 1) : 32;
-    } else {
-      x = lds_bases(a, pa - k - 31) ^ lds_bases(t, pt - k - 31);
-      mm = (x | (x >> 1)) & 0x5555555555555555ull;
-      run = mm ? (int32_t)(__builtin_clzll(mm) >> 1) : 32;
-    }
+    if (DIR > 0) run = run_fwd(plane_mismatch(a, pa + k, t, pt + k));
+    else         run = run_bwd(plane_mismatch(a, pa - k - 31, t, pt - k - 31));
     k += run;
     if (run < 32 || k >= lim) break;
   }
   return k < lim ? k : lim;
-}
-
-// Matching bases (0..32) at the first step of a slide, no limit applied.
-template <int DIR>
-__device__ __forceinline__ int32_t first_run(const lds_u64 *a, int32_t pa, const lds_u64 *t,
-                                             int32_t pt) {
-  if (DIR > 0) {
-    const uint64_t x = lds_bases(a, pa) ^ lds_bases(t, pt);
-    const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
-    return mm ? (int32_t)(__builtin_ctzll(mm) >> 1) : 32;
-  } else {
-    const uint64_t x = lds_bases(a, pa - 31) ^ lds_bases(t, pt - 31);
-    const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
-    return mm ? (int32_t)(__builtin_clzll(mm) >> 1) : 32;
-  }
 }
 
 template <int DIR, typename SS>
@@ -653,8 +656,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
           const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
           const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
           const int32_t ia = pa >> 5, it = pt >> 5;
-          sha[q] = ((uint32_t)pa & 31u) * 2u;
-          sht[q] = ((uint32_t)pt & 31u) * 2u;
+          sha[q] = (uint32_t)pa & 31u;
+          sht[q] = (uint32_t)pt & 31u;
           wa0[q] = A.w[ia]; wa1[q] = A.w[ia + 1];
           wt0[q] = T.w[it]; wt1[q] = T.w[it + 1];
         }
@@ -664,13 +667,14 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         const int j = g + q;
         if (j > jr) break;
         const int32_t r = NR[j], lim = LM[j];
-        const uint64_t xa = (wa0[q] >> sha[q]) | ((wa1[q] << 1) << (63u - sha[q]));
-        const uint64_t xt = (wt0[q] >> sht[q]) | ((wt1[q] << 1) << (63u - sht[q]));
-        const uint64_t x = xa ^ xt;
-        const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
-        int32_t run;
-        if (DIR > 0) run = mm ? (int32_t)(__builtin_ctzll(mm) >> 1) : 32;
-        else         run = mm ? (int32_t)(__builtin_clzll(mm) >> 1) : 32;
+        const uint32_t xa0 = __builtin_amdgcn_alignbit((uint32_t)wa1[q], (uint32_t)wa0[q], sha[q]);
+        const uint32_t xa1 = __builtin_amdgcn_alignbit((uint32_t)(wa1[q] >> 32),
+                                                       (uint32_t)(wa0[q] >> 32), sha[q]);
+        const uint32_t xt0 = __builtin_amdgcn_alignbit((uint32_t)wt1[q], (uint32_t)wt0[q], sht[q]);
+        const uint32_t xt1 = __builtin_amdgcn_alignbit((uint32_t)(wt1[q] >> 32),
+                                                       (uint32_t)(wt0[q] >> 32), sht[q]);
+        const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
+        const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
         const int32_t k = run < lim ? run : lim;
         NR[j] = r + (lim > 0 ? k : 0);
         LM[j] = ((run == 32) & (lim > 32)) ? lim - 32 : 0;
@@ -1258,7 +1262,10 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
 // staged: the staged kernel defers pairs with 'n' bases to the generic kernel.
 __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, uint32_t lane) {
   int32_t nw = (G.len + 31) / 32 + 1;
-  for (int32_t i = lane; i < nw; i += 64) dst[i] = G.w[i];
+  for (int32_t i = lane; i < nw; i += 64) {
+    const uint64_t w = G.w[i];
+    dst[i] = (uint64_t)compact_even(w) | ((uint64_t)compact_even(w >> 1) << 32);
+  }
   StrandLP L;
   L.w = dst;
   L.len = G.len;
