@@ -472,6 +472,10 @@ typedef __attribute__((address_space(1))) const int32_t g_ci32;
 typedef __attribute__((address_space(1))) const uint16_t g_cu16;
 typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 
+// Set_Right_Delta / Set_Left_Delta (forward.C:48, reverse.C:52) over the row log of
+// wave_ped_reg: row k's stripe holds L[k][d] (-2 outside the pruned band).  For 16 rows at a
+// time the previous rows are loaded into registers (lane = diagonal offset -17..17 from the
+// walk's position) and the walk is scalar, three readlanes per row.
 template <bool L16>
 __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t tb_e,
                                                     int32_t tb_d, int32_t last, int32_t *dst,
@@ -479,7 +483,8 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
                                                     int32_t &nd_out) {
   constexpr int W = 64 * OVL_RJ;               // cells per logged row
   g_ci32 *rows = (g_ci32 *)WM.rows;
-  g_cu16 *rows16 = (g_cu16 *)WM.rows;
+  typedef __attribute__((address_space(1))) const int16_t g_ci16;
+  g_ci16 *rows16 = (g_ci16 *)WM.rows;
   g_ci32 *rdir = (g_ci32 *)WM.rowdir;         // per row: B, the diagonal of cell 0
   vm_sync();                                  // the log is complete
   int32_t d = __builtin_amdgcn_readfirstlane(tb_d);
@@ -488,33 +493,39 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
   int32_t nd = 0;
   for (int32_t kh = tb_e; kh >= 1; kh -= 16) {
     const int32_t dc = d;
-    const int32_t diag = dc - 16 + (int32_t)(lane <= 32 ? lane : 32);
+    const int32_t diag = dc - 17 + (int32_t)(lane <= 34 ? lane : 34);
     int32_t b[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) b[i] = rdir[kh - i < 1 ? 1 : kh - i];
+    for (int i = 0; i < 16; i++) b[i] = rdir[kh - 1 - i < 0 ? 0 : kh - 1 - i];
     int32_t V[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      const int32_t kk = kh - i < 1 ? 1 : kh - i;
+      const int32_t kk = kh - 1 - i < 0 ? 0 : kh - 1 - i;   // row k-1 for k = kh - i
       int32_t cell = diag - b[i];
-      cell = cell < 0 ? 0 : cell >= W ? W - 1 : cell;   // the walk only reads in-band cells
+      cell = cell < 0 ? 0 : cell >= W ? W - 1 : cell;       // the walk reads in-band cells
       if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
       else               V[i] = rows[(size_t)kk * W + cell];
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       if (kh - i < 1) break;
-      const int32_t p = __builtin_amdgcn_readlane(V[i], 16 + d - dc);
-      const int32_t code = p & 3, val = p >> 2;
-      if (code == 1) {
-        if (lane == 0) dst[nd] = val - last - 1;
+      const int32_t x = 17 + d - dc;
+      const int32_t pm = __builtin_amdgcn_readlane(V[i], x - 1);
+      const int32_t p0 = __builtin_amdgcn_readlane(V[i], x);
+      const int32_t pp = __builtin_amdgcn_readlane(V[i], x + 1);
+      int32_t mx = 1 + p0;
+      int32_t from = 0;
+      if (pm > mx) { from = -1; mx = pm; }
+      if (1 + pp > mx) { from = 1; mx = 1 + pp; }
+      if (from < 0) {
+        if (lane == 0) dst[nd] = mx - last - 1;
         nd++;
-        last = val;
+        last = pm;
         d--;
-      } else if (code == 2) {
-        if (lane == 0) dst[nd] = last - val + 1;
+      } else if (from > 0) {
+        if (lane == 0) dst[nd] = last - (mx - 1);
         nd++;
-        last = val - 1;
+        last = pp;
         d++;
       }
     }
@@ -577,9 +588,15 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   PROF_T(pt_begin);
 #endif
 
-  // code log: row e is a fixed 64*J-cell stripe at e * 64J, cell = d - B_e; rowdir[e] = B_e
-  typedef typename std::conditional<L16, uint16_t, int32_t>::type cell_t;
+  // Row log for the traceback: row e (after pruning, -2 outside [nl, nr]) is a fixed
+  // 64*J-cell stripe at e * 64J, cell = d - B_e; rowdir[e] = B_e.  Row 0 is logged here.
+  typedef typename std::conditional<L16, int16_t, int32_t>::type cell_t;
   cell_t *clog = (cell_t *)rows;
+  clog[lane] = (cell_t)R[0];
+  if (lane == 0) rowdir[0] = B;
+  // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
+  // interleave); their lanes beyond the band are inactive by the lane predicates
+  constexpr int JU = 2;
 
   for (int32_t e = 1; e <= limit; e++) {
     PROF_T(pt_row);
@@ -611,17 +628,15 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     }
     const int32_t jr = (right - B) >> 6;
     const uint32_t span = (uint32_t)(right - left);
-    cell_t *crow = clog + (size_t)e * (64 * J) + lane;
     if (lane == 0) rowdir[e] = B;
 
-    // ---- A: neighbours from row e-1 for every chunk (DPP, no LDS), max3 with the
-    // traceback's choice (forward.C:62-70: d, then d-1, then d+1, strict >) ------------
+    // ---- A: neighbours from row e-1 for every chunk (DPP, no LDS) --------------------
     int32_t NR[J], LM[J];
     {
       int32_t carry = -2;                      // row e-1 at diagonal B+64j-1
 #pragma unroll
       for (int j = 0; j < J; j++) {
-        if (j > jr) break;
+        if (j >= JU && j > jr) break;
         const int32_t d = B + 64 * j + (int32_t)lane;
         const int32_t p0 = R[j];
         const int32_t nxt = (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
@@ -629,10 +644,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         const int32_t pp = dpp_from_upper(p0, nxt);
         carry = __builtin_amdgcn_readlane(p0, 63);
         const int32_t r0 = 1 + p0, r2 = 1 + pp;
-        const int32_t r01 = pm > r0 ? pm : r0;
-        const int32_t r = r2 > r01 ? r2 : r01;
-        const int32_t code = (r2 > r01) ? 2 : (pm > r0) ? 1 : 0;
-        crow[64 * j] = (cell_t)((r << 2) | code);
+        const int32_t r = (pm > r0 ? pm : r0) > r2 ? (pm > r0 ? pm : r0) : r2;
         const bool act = (uint32_t)(d - left) <= span;
         const int32_t l1 = m - r, l2 = n - r - d;
         NR[j] = r;
@@ -641,16 +653,16 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     }
 
     // ---- B: first 32-base slide step, per group of 4 chunks all strand loads first ----
-    bool more = false;
+    uint64_t need[J];
 #pragma unroll
     for (int g = 0; g < J; g += 4) {
-      if (g > jr) break;
+      if (g >= JU && g > jr) break;
       uint64_t wa0[4], wa1[4], wt0[4], wt1[4];
       uint32_t sha[4], sht[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int j = g + q;
-        if (j <= jr) {
+        if (j < JU || j <= jr) {
           const int32_t d = B + 64 * j + (int32_t)lane;
           const int32_t r = NR[j];
           const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
@@ -665,8 +677,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int j = g + q;
-        if (j > jr) break;
-        const int32_t r = NR[j], lim = LM[j];
+        if (j >= JU && j > jr) break;
+        const int32_t lim = LM[j];
         const uint32_t xa0 = __builtin_amdgcn_alignbit((uint32_t)wa1[q], (uint32_t)wa0[q], sha[q]);
         const uint32_t xa1 = __builtin_amdgcn_alignbit((uint32_t)(wa1[q] >> 32),
                                                        (uint32_t)(wa0[q] >> 32), sha[q]);
@@ -675,56 +687,81 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
                                                        (uint32_t)(wt0[q] >> 32), sht[q]);
         const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
         const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
+        // k = min(run, lim) when lim > 0, else 0  (run >= 0)
         const int32_t k = run < lim ? run : lim;
-        NR[j] = r + (lim > 0 ? k : 0);
-        LM[j] = ((run == 32) & (lim > 32)) ? lim - 32 : 0;
-        more = more | (LM[j] > 0);
+        NR[j] += k > 0 ? k : 0;
+        need[j] = __ballot((run == 32) & (lim > 32));
       }
     }
 #ifdef OVL_PROFILE
-    pc_nch += jr + 1;
+    pc_nch += (jr + 1 > JU ? jr + 1 : JU);
 #endif
-    if (__ballot(more)) {
+    // lanes that matched all 32 bases continue (the on-path diagonals): one loop over all
+    // chunks so their LDS loads overlap
+    {
+      uint64_t any = 0;
 #pragma unroll
       for (int j = 0; j < J; j++) {
-        if (j > jr) break;
-        if (LM[j] > 0) {
-          const int32_t d = B + 64 * j + (int32_t)lane;
-          NR[j] += slide_any<DIR>(A, a0, T, t0, NR[j], d, LM[j]);
-        }
+        if (j >= JU && j > jr) break;
+        any |= need[j];
+      }
+      if (any) {
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+          if (j >= JU && j > jr) break;
+          if (need[j] & (1ull << lane)) {
+            const int32_t d = B + 64 * j + (int32_t)lane;
+            NR[j] += slide_any<DIR>(A, a0, T, t0, NR[j], d, LM[j] - 32);
+          }
 #ifdef OVL_PROFILE
-        pc_slide++;
+          if (need[j]) pc_slide++;
 #endif
+        }
       }
     }
 
     // ---- C: end test (first d in order) and Edit_Match_Limit pruning -----------------
-    int32_t nl = NONE, nr = NEG;
-    bool ended = false;
-    int32_t end_d = 0, end_row = 0, end_pp = 0;
+    uint64_t em[J], km[J], endany = 0;
 #pragma unroll
     for (int j = 0; j < J; j++) {
-      if (j > jr) break;
-      const int32_t c = B + 64 * j;
-      const int32_t d = c + (int32_t)lane;
+      if (j >= JU && j > jr) break;
+      const int32_t d = B + 64 * j + (int32_t)lane;
       const bool act = (uint32_t)(d - left) <= span;
       const int32_t r = NR[j];
-      const uint64_t endm = __ballot(act & ((r == m) | (r + d == n)));
-      if (endm) {
-        const int32_t l = (int32_t)__builtin_ctzll(endm);
-        end_d = c + l;
-        end_row = __builtin_amdgcn_readlane(r, l);
-        // row e-1 at d+1 (R still holds row e-1)
-        end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
-               : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
-        ended = true;
-        break;
+      em[j] = __ballot(act & ((r == m) | (r + d == n)));
+      km[j] = __ballot(act & (r + (d > 0 ? d : 0) >= ML));
+      endany |= em[j];
+    }
+    bool ended = false;
+    int32_t end_d = 0, end_row = 0, end_pp = 0;
+    int32_t nl = NONE, nr = NEG;
+    if (endany) {
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        if (j >= JU && j > jr) break;
+        if (em[j]) {
+          const int32_t l = (int32_t)__builtin_ctzll(em[j]);
+          end_d = B + 64 * j + l;
+          end_row = __builtin_amdgcn_readlane(NR[j], l);
+          // row e-1 at d+1 (R still holds row e-1)
+          end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
+                 : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
+          ended = true;
+          break;
+        }
       }
-      const uint64_t km = __ballot(act & (r + (d > 0 ? d : 0) >= ML));
-      const int32_t f = c + (int32_t)__builtin_ctzll(km);
-      const int32_t h = c + 63 - (int32_t)__builtin_clzll(km);
-      nl = (km != 0 && nl == NONE) ? f : nl;
-      nr = (km != 0) ? h : nr;
+    }
+    if (!ended) {
+#pragma unroll
+      for (int j = J - 1; j >= 0; j--) {       // first chunk with a kept lane, from the top
+        if (j >= JU && j > jr) continue;
+        if (km[j]) nl = B + 64 * j + (int32_t)__builtin_ctzll(km[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < J; j++) {            // last chunk with a kept lane
+        if (j >= JU && j > jr) break;
+        if (km[j]) nr = B + 64 * j + 63 - (int32_t)__builtin_clzll(km[j]);
+      }
     }
 
     PROF_T(pt_chunks);
@@ -760,23 +797,27 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     }
     if (nl == NONE) break;                     // Left > Right
 
-    // prune to [nl, nr] (the rest becomes the -2 sentinel), longest row, first d on ties
+    // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
+    // traceback (cells up to nr+2 are read), longest row with the first d on ties
     int32_t mx = NEG;
     const uint32_t kspan = (uint32_t)(nr - nl);
+    const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
+    cell_t *crow = clog + (size_t)e * (64 * J) + lane;
 #pragma unroll
     for (int j = 0; j < J; j++) {
-      if (j > jr) break;
+      if (j >= JU && j > jrs) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
       R[j] = v;
       mx = v > mx ? v : mx;
+      crow[64 * j] = (cell_t)v;
     }
     const int32_t M = wave_max(mx);
     if (M > longest) {
       int32_t bd = NONE;
 #pragma unroll
       for (int j = 0; j < J; j++) {
-        if (j > jr) break;
+        if (j >= JU && j > jr) break;
         const uint64_t b = __ballot(R[j] == M);
         if (b) { bd = B + 64 * j + (int32_t)__builtin_ctzll(b); break; }
       }
