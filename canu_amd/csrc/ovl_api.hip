@@ -839,9 +839,9 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     (void)hipMemcpy(dd, dbg_ptr_for_print, 128, hipMemcpyDeviceToHost);
     fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu slide_iters=%llu tb=%llu iters=%llu "
             "cyc_chunks=%llu cyc_tb=%llu pairs=%llu maxrows=%llu cyc_rest=%llu cyc_ped=%llu "
-            "recenter=%llu cyc_pair=%llu\n",
+            "cyc_calls=%llu cyc_pair=%llu cyc_stage=%llu cyc_extend=%llu\n",
             dd[0], dd[1], dd[2], dd[3], dd[4], dd[5], dd[6], dd[7], dd[8], dd[9], dd[10], dd[11],
-            dd[12], dd[13]);
+            dd[12], dd[13], dd[14], dd[15]);
   }
   c->stats.kmer_hits_without_olap = hs[0];
   c->stats.kmer_hits_with_olap = hs[1];

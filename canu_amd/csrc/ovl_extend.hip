@@ -69,6 +69,8 @@ struct PedOut {
   int32_t ovf;             // register window overflow: the pair goes to the generic kernel
 };
 
+// Orders this wave's global-memory accesses across lanes (lane 0 writes, others read, or
+// the reverse): wait for the wave's outstanding vector memory operations.
 __device__ __forceinline__ void vm_sync() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
@@ -602,22 +604,43 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     PROF_T(pt_row);
     const int32_t ML = WM.mlim[e];
     const int32_t left = pl - 1, right = pr + 1;
-    // The window is anchored at the band: B <= pl-3 < B+64, so the row's chunks are
-    // 0..jr.  It must also hold pr+3 (the reads of this row and the log of the next).
-    if (pl - 3 < B) {                          // pl moves down by at most 1 per row
+    // The window is anchored at the band: B <= pl-3 < B+16, so the row's chunks are
+    // 0..jr with little waste in chunk 0.  When pl-3 leaves [B, B+16) the window moves to
+    // B = pl-9: whole chunks by register moves, the rest by one ds_bpermute per chunk
+    // (about one row in ten).  It must also hold pr+3 (the reads of this row and the log
+    // of the next).
+    if (pl - 3 < B || pl - 3 - B >= 16) {
+      const int32_t nb = pl - 9;
+      int32_t sft = nb - B;
+      while (sft >= 64) {
 #pragma unroll
-      for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
-      R[0] = -2;
-      B -= 64;
-#ifdef OVL_PROFILE
-      pc_recenter++;
-#endif
-    }
-    while (pl - 3 >= B + 64) {                 // pruning can move it up by any amount
+        for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
+        R[J - 1] = -2;
+        sft -= 64;
+      }
+      while (sft <= -64) {
 #pragma unroll
-      for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
-      R[J - 1] = -2;
-      B += 64;
+        for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
+        R[0] = -2;
+        sft += 64;
+      }
+      if (sft != 0) {
+        const int32_t ls = (int32_t)lane + sft;
+        const int32_t src = (ls & 63) << 2;
+        int32_t bp[J];
+#pragma unroll
+        for (int j = 0; j < J; j++) bp[j] = __builtin_amdgcn_ds_bpermute(src, R[j]);
+        if (sft > 0) {
+          const bool hi = ls >= 64;            // comes from the next chunk up
+#pragma unroll
+          for (int j = 0; j < J; j++) R[j] = hi ? (j + 1 < J ? bp[j + 1 < J ? j + 1 : j] : -2) : bp[j];
+        } else {
+          const bool lo = ls < 0;              // comes from the chunk below
+#pragma unroll
+          for (int j = 0; j < J; j++) R[j] = lo ? (j > 0 ? bp[j > 0 ? j - 1 : 0] : -2) : bp[j];
+        }
+      }
+      B = nb;
 #ifdef OVL_PROFILE
       pc_recenter++;
 #endif
@@ -860,7 +883,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     atomicAdd(&X.dbg[7], pt_tb1 - pt_tb0);
     atomicAdd(&X.dbg[10], pc_rest);
     atomicAdd(&X.dbg[11], pt_tb1 - pt_begin);
-    atomicAdd(&X.dbg[12], pc_recenter);
+    (void)pc_recenter;
   }
 #endif
   return out;
@@ -909,8 +932,13 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     int32_t am = s_first ? S_Right_Len : T_Right_Len;
     int32_t bn = s_first ? T_Right_Len : S_Right_Len;
     PedOut po;
+    PROF_T(pc0);
     if constexpr (FAST) po = wave_ped_reg<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
     else                po = wave_ped<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+#ifdef OVL_PROFILE
+    PROF_T(pc1);
+    if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc1 - pc0);
+#endif
     if (po.ovf) { r.kind = -1; return r; }
     right_errors = po.err;
     rmte = po.mte;
@@ -944,8 +972,13 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     int32_t a0 = s_first ? S_Left_Begin : T_Left_Begin;
     int32_t b0 = s_first ? T_Left_Begin : S_Left_Begin;
     PedOut po;
+    PROF_T(pc2);
     if constexpr (FAST) po = wave_ped_reg<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
     else                po = wave_ped<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+#ifdef OVL_PROFILE
+    PROF_T(pc3);
+    if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc3 - pc2);
+#endif
     if (po.ovf) { r.kind = -1; return r; }
     left_errors = po.err;
     lmte = po.mte;
@@ -960,10 +993,15 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
       if (fix) {
         int32_t l1 = LD[1];
         vm_sync();
-        if (lane == 0) {
-          LD[0] = (l1 > 0) ? l1 + 1 : l1 - 1;
-          for (int32_t i = 2; i < ld_len; i++) LD[i - 1] = LD[i];
+        // LD[i-1] = LD[i] for i >= 2, lane-parallel: each pass reads above what it writes
+        for (int32_t i0 = 2; i0 < ld_len; i0 += 64) {
+          const int32_t i = i0 + (int32_t)lane;
+          const int32_t v = (i < ld_len) ? LD[i] : 0;
+          vm_sync();
+          if (i < ld_len) LD[i - 1] = v;
+          vm_sync();
         }
+        if (lane == 0) LD[0] = (l1 > 0) ? l1 + 1 : l1 - 1;
         ld_len--;
         t_end--;
         if (ld_len == 0) leftover++;
@@ -1194,7 +1232,12 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     wave_argmax(bv, bi);
     Node M = nodes[bi];
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
+    PROF_T(px0);
     ExtOut eo = extend_alignment<FAST, L16>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+#ifdef OVL_PROFILE
+    PROF_T(px1);
+    if (X.dbg && lane == 0) atomicAdd(&X.dbg[15], px1 - px0);
+#endif
     if (FAST && eo.kind < 0) return false;
     kind = eo.kind;
     S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
