@@ -483,35 +483,30 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
                                                     int32_t tb_d, int32_t last, int32_t *dst,
                                                     uint32_t lane, int32_t &last_out,
                                                     int32_t &nd_out) {
-  constexpr int W = 64 * OVL_RJ;               // cells per logged row
+  constexpr int W = 64 * OVL_RJ;               // cells per logged row, cell = d mod W
+  constexpr int TBR = 30;                      // rows per window: lanes cover dc-31..dc+31
   g_ci32 *rows = (g_ci32 *)WM.rows;
   typedef __attribute__((address_space(1))) const int16_t g_ci16;
   g_ci16 *rows16 = (g_ci16 *)WM.rows;
-  g_ci32 *rdir = (g_ci32 *)WM.rowdir;         // per row: B, the diagonal of cell 0
   vm_sync();                                  // the log is complete
   int32_t d = __builtin_amdgcn_readfirstlane(tb_d);
   last = __builtin_amdgcn_readfirstlane(last);
   tb_e = __builtin_amdgcn_readfirstlane(tb_e);
   int32_t nd = 0;
-  for (int32_t kh = tb_e; kh >= 1; kh -= 16) {
+  for (int32_t kh = tb_e; kh >= 1; kh -= TBR) {
     const int32_t dc = d;
-    const int32_t diag = dc - 17 + (int32_t)(lane <= 34 ? lane : 34);
-    int32_t b[16];
+    const int32_t cell = (dc - 31 + (int32_t)(lane < 63 ? lane : 62)) & (W - 1);
+    int32_t V[TBR];
 #pragma unroll
-    for (int i = 0; i < 16; i++) b[i] = rdir[kh - 1 - i < 0 ? 0 : kh - 1 - i];
-    int32_t V[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < TBR; i++) {
       const int32_t kk = kh - 1 - i < 0 ? 0 : kh - 1 - i;   // row k-1 for k = kh - i
-      int32_t cell = diag - b[i];
-      cell = cell < 0 ? 0 : cell >= W ? W - 1 : cell;       // the walk reads in-band cells
       if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
       else               V[i] = rows[(size_t)kk * W + cell];
     }
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < TBR; i++) {
       if (kh - i < 1) break;
-      const int32_t x = 17 + d - dc;
+      const int32_t x = 31 + d - dc;
       const int32_t pm = __builtin_amdgcn_readlane(V[i], x - 1);
       const int32_t p0 = __builtin_amdgcn_readlane(V[i], x);
       const int32_t pp = __builtin_amdgcn_readlane(V[i], x + 1);
@@ -591,14 +586,14 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #endif
 
   // Row log for the traceback: row e (after pruning, -2 outside [nl, nr]) is a fixed
-  // 64*J-cell stripe at e * 64J, cell = d - B_e; rowdir[e] = B_e.  Row 0 is logged here.
+  // 64*J-cell stripe at e * 64J, cell = d mod 64J (the window holds 64J consecutive
+  // diagonals, so the index is unique and needs no per-row base).  Row 0 is logged here.
   typedef typename std::conditional<L16, int16_t, int32_t>::type cell_t;
   cell_t *clog = (cell_t *)rows;
-  clog[lane] = (cell_t)R[0];
-  if (lane == 0) rowdir[0] = B;
+  clog[(B + (int32_t)lane) & (64 * J - 1)] = (cell_t)R[0];
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
-  constexpr int JU = 2;
+  constexpr int JU = 1;
 
   for (int32_t e = 1; e <= limit; e++) {
     PROF_T(pt_row);
@@ -651,7 +646,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     }
     const int32_t jr = (right - B) >> 6;
     const uint32_t span = (uint32_t)(right - left);
-    if (lane == 0) rowdir[e] = B;
 
     // ---- A: neighbours from row e-1 for every chunk (DPP, no LDS) --------------------
     int32_t NR[J], LM[J];
@@ -825,7 +819,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     int32_t mx = NEG;
     const uint32_t kspan = (uint32_t)(nr - nl);
     const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
-    cell_t *crow = clog + (size_t)e * (64 * J) + lane;
+    cell_t *crow = clog + (size_t)e * (64 * J);
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jrs) break;
@@ -833,7 +827,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
       R[j] = v;
       mx = v > mx ? v : mx;
-      crow[64 * j] = (cell_t)v;
+      crow[(d & (64 * J - 1))] = (cell_t)v;
     }
     const int32_t M = wave_max(mx);
     if (M > longest) {
