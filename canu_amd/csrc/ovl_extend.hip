@@ -669,46 +669,32 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       }
     }
 
-    // ---- B: first 32-base slide step, per group of 4 chunks all strand loads first ----
+    // ---- B: first 32-base slide step of every lane, branch-free (the kernel is VALU
+    // bound: no batching copies, one chunk at a time) ------------------------------------
     uint64_t need[J];
 #pragma unroll
-    for (int g = 0; g < J; g += 4) {
-      if (g >= JU && g > jr) break;
-      uint64_t wa0[4], wa1[4], wt0[4], wt1[4];
-      uint32_t sha[4], sht[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int j = g + q;
-        if (j < JU || j <= jr) {
-          const int32_t d = B + 64 * j + (int32_t)lane;
-          const int32_t r = NR[j];
-          const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
-          const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
-          const int32_t ia = pa >> 5, it = pt >> 5;
-          sha[q] = (uint32_t)pa & 31u;
-          sht[q] = (uint32_t)pt & 31u;
-          wa0[q] = A.w[ia]; wa1[q] = A.w[ia + 1];
-          wt0[q] = T.w[it]; wt1[q] = T.w[it + 1];
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int j = g + q;
-        if (j >= JU && j > jr) break;
-        const int32_t lim = LM[j];
-        const uint32_t xa0 = __builtin_amdgcn_alignbit((uint32_t)wa1[q], (uint32_t)wa0[q], sha[q]);
-        const uint32_t xa1 = __builtin_amdgcn_alignbit((uint32_t)(wa1[q] >> 32),
-                                                       (uint32_t)(wa0[q] >> 32), sha[q]);
-        const uint32_t xt0 = __builtin_amdgcn_alignbit((uint32_t)wt1[q], (uint32_t)wt0[q], sht[q]);
-        const uint32_t xt1 = __builtin_amdgcn_alignbit((uint32_t)(wt1[q] >> 32),
-                                                       (uint32_t)(wt0[q] >> 32), sht[q]);
-        const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
-        const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
-        // k = min(run, lim) when lim > 0, else 0  (run >= 0)
-        const int32_t k = run < lim ? run : lim;
-        NR[j] += k > 0 ? k : 0;
-        need[j] = __ballot((run == 32) & (lim > 32));
-      }
+    for (int j = 0; j < J; j++) {
+      if (j >= JU && j > jr) break;
+      const int32_t d = B + 64 * j + (int32_t)lane;
+      const int32_t r = NR[j], lim = LM[j];
+      const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
+      const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
+      const int32_t ia = pa >> 5, it = pt >> 5;
+      const uint64_t wa0 = A.w[ia], wa1 = A.w[ia + 1];
+      const uint64_t wt0 = T.w[it], wt1 = T.w[it + 1];
+      // v_alignbit_b32 uses the low 5 bits of the shift
+      const uint32_t xa0 = __builtin_amdgcn_alignbit((uint32_t)wa1, (uint32_t)wa0, (uint32_t)pa);
+      const uint32_t xa1 = __builtin_amdgcn_alignbit((uint32_t)(wa1 >> 32), (uint32_t)(wa0 >> 32),
+                                                     (uint32_t)pa);
+      const uint32_t xt0 = __builtin_amdgcn_alignbit((uint32_t)wt1, (uint32_t)wt0, (uint32_t)pt);
+      const uint32_t xt1 = __builtin_amdgcn_alignbit((uint32_t)(wt1 >> 32), (uint32_t)(wt0 >> 32),
+                                                     (uint32_t)pt);
+      const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
+      const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
+      // k = min(run, lim) when lim > 0, else 0  (run >= 0)
+      const int32_t k = run < lim ? run : lim;
+      NR[j] = r + (k > 0 ? k : 0);
+      need[j] = __ballot((mm == 0u) & (lim > 32));
     }
 #ifdef OVL_PROFILE
     pc_nch += (jr + 1 > JU ? jr + 1 : JU);
