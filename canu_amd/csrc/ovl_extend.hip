@@ -120,6 +120,17 @@ __device__ __forceinline__ int32_t ped_slide(const SS &A, int32_t a0, int32_t m,
   return slide_bwd(A, a0 - r, T, t0 - r - d, lim);
 }
 
+// Inclusive prefix sum over the 64 lanes (DPP row shifts, then row broadcasts).
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
 // Max over the 64 lanes: DPP row shifts within 16-lane rows, then row broadcasts.
 __device__ __forceinline__ int32_t wave_max(int32_t v) {
   const int32_t NEG = (int32_t)0x80000000;
@@ -1232,21 +1243,65 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     }
     if (consistent) break;
     // drop the longest match and every match on this alignment (:517-531)
-    const int32_t *ldp = LD;
-    if (ld_len <= WM.ldcap) {
-      for (int32_t i = lane; i < ld_len; i += 64) WM.ldc[i] = LD[i];
-      lds_sync();
-      ldp = (const int32_t *)WM.ldc;
-    }
     int32_t removed = 0;
-    for (int32_t i = lane; i < nn; i += 64) {
-      Node nd = nodes[i];
-      if (nd.Len < 0) continue;
-      bool rm = (i == bi) ||
-                ((kind == K_DOVETAIL || X.partial) && S_Lo - SHIFT_SLACK <= nd.Start &&
-                 nd.Start + nd.Len <= (S_Hi + 1) + SHIFT_SLACK - 1 &&
-                 lies_on_alignment(nd.Start, nd.Offset, S_Lo, T_Lo, ldp, ld_len));
-      if (rm) { nodes[i].Len = ~nd.Len; removed++; }
+    const bool on_aln = (kind == K_DOVETAIL || X.partial);
+    if (on_aln && 2 * ld_len + 2 <= WM.ldcap) {
+      // Lies_On_Alignment (:307) by binary search: walking the deltas, delta i is reached
+      // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
+      // and compares with diag_i (or with the final diag).  thr is non-decreasing.
+      lds_i32 *thr = WM.ldc, *dgl = WM.ldc + ld_len + 1;
+      int32_t cs = S_Lo, cd = T_Lo - S_Lo;
+      for (int32_t i0 = 0; i0 < ld_len; i0 += 64) {
+        const int32_t i = i0 + (int32_t)lane;
+        const bool in = i < ld_len;
+        const int32_t v = in ? LD[i] : 0;
+        const int32_t a = v < 0 ? -v : v;
+        const int32_t inc_s = in ? a + (v >= 0 ? 1 : 0) : 0;
+        const int32_t inc_d = in ? (v < 0 ? 1 : -1) : 0;
+        const int32_t ss = wave_incl_scan(inc_s), sd = wave_incl_scan(inc_d);
+        if (in) {
+          thr[i] = cs + (ss - inc_s) + a;
+          dgl[i] = cd + (sd - inc_d);
+        }
+        cs += __builtin_amdgcn_readlane(ss, 63);
+        cd += __builtin_amdgcn_readlane(sd, 63);
+      }
+      if (lane == 0) { thr[ld_len] = 0x7fffffff; dgl[ld_len] = cd; }
+      lds_sync();
+      for (int32_t i = lane; i < nn; i += 64) {
+        Node nd = nodes[i];
+        if (nd.Len < 0) continue;
+        bool rm = (i == bi);
+        if (!rm && S_Lo - SHIFT_SLACK <= nd.Start &&
+            nd.Start + nd.Len <= (S_Hi + 1) + SHIFT_SLACK - 1) {
+          int32_t lo = 0, hi = ld_len;               // first index with thr > start
+          while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if (thr[mid] > nd.Start) hi = mid;
+            else lo = mid + 1;
+          }
+          const int32_t dd = (nd.Offset - nd.Start) - dgl[lo];
+          rm = (dd < 0 ? -dd : dd) <= SHIFT_SLACK;
+        }
+        if (rm) { nodes[i].Len = ~nd.Len; removed++; }
+      }
+      lds_sync();
+    } else {
+      const int32_t *ldp = LD;
+      if (ld_len <= WM.ldcap) {
+        for (int32_t i = lane; i < ld_len; i += 64) WM.ldc[i] = LD[i];
+        lds_sync();
+        ldp = (const int32_t *)WM.ldc;
+      }
+      for (int32_t i = lane; i < nn; i += 64) {
+        Node nd = nodes[i];
+        if (nd.Len < 0) continue;
+        bool rm = (i == bi) ||
+                  (on_aln && S_Lo - SHIFT_SLACK <= nd.Start &&
+                   nd.Start + nd.Len <= (S_Hi + 1) + SHIFT_SLACK - 1 &&
+                   lies_on_alignment(nd.Start, nd.Offset, S_Lo, T_Lo, ldp, ld_len));
+        if (rm) { nodes[i].Len = ~nd.Len; removed++; }
+      }
     }
     for (int s = 32; s > 0; s >>= 1) removed += __shfl_xor(removed, s);
     remaining -= removed;
