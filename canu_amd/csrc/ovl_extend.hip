@@ -660,6 +660,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 
     // ---- A: neighbours from row e-1 for every chunk (DPP, no LDS) --------------------
     int32_t NR[J], LM[J];
+    uint64_t actm[J];
     {
       int32_t carry = -2;                      // row e-1 at diagonal B+64j-1
 #pragma unroll
@@ -674,6 +675,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         const int32_t r0 = 1 + p0, r2 = 1 + pp;
         const int32_t r = (pm > r0 ? pm : r0) > r2 ? (pm > r0 ? pm : r0) : r2;
         const bool act = (uint32_t)(d - left) <= span;
+        actm[j] = __builtin_amdgcn_ballot_w64(act);
         const int32_t l1 = m - r, l2 = n - r - d;
         NR[j] = r;
         LM[j] = act ? (l1 < l2 ? l1 : l2) : 0;
@@ -705,7 +707,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       // k = min(run, lim) when lim > 0, else 0  (run >= 0)
       const int32_t k = run < lim ? run : lim;
       NR[j] = r + (k > 0 ? k : 0);
-      need[j] = __ballot((mm == 0u) & (lim > 32));
+      need[j] = __builtin_amdgcn_ballot_w64((mm == 0u) & (lim > 32));
     }
 #ifdef OVL_PROFILE
     pc_nch += (jr + 1 > JU ? jr + 1 : JU);
@@ -740,10 +742,9 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
-      const bool act = (uint32_t)(d - left) <= span;
       const int32_t r = NR[j];
-      em[j] = __ballot(act & ((r == m) | (r + d == n)));
-      km[j] = __ballot(act & (r + (d > 0 ? d : 0) >= ML));
+      em[j] = __builtin_amdgcn_ballot_w64((r == m) | (r + d == n)) & actm[j];
+      km[j] = __builtin_amdgcn_ballot_w64(r + (d > 0 ? d : 0) >= ML) & actm[j];
       endany |= em[j];
     }
     bool ended = false;
@@ -832,7 +833,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #pragma unroll
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
-        const uint64_t b = __ballot(R[j] == M);
+        const uint64_t b = __builtin_amdgcn_ballot_w64(R[j] == M);
         if (b) { bd = B + 64 * j + (int32_t)__builtin_ctzll(b); break; }
       }
       longest = M; best_d = bd; best_e = e;
