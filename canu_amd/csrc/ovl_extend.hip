@@ -1401,7 +1401,7 @@ static_assert(OVL_SCR >= TB_ROWS * TB_W && OVL_SCR >= 64 * OVL_RJ, "scratch too 
 // STAGE = false: the generic kernel (global strands with exception masks, rows in LDS).
 // L16: every read < 16384 bases, so the traceback code log holds 16-bit cells
 template <bool STAGE, bool L16>
-__global__ void __launch_bounds__(256, 4) k_extend(ExtendArgs X) {
+__global__ void __launch_bounds__(256, 5) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
