@@ -629,9 +629,9 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     return fail(OVL_ERR_UNSUPPORTED, "error limit %d needs more LDS than a CU has", e_cap);
   int32_t sw_words = (int32_t)((((uint64_t)c->max_len + 31) / 32 + 2) & ~1ull);
   size_t stg_lds_wave = 4ull * (4ull * sw_words + OVL_SCR);
-  const uint32_t stg_wpb = 4;
+  const uint32_t stg_wpb = 8;                  // 512-thread blocks: one ML table per 8 waves
   bool staged = stg_lds_wave * stg_wpb + ml_lds <= 64 * 1024;
-  ext_waves = (ext_waves / 4) * 4;
+  ext_waves = (ext_waves / 8) * 8;
   uint32_t chain_waves = 16u * c->n_cu;
   const uint32_t DONE_CAP = 4096;
   if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");

@@ -1246,11 +1246,15 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     // drop the longest match and every match on this alignment (:517-531)
     int32_t removed = 0;
     const bool on_aln = (kind == K_DOVETAIL || X.partial);
-    if (on_aln && 2 * ld_len + 2 <= WM.ldcap) {
+    // thresholds and diagonals as int16 when every read is < 16384 (L16), else int32
+    typedef typename std::conditional<L16, __attribute__((address_space(3))) int16_t,
+                                      lds_i32>::type lds_t;
+    constexpr int32_t per = L16 ? 1 : 2;               // ints per (thr, diag) pair
+    if (on_aln && per * (ld_len + 1) <= WM.ldcap) {
       // Lies_On_Alignment (:307) by binary search: walking the deltas, delta i is reached
       // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
       // and compares with diag_i (or with the final diag).  thr is non-decreasing.
-      lds_i32 *thr = WM.ldc, *dgl = WM.ldc + ld_len + 1;
+      lds_t *thr = (lds_t *)WM.ldc, *dgl = thr + ld_len + 1;
       int32_t cs = S_Lo, cd = T_Lo - S_Lo;
       for (int32_t i0 = 0; i0 < ld_len; i0 += 64) {
         const int32_t i = i0 + (int32_t)lane;
@@ -1267,7 +1271,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
         cs += __builtin_amdgcn_readlane(ss, 63);
         cd += __builtin_amdgcn_readlane(sd, 63);
       }
-      if (lane == 0) { thr[ld_len] = 0x7fffffff; dgl[ld_len] = cd; }
+      if (lane == 0) { thr[ld_len] = L16 ? 32767 : 0x7fffffff; dgl[ld_len] = cd; }
       lds_sync();
       for (int32_t i = lane; i < nn; i += 64) {
         Node nd = nodes[i];
@@ -1278,10 +1282,10 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
           int32_t lo = 0, hi = ld_len;               // first index with thr > start
           while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
-            if (thr[mid] > nd.Start) hi = mid;
+            if ((int32_t)thr[mid] > nd.Start) hi = mid;
             else lo = mid + 1;
           }
-          const int32_t dd = (nd.Offset - nd.Start) - dgl[lo];
+          const int32_t dd = (nd.Offset - nd.Start) - (int32_t)dgl[lo];
           rm = (dd < 0 ? -dd : dd) <= SHIFT_SLACK;
         }
         if (rm) { nodes[i].Len = ~nd.Len; removed++; }
@@ -1392,16 +1396,15 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
   return L;
 }
 
-#define OVL_SCR 560              // staged kernel: per-wave LDS scratch ints (traceback window,
-                                 // window re-centring, Left_Delta cache), >= TB_ROWS * TB_W
-static_assert(OVL_SCR >= TB_ROWS * TB_W && OVL_SCR >= 64 * OVL_RJ, "scratch too small");
+#define OVL_SCR 256              // staged kernel: per-wave LDS scratch ints (Lies_On_Alignment
+                                 // thresholds, Left_Delta cache)
 
 // STAGE = true: exception-free pairs, strands staged in LDS, rows in registers; pairs with
 // 'n' bases or a band wider than the register window are deferred to the generic kernel.
 // STAGE = false: the generic kernel (global strands with exception masks, rows in LDS).
 // L16: every read < 16384 bases, so the traceback code log holds 16-bit cells
 template <bool STAGE, bool L16>
-__global__ void __launch_bounds__(256, 5) k_extend(ExtendArgs X) {
+__global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
