@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
 
 // ---------------------------------------------------------------------------------------
 
-#define OVL_HCAP   1024          // staged occurrences per wave
+#define OVL_HCAP   512           // staged occurrences per wave
 #define OVL_MAXT   128           // targets per pass (2 per lane)
 #define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
 
@@ -327,6 +327,10 @@ __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32
 
 __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
   __shared__ uint64_t s_hb[4][OVL_HCAP];
+  __shared__ uint8_t  s_hw[4][OVL_HCAP];      // window (0..63) of each staged occurrence
+  __shared__ uint8_t  s_hs[4][OVL_HCAP];      // its target slot (0..127), 0xFF: none
+  __shared__ uint16_t s_sx[4][OVL_HCAP];      // staged indices sorted by (slot, order)
+  __shared__ uint32_t s_cnt[4][2 * OVL_MAXT]; // per slot: base, running count
   __shared__ uint32_t s_seg[4][65];
   __shared__ uint32_t s_off[4][64];
   __shared__ uint32_t s_tgt[4][OVL_MAXT];
@@ -334,6 +338,10 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
   __shared__ uint32_t s_over[4];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t *hb = s_hb[wave];
+  uint8_t *hw = s_hw[wave];
+  uint8_t *hs = s_hs[wave];
+  uint16_t *sx = s_sx[wave];
+  uint32_t *cnt = s_cnt[wave];
   uint32_t *seg = s_seg[wave];
   uint32_t *soff = s_off[wave];
   uint32_t *tgt = s_tgt[wave];
@@ -393,42 +401,104 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
               if (seg[mid] <= idx) lo = mid; else hi = mid;
             }
             hb[idx - p0] = A.occ[soff[lo] + (idx - seg[lo])];
+            hw[idx - p0] = (uint8_t)lo;
           }
+          for (uint32_t i = lane; i < 2 * OVL_MAXT; i += 64) cnt[i] = 0;
           WAVE_SYNC();
-          // discover targets (LDS open-addressing set, 128 slots)
+          // discover targets (LDS open-addressing set, 128 slots); remember each staged
+          // occurrence's slot and count occurrences per slot
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
             uint32_t t = (uint32_t)(hb[idx - p0] >> 32);
-            if (t <= a_iid) continue;            // Find_Overlaps.C:328
-            if (pass == 0) nhits++;
-            bool skip = false;
-            for (uint32_t q = 0; q < ndone; q++)
-              if (done_list[q] == t) { skip = true; break; }
-            if (skip) continue;
-            uint32_t h = thash(t);
-            bool placed = false;
-            for (uint32_t probe = 0; probe < OVL_MAXT; probe++) {
-              uint32_t cur = tgt[h];
-              if (cur == t) { placed = true; break; }
-              if (cur == 0) {
-                uint32_t old = atomicCAS(&tgt[h], 0u, t);
-                if (old == 0 || old == t) { placed = true; break; }
+            uint8_t slot = 0xFF;
+            if (t > a_iid) {                     // Find_Overlaps.C:328
+              if (pass == 0) nhits++;
+              bool skip = false;
+              for (uint32_t q = 0; q < ndone; q++)
+                if (done_list[q] == t) { skip = true; break; }
+              if (!skip) {
+                uint32_t h = thash(t);
+                bool placed = false;
+                for (uint32_t probe = 0; probe < OVL_MAXT; probe++) {
+                  uint32_t cur = tgt[h];
+                  if (cur == t) { placed = true; break; }
+                  if (cur == 0) {
+                    uint32_t old = atomicCAS(&tgt[h], 0u, t);
+                    if (old == 0 || old == t) { placed = true; break; }
+                  }
+                  h = (h + 1) & (OVL_MAXT - 1);
+                }
+                if (placed) { slot = (uint8_t)h; atomicAdd(&cnt[h], 1u); }
+                else atomicOr(&s_over[wave], 1u);
               }
-              h = (h + 1) & (OVL_MAXT - 1);
             }
-            if (!placed) atomicOr(&s_over[wave], 1u);
+            hs[idx - p0] = slot;
+          }
+          WAVE_SYNC();
+          // slot bases: exclusive scan over the 128 counts (two per lane)
+          {
+            uint32_t c0 = cnt[2 * lane], c1 = cnt[2 * lane + 1];
+            uint32_t incl = c0 + c1;
+            for (int d = 1; d < 64; d <<= 1) {
+              uint32_t v = __shfl_up(incl, d);
+              if ((int)lane >= d) incl += v;
+            }
+            uint32_t ex = incl - c0 - c1;
+            WAVE_SYNC();
+            cnt[2 * lane] = ex;                    // base of slot 2*lane
+            cnt[2 * lane + 1] = ex + c0;           // base of slot 2*lane+1
+            cnt[OVL_MAXT + 2 * lane] = 0;          // running counts
+            cnt[OVL_MAXT + 2 * lane + 1] = 0;
+          }
+          WAVE_SYNC();
+          // stable scatter: within each 64-entry step, rank the lanes of each slot in
+          // lane order (one ballot per distinct slot), so every slot's list keeps the
+          // staged (window, chain) order
+          for (uint32_t b0 = p0; b0 < p1; b0 += 64) {
+            uint32_t idx = b0 + lane;
+            uint32_t slot = (idx < p1) ? hs[idx - p0] : 0xFFu;
+            uint64_t todo = __ballot(slot != 0xFFu);
+            while (todo) {
+              uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+              uint32_t sl = __builtin_amdgcn_readlane(slot, leader);
+              uint64_t grp = __ballot(slot == sl) & todo;
+              uint32_t run = cnt[OVL_MAXT + sl];
+              if ((grp >> lane) & 1ull) {
+                uint32_t rank = __builtin_popcountll(grp & ((1ull << lane) - 1));
+                sx[cnt[sl] + run + rank] = (uint16_t)(idx - p0);
+              }
+              WAVE_SYNC();
+              if (lane == leader) cnt[OVL_MAXT + sl] = run + __builtin_popcountll(grp);
+              WAVE_SYNC();
+              todo &= ~grp;
+            }
           }
           WAVE_SYNC();
           uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
           if (t0 != s0.t) { slot_reset(s0); s0.t = t0; }
           if (t1 != s1.t) { slot_reset(s1); s1.t = t1; }
-          // replay Add_Match per target, windows in order
-          for (uint32_t j = 0; j < 64; j++) {
-            uint32_t sj = seg[j], ej = seg[j + 1];
-            if (ej <= p0 || sj >= p1 || ej == sj) continue;
-            uint32_t lo0 = (sj > p0 ? sj : p0) - p0, hi0 = (ej < p1 ? ej : p1) - p0;
-            int32_t o_j = (int32_t)(base + j);
-            replay_window(s0, hb, lo0, hi0, o_j, k, W, A, lane);
-            replay_window(s1, hb, lo0, hi0, o_j, k, W, A, lane);
+          // replay Add_Ref / Add_Match per target over its own occurrences, in order
+          {
+            uint32_t b = cnt[lane], n = cnt[OVL_MAXT + lane];
+            for (uint32_t i = 0; i < n; i++) {
+              uint32_t x = sx[b + i];
+              int32_t pp = (int32_t)(uint32_t)hb[x];
+              int32_t o_j = (int32_t)(base + hw[x]);
+              s0.diag_ct++;                                   // Add_Ref (:203-206)
+              if (s0.diag_bgn > o_j) s0.diag_bgn = o_j;
+              if (s0.diag_end < o_j) s0.diag_end = o_j;
+              add_match(s0, pp, o_j, k, A.pool, W, A, lane);
+            }
+            b = cnt[lane + 64];
+            n = cnt[OVL_MAXT + lane + 64];
+            for (uint32_t i = 0; i < n; i++) {
+              uint32_t x = sx[b + i];
+              int32_t pp = (int32_t)(uint32_t)hb[x];
+              int32_t o_j = (int32_t)(base + hw[x]);
+              s1.diag_ct++;
+              if (s1.diag_bgn > o_j) s1.diag_bgn = o_j;
+              if (s1.diag_end < o_j) s1.diag_end = o_j;
+              add_match(s1, pp, o_j, k, A.pool, W, A, lane);
+            }
           }
           WAVE_SYNC();
         }
