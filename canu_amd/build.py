@@ -9,7 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "lib")
 OUT = os.path.join(OUT_DIR, "libcanu_ovl.so")
-SOURCES = ["ovl_api.hip", "ovl_index.hip", "ovl_seed.hip", "ovl_extend.hip", "ovl_common.h"]
+SOURCES = ["ovl_api.hip", "ovl_index.hip", "ovl_seed.hip", "ovl_extend.hip", "ovl_common.h",
+           "ovl_ovb.h"]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                # doubles in the extension (branch score, slope, quality) must round exactly

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -22,6 +23,7 @@
 #include "ovl_index.hip"
 #include "ovl_seed.hip"
 #include "ovl_extend.hip"
+#include "ovl_ovb.h"
 
 using namespace ovl;
 
@@ -631,6 +633,13 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   size_t stg_lds_wave = 4ull * (4ull * sw_words + OVL_SCR);
   const uint32_t stg_wpb = 8;                  // 512-thread blocks: one ML table per 8 waves
   bool staged = stg_lds_wave * stg_wpb + ml_lds <= 64 * 1024;
+  // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the staged kernel's LDS so that at most that
+  // many 512-thread blocks fit on a CU (occupancy studies); unset = natural occupancy
+  size_t stg_lds = stg_lds_wave * stg_wpb + ml_lds;
+  if (const char *bp = getenv("OVL_EXT_BLOCKS_PER_CU")) {
+    int nb = atoi(bp);
+    if (nb > 0) stg_lds = std::max<size_t>(stg_lds, (160 * 1024) / nb - 256);
+  }
   ext_waves = (ext_waves / 8) * 8;
   uint32_t chain_waves = 16u * c->n_cu;
   const uint32_t DONE_CAP = 4096;
@@ -641,6 +650,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
   uint64_t npairs_tot = 0, probe_bytes = 0;
+  uint32_t n_probe_launch = 0, n_ext_launch = 0;
   uint32_t nu = (uint32_t)units.size();
   uint32_t u0 = 0;
   while (u0 < nu) {
@@ -670,6 +680,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     PA.k = k;
     HIPC(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(k_probe, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
+    n_probe_launch++;
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev[3], s));
     std::vector<uint32_t> uh(nb);
@@ -799,12 +810,13 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
         if (d_defer.alloc(npairs)) return fail(OVL_ERR_OOM, "defer list");
         EA.defer = d_defer.p;
         // 16-bit traceback cells hold (r << 2 | code) when every r < 2^14
+        n_ext_launch++;
         if (c->max_len < 16384)
           hipLaunchKernelGGL((k_extend<true, true>), dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
-                             stg_lds_wave * stg_wpb + ml_lds, s, EA);
+                             stg_lds, s, EA);
         else
           hipLaunchKernelGGL((k_extend<true, false>), dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
-                             stg_lds_wave * stg_wpb + ml_lds, s, EA);
+                             stg_lds, s, EA);
         HIPC(hipGetLastError());
         uint32_t nd = 0;
         HIPC(hipMemcpyAsync(&nd, d_ctr.p + 8, 4, hipMemcpyDeviceToHost, s));
@@ -814,10 +826,12 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
           EA.list = d_defer.p;
           EA.npairs = nd;
           EA.pair_next = d_ctr.p + 9;
+          n_ext_launch++;
           hipLaunchKernelGGL((k_extend<false, false>), dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
                              lds, s, EA);
         }
       } else {
+        n_ext_launch++;
         hipLaunchKernelGGL((k_extend<false, false>), dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
                            lds, s, EA);
       }
@@ -856,6 +870,8 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   c->stats.ms_extend = ms_ext;
   c->stats.ms_probe_kernel = ms_probe;
   c->stats.probe_bytes = probe_bytes;
+  c->stats.probe_launches = n_probe_launch;
+  c->stats.extend_launches = n_ext_launch;
   *n_out = c->nout;
   return OVL_OK;
 }
@@ -880,6 +896,29 @@ int ovl_fetch_overlaps(ovl_ctx *c, ovl_record *out, uint64_t max_records, uint64
     out[i].dat[1] = h[i].w1;
   }
   *n_copied = n;
+  return OVL_OK;
+}
+
+int ovl_write_ovb(const ovl_record *recs, uint64_t n, const char *path, int with_counts) {
+  if (!path || (n && !recs)) return fail(OVL_ERR_BAD_PARAM, "null argument");
+  if (write_ovb_file(recs, n, path, with_counts != 0))
+    return fail(OVL_ERR_BAD_INPUT, "writing '%s': %s", path, strerror(errno));
+  return OVL_OK;
+}
+
+int ovl_ctx_write_ovb(ovl_ctx *c, const char *path) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  std::vector<ovl_record> h(c->nout);
+  uint64_t got = 0;
+  int rc = ovl_fetch_overlaps(c, h.data(), h.size(), &got);
+  if (rc) return rc;
+  return ovl_write_ovb(h.data(), got, path, 1);
+}
+
+int ovl_ctx_write_stats(ovl_ctx *c, const char *path) {
+  if (!c || !path) return fail(OVL_ERR_STATE, "null argument");
+  if (write_stats_file(c->stats, path))
+    return fail(OVL_ERR_BAD_INPUT, "writing '%s': %s", path, strerror(errno));
   return OVL_OK;
 }
 

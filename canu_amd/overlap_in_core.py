@@ -52,14 +52,16 @@ class _Stats(ctypes.Structure):
         "total_overlaps", "contained_overlaps", "dovetail_overlaps", "seed_hits", "pairs")] + \
         [("ms_index", ctypes.c_double), ("ms_seed", ctypes.c_double),
          ("ms_extend", ctypes.c_double), ("ms_probe_kernel", ctypes.c_double),
-         ("probe_bytes", ctypes.c_uint64)]
+         ("probe_bytes", ctypes.c_uint64), ("probe_launches", ctypes.c_uint32),
+         ("extend_launches", ctypes.c_uint32)]
 
 
 # Every symbol include/canu_ovl.h declares (tests check the library exports them all).
 EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_destroy",
            "ovl_last_error", "ovl_abi_version", "ovl_load_reads", "ovl_load_reads_device",
            "ovl_set_skip_kmers", "ovl_build_hash_index", "ovl_find_overlaps",
-           "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream"]
+           "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream", "ovl_write_ovb",
+           "ovl_ctx_write_ovb", "ovl_ctx_write_stats"]
 
 _lib = None
 
@@ -93,6 +95,9 @@ def load_library(path: str | None = None):
     lib.ovl_get_stats.argtypes = [ctypes.c_void_p, P(_Stats)]
     lib.ovl_ctx_stream.argtypes = [ctypes.c_void_p]
     lib.ovl_ctx_stream.restype = ctypes.c_void_p
+    lib.ovl_write_ovb.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
+    lib.ovl_ctx_write_ovb.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.ovl_ctx_write_stats.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     _lib = lib
     return lib
 
@@ -298,6 +303,14 @@ class OverlapInCore:
     def stream(self) -> int:
         return self.lib.ovl_ctx_stream(self.ctx)
 
+    def write_ovb(self, path: str) -> None:
+        """overlapInCore's -o output: the last find's records as an .ovb + .counts."""
+        self._check(self.lib.ovl_ctx_write_ovb(self.ctx, path.encode()))
+
+    def write_stats(self, path: str) -> None:
+        """overlapInCore's -s statistics file."""
+        self._check(self.lib.ovl_ctx_write_stats(self.ctx, path.encode()))
+
     def run(self, rs, skip_kmers=None) -> np.ndarray:
         """OverlapDriver() for one hash batch: load, index, search, fetch (sorted)."""
         self.load_reads(rs)
@@ -306,3 +319,14 @@ class OverlapInCore:
         self.build_hash_index()
         n = self.find_overlaps()
         return self.fetch(n)
+
+
+def write_ovb(records: np.ndarray, path: str, counts: bool = True) -> None:
+    """Write ovOverlap records (RECORD_DTYPE, in the given order) as an ovFileFullWrite
+    .ovb (src/stores/ovStoreFile.C:198) plus its .counts file (ovStoreHistogram.C:322)."""
+    lib = load_library()
+    rec = np.ascontiguousarray(records, dtype=RECORD_DTYPE)
+    rc = lib.ovl_write_ovb(rec.ctypes.data if rec.size else None, rec.shape[0],
+                           path.encode(), 1 if counts else 0)
+    if rc != 0:
+        raise OvlError(rc, lib.ovl_last_error().decode())

@@ -146,9 +146,27 @@ typedef struct {
   double   ms_extend;              /* device time of extension + output                */
   double   ms_probe_kernel;        /* device time of the hash-probe kernel alone       */
   uint64_t probe_bytes;            /* algorithmic bytes of the hash-probe kernel       */
+  uint32_t probe_launches;         /* k_probe launches of the last find                */
+  uint32_t extend_launches;        /* k_extend launches (staged + generic)             */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);
+
+/* overlapInCore's output files (host code, no device needed):
+ *   ovl_write_ovb      records, in the given order, as the .ovb that
+ *                      ovFile(gkp, name, ovFileFullWrite) writes (src/stores/ovStoreFile.C:198:
+ *                      a_iid, b_iid, dat words as hi32/lo32, in 43,680-record blocks, each
+ *                      framed as size_t length + a snappy stream the reference reader
+ *                      decodes -- literal-only, see canu_amd/csrc/ovl_ovb.h) and,
+ *                      when with_counts, the "<base>.counts" overlaps-per-read file the
+ *                      ovFile destructor saves (src/stores/ovStoreHistogram.C:226/:322)
+ *   ovl_ctx_write_ovb  the last find's records (ovl_fetch_overlaps order) + .counts, i.e.
+ *                      overlapInCore's -o output (overlapInCore.C:197)
+ *   ovl_ctx_write_stats  the -s statistics text (overlapInCore.C:580-588) */
+int         ovl_write_ovb(const ovl_record *recs, uint64_t n, const char *path,
+                          int with_counts);
+int         ovl_ctx_write_ovb(ovl_ctx *ctx, const char *path);
+int         ovl_ctx_write_stats(ovl_ctx *ctx, const char *path);
 
 /* HIP stream the context runs on (as void*, a hipStream_t), for callers that time or
  * order work around it. */

@@ -135,6 +135,19 @@ def reference_available() -> bool:
     return os.path.exists(REF_BIN)
 
 
+def read_ovb_reference(path: str) -> np.ndarray:
+    """Records of an .ovb in FILE order, read by the reference's own ovFile reader
+    (oic_ref --read-ovb, ref_harness.cpp)."""
+    if not reference_available():
+        raise FileNotFoundError(REF_BIN)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as wd:
+        out = os.path.join(wd, "rec.bin")
+        cp = subprocess.run([REF_BIN, "--read-ovb", path, out], capture_output=True, text=True)
+        if cp.returncode != 0:
+            raise RuntimeError(f"oic_ref --read-ovb failed: {cp.stderr[-2000:]}")
+        return np.fromfile(out, dtype=RECORD_DTYPE)
+
+
 def params_to_ref_args(params: dict) -> list[str]:
     a = ["-k", str(params["kmer_len"]), "--maxerate", repr(params["max_erate"]),
          "--minlength", str(params["min_olap_len"])]

@@ -23,6 +23,7 @@
  *   u32 len[nreads], then all bases back to back, then (if has_quals) all quals (0..60).
  *
  * usage: oic_ref <reads.bin> <workdir> <out.bin> [options]
+ *        oic_ref --read-ovb <in.ovb> <out.bin>
  *   -k N  --maxerate F  --minlength N  -G  -m|-u  -w  -z  -l N  --minkmers
  *   --hashbits N  --hashload F  --hashstrings N  --hashdatalen N  -t N
  *   -h a-b  -r a-b  --skip <kmers.fasta>  --time (print wall seconds of OverlapDriver)
@@ -49,7 +50,31 @@ static void die(const char *m) {
   exit(1);
 }
 
+//  oic_ref --read-ovb <in.ovb> <out.bin>: read any .ovb with the reference's
+//  ovFile(NULL, name, ovFileFull)::readOverlap (ovStoreFile.C) and dump its records in file
+//  order, 24 bytes each -- the checker for the library's own .ovb writer.
+static int read_ovb(const char *inPath, const char *outPath) {
+  ovFile   *in = new ovFile(NULL, inPath, ovFileFull);
+  ovOverlap ov(NULL);
+  FILE *O = fopen(outPath, "wb");
+  if (!O) die("can't open output");
+  uint64_t n = 0;
+  while (in->readOverlap(&ov)) {
+    uint32_t ids[2] = { ov.a_iid, ov.b_iid };
+    uint64_t w[2]   = { ov.dat.dat[0], ov.dat.dat[1] };
+    fwrite(ids, 4, 2, O);
+    fwrite(w, 8, 2, O);
+    n++;
+  }
+  fclose(O);
+  delete in;
+  fprintf(stdout, "RECORDS %lu\n", (unsigned long)n);
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc == 4 && strcmp(argv[1], "--read-ovb") == 0)
+    return read_ovb(argv[2], argv[3]);
   if (argc < 4)
     die("usage: oic_ref <reads.bin> <workdir> <out.bin> [options]");
 

@@ -77,3 +77,26 @@ def test_ont_shards_union_and_determinism(built, ont):
     assert np.all(span > 0) and np.all(((w0 >> 42) & 0xFFF) <= 4095)
     assert np.all(ahg5 + ahg3 < L[a]) and np.all(bhg5 + bhg3 < L[b])
     assert np.all(a != b)
+
+
+def test_gpu_output_files(built, tmp_path):
+    """overlapInCore's -o/-s outputs from the GPU job: the .ovb decodes (reference reader
+    where built, else the test decoder) to the reference's records, the .counts file is
+    byte-identical to the one the reference wrote, the stats text has the reference's lines."""
+    import os
+    from test_ovb import GOLDEN, read_ovb_py
+    rs, p, skip, want = load_golden("basic")
+    oic = OverlapInCore(_P(p), device=0)
+    oic.run(rs)
+    path = str(tmp_path / "001.ovb.WORKING")
+    oic.write_ovb(path)
+    oic.write_stats(str(tmp_path / "001.stats"))
+    st = oic.stats()
+    oic.close()
+    got = oracle.read_ovb_reference(path) if oracle.reference_available() else read_ovb_py(path)
+    assert np.array_equal(got, want)
+    assert open(str(tmp_path / "001.counts"), "rb").read() == \
+        open(os.path.join(GOLDEN, "basic_ref.counts"), "rb").read()
+    txt = open(str(tmp_path / "001.stats")).read().splitlines()
+    assert txt[3] == f" Total overlaps produced = {st['total_overlaps']}"
+    assert len(txt) == 8

@@ -32,17 +32,39 @@ def short(name):
     return None
 
 
-def counters(tag, what):
+def counters(tag, what, name=None):
     f = glob.glob(os.path.join(OUT, f"{tag}_{what}", "**", "*counter_collection.csv"),
                   recursive=True)
     tot, calls = defaultdict(float), defaultdict(set)
     for path in f:
         for row in csv.DictReader(open(path)):
             k = short(row["Kernel_Name"])
-            if k:
+            if k and (name is None or row["Counter_Name"] == name):
                 tot[k] += float(row["Counter_Value"])
                 calls[k].add(row["Dispatch_Id"])
     return tot, {k: len(v) for k, v in calls.items()}
+
+
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
+VALU_ISSUE_CYC = 2     # MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles
+
+
+def issue(tag):
+    """VALU issue fraction per kernel: SQ_INSTS_VALU x 2 cycles over the SIMD-cycles of its
+    dispatches (GRBM_GUI_ACTIVE is summed over the 8 XCDs: cycles = GUI_ACTIVE / 8)."""
+    valu, n = counters(tag, "issue", "SQ_INSTS_VALU")
+    salu, _ = counters(tag, "issue", "SQ_INSTS_SALU")
+    lds, _ = counters(tag, "issue", "SQ_INSTS_LDS")
+    gui, _ = counters(tag, "issue", "GRBM_GUI_ACTIVE")
+    out = {}
+    for k in valu:
+        cyc = gui.get(k, 0.0) / 8.0
+        if cyc <= 0:
+            continue
+        out[k] = {"valu_insts": valu[k], "salu_insts": salu.get(k, 0.0),
+                  "lds_insts": lds.get(k, 0.0), "gpu_cycles": cyc,
+                  "valu_issue_frac": round(valu[k] * VALU_ISSUE_CYC / (N_SIMD * cyc), 4)}
+    return out
 
 
 def main():
@@ -59,6 +81,7 @@ def main():
             k = short(row["Name"])
             if k:
                 avg_ns[k] = float(row["AverageNs"])
+    iss = issue(tag)
     traffic = {}
     with open(os.path.join(PROF, f"{tag}_traffic.csv"), "w") as f:
         f.write("kernel,launches,avg_ns,fetch_kib_per_launch,write_kib_per_launch,"
@@ -69,6 +92,8 @@ def main():
             b = (2.0 * fk + wk) * 1024.0
             traffic[k] = {"hbm_bytes_per_step": int(b * n), "launches_per_step": n,
                           "hbm_bytes_per_launch": int(b)}
+            if k in iss:
+                traffic[k]["issue"] = iss[k]
             f.write(f"{k},{n},{avg_ns.get(k, 0):.0f},{fk:.1f},{wk:.1f},{b:.0f}\n")
     with open(os.path.join(PROF, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
