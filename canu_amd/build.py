@@ -1,4 +1,5 @@
-"""Build libcanu_ovl.so for gfx950 in-tree (canu_amd/lib/) with hipcc."""
+"""Build libcanu_ovl.so (overlapInCore) and libcanu_mhap.so (MHAP stage) for gfx950 in-tree
+(canu_amd/lib/) with hipcc."""
 from __future__ import annotations
 
 import os
@@ -28,6 +29,22 @@ def needs_build() -> bool:
 
 
 PROF_OUT = os.path.join(OUT_DIR, "libcanu_ovl_prof.so")
+MHAP_OUT = os.path.join(OUT_DIR, "libcanu_mhap.so")
+MHAP_DEPS = [os.path.join(CSRC, "mhap.hip"), os.path.join(HERE, "..", "include", "canu_mhap.h")]
+
+
+def build_mhap(force: bool = False, verbose: bool = True) -> str:
+    if not force and os.path.exists(MHAP_OUT) and \
+            all(os.path.getmtime(d) <= os.path.getmtime(MHAP_OUT) for d in MHAP_DEPS):
+        return MHAP_OUT
+    os.makedirs(OUT_DIR, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", MHAP_OUT + ".tmp", os.path.join(CSRC, "mhap.hip")]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(MHAP_OUT + ".tmp", MHAP_OUT)
+    return MHAP_OUT
 
 
 def build(force: bool = False, verbose: bool = True, profile: bool = False) -> str:
@@ -49,3 +66,5 @@ def build(force: bool = False, verbose: bool = True, profile: bool = False) -> s
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, profile="--profile" in sys.argv)
+    if "--profile" not in sys.argv:
+        build_mhap(force="--force" in sys.argv)

@@ -1,0 +1,262 @@
+"""Host side of the MHAP stage: ctypes binding of libcanu_mhap.so (include/canu_mhap.h) and
+the MHAP command-line options canu passes (src/pipelines/canu/OverlapMhap.pm:374-498).
+
+There is no CPU fallback: every compute call goes to the gfx950 library, and loading it
+fails loudly when it was not built."""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcanu_mhap.so")
+
+# the C struct mhap_record
+MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("count", "<u4"),
+                       ("a_bgn", "<i4"), ("a_end", "<i4"), ("a_len", "<i4"), ("o", "<u4"),
+                       ("b_bgn", "<i4"), ("b_end", "<i4"), ("b_len", "<i4")], align=True)
+
+EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last_error",
+           "mhap_abi_version", "mhap_load_reads", "mhap_load_reads_device",
+           "mhap_set_filter_kmers", "mhap_sketch", "mhap_sketch_buffers", "mhap_build_index",
+           "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
+
+
+class MhapError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_uint32), ("num_hashes", ctypes.c_uint32),
+                ("min_matches", ctypes.c_uint32), ("ordered_sketch", ctypes.c_uint32),
+                ("ordered_k", ctypes.c_uint32), ("min_olap", ctypes.c_int32),
+                ("threshold", ctypes.c_double)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("sketched_reads", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
+                ("overlaps", ctypes.c_uint64), ("ms_sketch", ctypes.c_double),
+                ("ms_index", ctypes.c_double), ("ms_candidates", ctypes.c_double),
+                ("ms_compare", ctypes.c_double), ("sketch_kmers", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def load_library(path: str | None = None):
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("CANU_MHAP_LIB") or LIB_PATH
+    if not os.path.exists(path):
+        raise MhapError(-1, f"{path} missing: run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    P, V, U32, U64 = ctypes.POINTER, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    lib.mhap_params_init.argtypes = [P(_Params)]
+    lib.mhap_ctx_create.argtypes = [P(_Params), ctypes.c_int, P(V)]
+    lib.mhap_ctx_destroy.argtypes = [V]
+    lib.mhap_last_error.restype = ctypes.c_char_p
+    lib.mhap_load_reads.argtypes = [V, U32, U32, V, V, V]
+    lib.mhap_load_reads_device.argtypes = [V, U32, U32, V, V, V]
+    lib.mhap_set_filter_kmers.argtypes = [V, ctypes.c_char_p, U64]
+    lib.mhap_sketch.argtypes = [V, U32, U32]
+    lib.mhap_sketch_buffers.argtypes = [V, P(V), P(V), P(V)]
+    lib.mhap_build_index.argtypes = [V]
+    lib.mhap_compare.argtypes = [V, U32, U32, P(U64)]
+    lib.mhap_fetch.argtypes = [V, V, U64, P(U64)]
+    lib.mhap_write_text.argtypes = [V, ctypes.c_char_p, U32, U32, U32]
+    lib.mhap_get_stats.argtypes = [V, P(_Stats)]
+    _lib = lib
+    return lib
+
+
+@dataclasses.dataclass
+class MhapParameters:
+    """MHAP options canu sets (OverlapMhap.pm:109-150; Defaults.pm:698-706)."""
+    k: int = 16
+    num_hashes: int = 512
+    num_min_matches: int = 3
+    threshold: float = 0.78
+    ordered_sketch_size: int = 1536
+    ordered_kmer_size: int = 12
+    min_olap_length: int = 500
+
+    @classmethod
+    def sensitivity(cls, level: str, tag: str = "cor", nanopore: bool = False,
+                    ordered_mer: int | None = None, min_olap: int = 500) -> "MhapParameters":
+        """The presets of OverlapMhap.pm:109-150 ('low' / 'normal' / 'high', +0.05
+        threshold for nanopore-raw libraries, obt/utg hash count override)."""
+        om = ordered_mer if ordered_mer is not None else (12 if tag == "cor" else 18)
+        if level == "low":
+            p = cls(num_hashes=256, num_min_matches=3, threshold=0.80, ordered_sketch_size=1000,
+                    ordered_kmer_size=om + 2)
+        elif level == "normal":
+            p = cls(num_hashes=512, num_min_matches=3, threshold=0.78, ordered_sketch_size=1536,
+                    ordered_kmer_size=om)
+        elif level == "high":
+            p = cls(num_hashes=768, num_min_matches=2, threshold=0.73, ordered_sketch_size=1536,
+                    ordered_kmer_size=om)
+        else:
+            raise ValueError(f"invalid MhapSensitivity={level}")
+        if nanopore:
+            p.threshold += 0.05
+        if tag in ("obt", "utg"):
+            p.num_hashes, p.num_min_matches = 128, 5
+        p.min_olap_length = min_olap
+        return p
+
+    def to_c(self) -> _Params:
+        return _Params(self.k, self.num_hashes, self.num_min_matches, self.ordered_sketch_size,
+                       self.ordered_kmer_size, self.min_olap_length, self.threshold)
+
+    def as_oracle(self) -> dict:
+        return dict(k=self.k, num_hashes=self.num_hashes, min_matches=self.num_min_matches,
+                    threshold=self.threshold, ordered_sketch=self.ordered_sketch_size,
+                    ordered_k=self.ordered_kmer_size, min_olap=self.min_olap_length)
+
+
+def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
+    """The jar's options as canu writes them (OverlapMhap.pm:380-395, :480-495).  Options
+    that only steer the jar's own I/O (-p, -q, -s, --num-threads, ...) are returned in the
+    second dict; weighting options this build does not implement raise."""
+    p = MhapParameters()
+    io: dict = {}
+    i = 0
+    while i < len(argv):
+        a = argv[i]
+        val = argv[i + 1] if i + 1 < len(argv) else None
+        if a == "-k":
+            p.k = int(val); i += 1
+        elif a == "--num-hashes":
+            p.num_hashes = int(val); i += 1
+        elif a == "--num-min-matches":
+            p.num_min_matches = int(val); i += 1
+        elif a == "--threshold":
+            p.threshold = float(val); i += 1
+        elif a == "--ordered-sketch-size":
+            p.ordered_sketch_size = int(val); i += 1
+        elif a == "--ordered-kmer-size":
+            p.ordered_kmer_size = int(val); i += 1
+        elif a == "--min-olap-length":
+            p.min_olap_length = int(val); i += 1
+        elif a in ("-f", "-p", "-q", "-s", "--num-threads", "--filter-threshold",
+                   "--repeat-weight", "--repeat-idf-scale"):
+            io[a] = val; i += 1
+        elif a in ("--no-self",):
+            io[a] = True
+        elif a in ("--supress-noise", "--no-tf"):
+            raise MhapError(-3, f"{a}: tf-idf weighting options are not implemented")
+        else:
+            raise MhapError(-2, f"unknown MHAP option '{a}'")
+        i += 1
+    return p, io
+
+
+class Mhap:
+    """One MHAP job on one gfx950 device: load -> sketch -> index -> compare -> fetch."""
+
+    def __init__(self, params: MhapParameters, device: int = 0):
+        self.lib = load_library()
+        self.params = params
+        cp = params.to_c()
+        ctx = ctypes.c_void_p()
+        self._check(self.lib.mhap_ctx_create(ctypes.byref(cp), device, ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.first_iid, self.nreads = 1, 0
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise MhapError(rc, self.lib.mhap_last_error().decode())
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.mhap_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_reads(self, rs) -> None:
+        bases = np.ascontiguousarray(rs.bases, dtype=np.uint8)
+        offs = np.ascontiguousarray(rs.offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(rs.lengths, dtype=np.uint32)
+        self._check(self.lib.mhap_load_reads(self.ctx, rs.first_iid, rs.nreads,
+                                             bases.ctypes.data, offs.ctypes.data,
+                                             lens.ctypes.data))
+        self.first_iid, self.nreads = rs.first_iid, rs.nreads
+
+    def load_reads_device(self, first_iid: int, d_bases: int, d_offsets: int,
+                          lengths: np.ndarray) -> None:
+        lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+        self._check(self.lib.mhap_load_reads_device(self.ctx, first_iid, lens.shape[0],
+                                                    d_bases, d_offsets, lens.ctypes.data))
+        self.first_iid, self.nreads = first_iid, int(lens.shape[0])
+
+    def set_filter_kmers(self, kmers: list[str]) -> None:
+        blob = "".join(kmers).encode()
+        self._check(self.lib.mhap_set_filter_kmers(self.ctx, blob, len(kmers)))
+
+    def sketch(self, bgn: int | None = None, end: int | None = None) -> None:
+        bgn = self.first_iid if bgn is None else bgn
+        end = self.first_iid + self.nreads - 1 if end is None else end
+        self._check(self.lib.mhap_sketch(self.ctx, bgn, end))
+
+    def sketch_buffers(self) -> tuple[int, int, int]:
+        a, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self.lib.mhap_sketch_buffers(self.ctx, ctypes.byref(a), ctypes.byref(b),
+                                                 ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def build_index(self) -> None:
+        self._check(self.lib.mhap_build_index(self.ctx))
+
+    def compare(self, bgn: int | None = None, end: int | None = None) -> int:
+        bgn = self.first_iid if bgn is None else bgn
+        end = self.first_iid + self.nreads - 1 if end is None else end
+        n = ctypes.c_uint64()
+        self._check(self.lib.mhap_compare(self.ctx, bgn, end, ctypes.byref(n)))
+        return n.value
+
+    def fetch(self) -> np.ndarray:
+        n = self.stats()["overlaps"]
+        rec = np.zeros(max(n, 1), dtype=MHAP_DTYPE)
+        got = ctypes.c_uint64()
+        self._check(self.lib.mhap_fetch(self.ctx, rec.ctypes.data, n, ctypes.byref(got)))
+        return rec[:got.value]
+
+    def write_text(self, path: str, hash_base: int = 1, num_hash: int | None = None,
+                   query_base: int = 1) -> None:
+        nh = self.nreads if num_hash is None else num_hash
+        self._check(self.lib.mhap_write_text(self.ctx, path.encode(), hash_base, nh, query_base))
+
+    def stats(self) -> dict:
+        s = _Stats()
+        self._check(self.lib.mhap_get_stats(self.ctx, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in _Stats._fields_}
+
+    def run(self, rs, filter_kmers=None) -> np.ndarray:
+        """One all-vs-all job over rs: every pair (a < b) once, records sorted by (a, b)."""
+        self.load_reads(rs)
+        if filter_kmers:
+            self.set_filter_kmers(filter_kmers)
+        self.sketch()
+        self.build_index()
+        self.compare()
+        return self.fetch()
+
+
+def format_line(r, hash_base: int = 1, num_hash: int = 0, query_base: int = 1) -> str:
+    """One record as MHAP's text line (the layout mhap_write_text writes)."""
+    w0 = int(r["a"]) - (query_base - 1) + num_hash
+    w1 = int(r["b"]) - (hash_base - 1)
+    return (f"{w0} {w1} {float(r['erate']):.6f} {int(r['count'])} 0 {int(r['a_bgn'])} "
+            f"{int(r['a_end'])} {int(r['a_len'])} {int(r['o'])} {int(r['b_bgn'])} "
+            f"{int(r['b_end'])} {int(r['b_len'])}")

@@ -26,6 +26,8 @@ class ReadSet:
     lengths: np.ndarray      # uint32
     quals: np.ndarray | None = None   # uint8 0..60, same layout as bases
     first_iid: int = 1
+    starts: np.ndarray | None = None  # synthetic truth: genome start of each read
+    strands: np.ndarray | None = None # synthetic truth: 1 = reverse-complemented
 
     @property
     def nreads(self) -> int:
@@ -99,6 +101,8 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
     genome_len = genome.shape[0]
     lo, hi = read_range if read_range else (0, n_reads)
     lengths = np.empty(hi - lo, dtype=np.uint32)
+    starts = np.empty(hi - lo, dtype=np.int64)
+    strands = np.zeros(hi - lo, dtype=np.uint8)
     chunks = []
     for i in range(lo, hi):
         rng = np.random.default_rng([seed, i])
@@ -110,8 +114,10 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
         start = int(rng.integers(0, genome_len - span + 1))
         seg = genome[start:start + span]
         rd = _mutate(rng, seg, L, error_rate, sub_frac, ins_frac)
+        starts[i - lo] = start
         if rng.random() < 0.5:
             rd = _COMP[rd[::-1]]
+            strands[i - lo] = 1
         if n_rate > 0:
             m = rng.random(rd.shape[0]) < n_rate
             rd = rd.copy()
@@ -127,7 +133,7 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
         quals = np.random.default_rng([seed, n_reads, 7]).integers(
             2, 41, size=bases.shape[0]).astype(np.uint8)
     return ReadSet(bases=bases, offsets=offsets, lengths=lengths, quals=quals,
-                   first_iid=1 + lo)
+                   first_iid=1 + lo, starts=starts, strands=strands)
 
 
 def profile(name: str, seed: int = 1, **over) -> ReadSet:

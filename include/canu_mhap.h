@@ -1,0 +1,132 @@
+/*
+ * canu_mhap.h -- C-ABI of the MI355X-native MHAP MinHash sketch / filter stage.
+ *
+ * Replaces the MHAP jar canu runs for overlapper=mhap (src/mhap/mhap-2.1.2.tar, invoked by
+ * src/pipelines/canu/OverlapMhap.pm:374-498: "precompute" = sketch a block, then one job per
+ * query block = compare against the hash blocks).  The output keeps MHAP's text format, the
+ * one src/mhap/mhapConvert.C:114-150 turns into ovOverlap records (.ovb), so canu's
+ * mhapConvert step runs unchanged on it.
+ *
+ *   reference (OverlapMhap.pm option)          here
+ *   -----------------------------------------  -------------------------------------------
+ *   -k <MhapMerSize>              (:381)       mhap_params.k
+ *   --num-hashes                  (:386)       mhap_params.num_hashes
+ *   --num-min-matches             (:387)       mhap_params.min_matches
+ *   --ordered-sketch-size         (:388)       mhap_params.ordered_sketch
+ *   --ordered-kmer-size           (:389)       mhap_params.ordered_k
+ *   --threshold                   (:390)       mhap_params.threshold
+ *   --min-olap-length             (:392)       mhap_params.min_olap
+ *   -f frequentMers.ignore        (:394)       mhap_set_filter_kmers()
+ *   -p block.fasta (precompute)   (:395)       mhap_load_reads*() + mhap_sketch()
+ *   -s hash blocks / -q queries   (:494-495)   mhap_build_index() + mhap_compare()
+ *   stdout  *.mhap                (:496)       mhap_fetch() / mhap_write_text()
+ *
+ * The algorithm is the published MinHash sketch + ordered-sketch filter, restated in
+ * oracle/mhap_oracle.py (PARITY UNPINNED against the jar, which is never run).
+ * All functions return 0 or a negative status (same codes as canu_ovl.h); mhap_last_error()
+ * gives a message.  No CPU fallback: without a gfx950 device mhap_ctx_create() fails.
+ */
+#ifndef CANU_MHAP_H
+#define CANU_MHAP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHAP_ABI_VERSION 1
+
+typedef struct {
+  uint32_t k;               /* -k                      MinHash k-mer size, 1..32        */
+  uint32_t num_hashes;      /* --num-hashes            1..1024                          */
+  uint32_t min_matches;     /* --num-min-matches                                        */
+  uint32_t ordered_sketch;  /* --ordered-sketch-size   1..1984                          */
+  uint32_t ordered_k;       /* --ordered-kmer-size     1..32                            */
+  int32_t  min_olap;        /* --min-olap-length                                        */
+  double   threshold;       /* --threshold (identity of the second-stage filter)        */
+} mhap_params;
+
+/* canu's correction defaults at 'normal' sensitivity (OverlapMhap.pm:116-121,
+ * Defaults.pm:704-705): k 16, 512 hashes, 3 min matches, threshold 0.78, ordered sketch
+ * 1536 of 12-mers, min overlap 500. */
+void        mhap_params_init(mhap_params *p);
+
+/* One MHAP output line (mhapConvert.C:117-120 column order). */
+typedef struct {
+  uint32_t a_iid, b_iid;    /* query read, hash read (gkStore IDs)                      */
+  double   erate;           /* estimated error (Mash distance of the 2nd-stage Jaccard) */
+  uint32_t count;           /* shared min-mers (first stage)                            */
+  int32_t  a_bgn, a_end, a_len;
+  uint32_t b_rc;            /* 1: b coordinates are on b's reverse complement           */
+  int32_t  b_bgn, b_end, b_len;
+} mhap_record;
+
+typedef struct {
+  uint64_t sketched_reads;
+  uint64_t candidates;      /* pairs passing the first stage                            */
+  uint64_t overlaps;        /* pairs passing the second stage                           */
+  double   ms_sketch;       /* device time: MinHash + ordered sketches                  */
+  double   ms_index;        /* device time: MinHash index sort                          */
+  double   ms_candidates;   /* device time: first-stage lookups                         */
+  double   ms_compare;      /* device time: second-stage filter                         */
+  uint64_t sketch_kmers;    /* k-mers hashed by the MinHash kernel                      */
+} mhap_stats;
+
+typedef struct mhap_ctx mhap_ctx;
+
+int         mhap_ctx_create(const mhap_params *p, int device, mhap_ctx **out);
+void        mhap_ctx_destroy(mhap_ctx *ctx);
+const char *mhap_last_error(void);
+int         mhap_abi_version(void);
+
+/* Reads first_iid .. first_iid+nreads-1; bases concatenated (any case; non-ACGT breaks
+ * k-mers), read i at offsets[i] for lengths[i] bytes.  Copied to the device once. */
+int         mhap_load_reads(mhap_ctx *ctx, uint32_t first_iid, uint32_t nreads,
+                            const uint8_t *bases, const uint64_t *offsets,
+                            const uint32_t *lengths);
+/* Same with device-resident bases/offsets (HBM), host lengths. */
+int         mhap_load_reads_device(mhap_ctx *ctx, uint32_t first_iid, uint32_t nreads,
+                                   const uint8_t *d_bases, const uint64_t *d_offsets,
+                                   const uint32_t *h_lengths);
+
+/* -f: k-mers (n * k ACGT bytes, back to back) that never enter a MinHash sketch. */
+int         mhap_set_filter_kmers(mhap_ctx *ctx, const char *kmers, uint64_t n);
+
+/* Sketch reads bgn_iid..end_iid (inclusive): MinHash sketch + ordered sketch. */
+int         mhap_sketch(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);
+
+/* Device arrays holding every loaded read's sketches, for an all-gather across ranks:
+ *   minhash  int32 [nreads][num_hashes]
+ *   ordered  uint64 [nreads][ordered_sketch]  (hash << 32 | pos << 1 | strand)
+ *   ocount   uint32 [nreads]                  (entries used in each ordered row)
+ * Valid after mhap_load_reads*(); rows of reads this rank did not sketch are filled by the
+ * caller (e.g. RCCL all-gather) before mhap_build_index(). */
+int         mhap_sketch_buffers(mhap_ctx *ctx, void **d_minhash, void **d_ordered,
+                                void **d_ocount);
+
+/* Build the MinHash index over all loaded reads' sketches. */
+int         mhap_build_index(mhap_ctx *ctx);
+
+/* Compare queries bgn_iid..end_iid against every loaded read with a larger ID (each pair
+ * once); results stay on the device; *n_out = records found. */
+int         mhap_compare(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid, uint64_t *n_out);
+
+/* Records of the last compare, sorted by (a_iid, b_iid). */
+int         mhap_fetch(mhap_ctx *ctx, mhap_record *out, uint64_t max_records,
+                       uint64_t *n_copied);
+
+/* MHAP's text output of the last compare, numbered the way mhapConvert -h/-q expects:
+ * hash read b_iid is written as b_iid - (hash_base - 1); query a_iid as
+ * a_iid - (query_base - 1) + num_hash (mhapConvert.C:122-123). */
+int         mhap_write_text(mhap_ctx *ctx, const char *path, uint32_t hash_base,
+                            uint32_t num_hash, uint32_t query_base);
+
+int         mhap_get_stats(mhap_ctx *ctx, mhap_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -148,6 +148,39 @@ def read_ovb_reference(path: str) -> np.ndarray:
         return np.fromfile(out, dtype=RECORD_DTYPE)
 
 
+MHAPCONVERT_BIN = os.path.join(HERE, "_ref", "mhapConvert")
+
+
+def mhap_convert_available() -> bool:
+    return os.path.exists(MHAPCONVERT_BIN) and os.path.exists(REF_BIN)
+
+
+def mhap_convert(rs, mhap_path: str, hash_base: int = 1, num_hash: int | None = None,
+                 query_base: int = 1) -> np.ndarray:
+    """Run the REFERENCE mhapConvert (src/mhap/mhapConvert.C, built from its source) on an
+    MHAP text file against a gkpStore of rs (built by the reference's gkStore code via
+    oic_ref --gkp-only); return the ovOverlap records of the .ovb it writes, in file order
+    (read back with the reference's ovFile reader)."""
+    from canu_amd.synth import write_reads_file  # input writer only
+    if not mhap_convert_available():
+        raise FileNotFoundError(MHAPCONVERT_BIN)
+    nh = rs.nreads if num_hash is None else num_hash
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as wd:
+        reads = os.path.join(wd, "reads.bin")
+        write_reads_file(reads, rs)
+        cp = subprocess.run([REF_BIN, reads, os.path.join(wd, "w"), "-", "--gkp-only"],
+                            capture_output=True, text=True)
+        if cp.returncode != 0:
+            raise RuntimeError(f"oic_ref --gkp-only failed: {cp.stderr[-2000:]}")
+        ovb = os.path.join(wd, "mhap.ovb")
+        cp = subprocess.run([MHAPCONVERT_BIN, "-G", os.path.join(wd, "w", "ref.gkpStore"),
+                             "-o", ovb, "-h", str(hash_base), str(nh), "-q", str(query_base),
+                             mhap_path], capture_output=True, text=True)
+        if cp.returncode != 0:
+            raise RuntimeError(f"mhapConvert failed ({cp.returncode}): {cp.stderr[-2000:]}")
+        return read_ovb_reference(ovb)
+
+
 def params_to_ref_args(params: dict) -> list[str]:
     a = ["-k", str(params["kmer_len"]), "--maxerate", repr(params["max_erate"]),
          "--minlength", str(params["min_olap_len"])]

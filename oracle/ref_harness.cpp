@@ -24,6 +24,7 @@
  *
  * usage: oic_ref <reads.bin> <workdir> <out.bin> [options]
  *        oic_ref --read-ovb <in.ovb> <out.bin>
+ *        oic_ref <reads.bin> <workdir> - --gkp-only   (gkpStore for mhapConvert -G)
  *   -k N  --maxerate F  --minlength N  -G  -m|-u  -w  -z  -l N  --minkmers
  *   --hashbits N  --hashload F  --hashstrings N  --hashdatalen N  -t N
  *   -h a-b  -r a-b  --skip <kmers.fasta>  --time (print wall seconds of OverlapDriver)
@@ -85,6 +86,7 @@ int main(int argc, char **argv) {
   G.initialize();
   bool        minkmers = false;
   bool        timeIt   = false;
+  bool        gkpOnly  = false;   //  build <workdir>/ref.gkpStore and stop (mhapConvert's -G)
   const char *skipPath = NULL;
 
   for (int arg = 4; arg < argc; arg++) {
@@ -111,6 +113,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-r"))            AS_UTL_decodeRange(argv[++arg], G.bgnRefID, G.endRefID);
     else if (!strcmp(a, "--skip"))        skipPath = argv[++arg];
     else if (!strcmp(a, "--time"))        timeIt = true;
+    else if (!strcmp(a, "--gkp-only"))    gkpOnly = true;
     else { fprintf(stderr, "unknown option '%s'\n", a); exit(1); }
   }
 
@@ -165,6 +168,11 @@ int main(int argc, char **argv) {
       off += lens[i];
     }
     store->gkStore_close();
+  }
+
+  if (gkpOnly) {
+    fprintf(stdout, "GKPSTORE %s\n", gkp.c_str());
+    return 0;
   }
 
   //  ---- 2. globals, as overlapInCore.C main() sets them ---------------------------------

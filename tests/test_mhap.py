@@ -1,0 +1,255 @@
+"""The MHAP stage (include/canu_mhap.h, canu_amd/csrc/mhap.hip).
+
+PARITY UNPINNED against the MHAP jar (src/mhap/mhap-2.1.2.tar: a prebuilt third-party
+archive, never run here).  What IS pinned:
+  * the output format, by the reference's own consumer: every line must go through
+    mhapConvert (src/mhap/mhapConvert.C, compiled from the reference source into
+    oracle/_ref/) and come out as the ovOverlap records the line describes;
+  * the GPU path, against the CPU restatement oracle/mhap_oracle.py: integers bit-exact,
+    erate within 1e-6 (written with 6 decimals);
+  * sanity of the restated algorithm against the synthetic reads' known genome layout.
+CPU tests run here; @gpu tests on the MI355X box."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import mhap_oracle as M
+import oracle
+from canu_amd import mhap
+from canu_amd.synth import synth_reads
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "canu_mhap.h")
+FIELDS = ("a", "b", "count", "a_bgn", "a_end", "a_len", "o", "b_bgn", "b_end", "b_len")
+
+
+def _reads(n=90, L=4000, cov=15, err=0.04, seed=3, **kw):
+    return synth_reads(n_reads=n, read_len=L, genome_len=int(n * L / cov), error_rate=err,
+                       seed=seed, **kw)
+
+
+@pytest.fixture(scope="module")
+def small():
+    return _reads()
+
+
+@pytest.fixture(scope="module")
+def small_oracle(small):
+    return M.run(small, M.default_params())
+
+
+def test_header_declares_the_python_exports():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    assert sorted(set(re.findall(r"\b(mhap_[a-z_]+)\s*\(", src))) == sorted(mhap.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(built):
+    lib = mhap.load_library()
+    assert [f for f in mhap.EXPORTS if not hasattr(lib, f)] == []
+    assert lib.mhap_abi_version() == 1
+
+
+def test_params_init_is_canu_normal(built):
+    lib = mhap.load_library()
+    p = mhap._Params()
+    lib.mhap_params_init(p)
+    d = mhap.MhapParameters()
+    assert (p.k, p.num_hashes, p.min_matches, p.ordered_sketch, p.ordered_k, p.min_olap) == \
+        (d.k, d.num_hashes, d.num_min_matches, d.ordered_sketch_size, d.ordered_kmer_size,
+         d.min_olap_length) == (16, 512, 3, 1536, 12, 500)
+    assert abs(p.threshold - 0.78) < 1e-12
+
+
+def test_sensitivity_presets():
+    """OverlapMhap.pm:109-150."""
+    lo = mhap.MhapParameters.sensitivity("low")
+    assert (lo.num_hashes, lo.num_min_matches, lo.ordered_sketch_size, lo.ordered_kmer_size) == \
+        (256, 3, 1000, 14)
+    hi = mhap.MhapParameters.sensitivity("high", nanopore=True)
+    assert hi.num_hashes == 768 and hi.num_min_matches == 2 and abs(hi.threshold - 0.78) < 1e-12
+    utg = mhap.MhapParameters.sensitivity("normal", tag="utg")
+    assert (utg.num_hashes, utg.num_min_matches, utg.ordered_kmer_size) == (128, 5, 18)
+    with pytest.raises(ValueError):
+        mhap.MhapParameters.sensitivity("fast")
+
+
+def test_parse_canu_command_line():
+    argv = ("--repeat-weight 0.9 --repeat-idf-scale 10 -k 16 --num-hashes 768 "
+            "--num-min-matches 2 --threshold 0.73 --filter-threshold 0.000005 "
+            "--ordered-sketch-size 1536 --ordered-kmer-size 12 --min-olap-length 500 "
+            "--num-threads 8 -s ./blocks/000001.dat -q queries/000001").split()
+    p, io = mhap.parse_mhap_args(argv)
+    assert (p.k, p.num_hashes, p.num_min_matches, p.ordered_sketch_size) == (16, 768, 2, 1536)
+    assert abs(p.threshold - 0.73) < 1e-12 and p.min_olap_length == 500
+    assert io["-s"] == "./blocks/000001.dat" and io["--num-threads"] == "8"
+    with pytest.raises(mhap.MhapError):
+        mhap.parse_mhap_args(["--no-tf"])
+    with pytest.raises(mhap.MhapError):
+        mhap.parse_mhap_args(["--bogus"])
+
+
+def test_oracle_kmer_codes():
+    """Canonical 2-bit codes, first base most significant; non-ACGT breaks k-mers."""
+    c = M._CODE[np.frombuffer(b"ACGTNACGTA", dtype=np.uint8)]
+    pos, can, s = M.kmers(c, 4)
+    # ACGT is its own reverse complement; CGTA/ACGT after the N
+    assert pos.tolist() == [0, 5, 6]
+    assert int(can[0]) == 0b00011011 == int(can[1])      # ACGT = its own reverse complement
+    assert int(can[2]) == 0b01101100                      # CGTA < rc TACG (0b11000110)
+    assert s.tolist() == [0, 0, 0]
+    pos, can, s = M.kmers(M._CODE[np.frombuffer(b"TTTT", dtype=np.uint8)], 4)
+    assert int(can[0]) == 0 and s.tolist() == [1]        # AAAA on the other strand
+
+
+def test_oracle_finds_the_true_overlaps(small, small_oracle):
+    """Sanity of the restated algorithm: overlaps it reports are real (genome intervals
+    intersect, orientation = strand difference, offset close to the truth) and it finds
+    most true overlaps of >= 1.5 kb."""
+    rs, rec = small, small_oracle
+    assert len(rec) > 100
+    st, sd, L = rs.starts, rs.strands.astype(int), rs.lengths.astype(int)
+    for r in rec:
+        a, b = int(r["a"]) - 1, int(r["b"]) - 1
+        ov = min(st[a] + L[a], st[b] + L[b]) - max(st[a], st[b])
+        assert ov > 0, (a, b)
+        assert int(r["o"]) == (sd[a] ^ sd[b])
+    found = {(int(r["a"]) - 1, int(r["b"]) - 1) for r in rec}
+    true = [(a, b) for a in range(rs.nreads) for b in range(a + 1, rs.nreads)
+            if min(st[a] + L[a], st[b] + L[b]) - max(st[a], st[b]) >= 1500]
+    hit = sum((a, b) in found for a, b in true)
+    assert hit >= 0.9 * len(true), (hit, len(true))
+
+
+@pytest.mark.skipif(not oracle.mhap_convert_available(), reason="reference mhapConvert not built")
+def test_reference_mhapconvert_reads_our_lines(small, small_oracle, tmp_path):
+    """The format is the one the reference's mhapConvert consumes: IDs, hangs, flip and
+    erate of every converted ovOverlap match the line."""
+    rec = small_oracle
+    path = str(tmp_path / "q.mhap")
+    with open(path, "w") as f:
+        for r in rec:
+            f.write(mhap.format_line(r, 1, small.nreads, 1) + "\n")
+    ov = oracle.mhap_convert(small, path, 1, small.nreads, 1)
+    assert len(ov) == len(rec)
+    w0, w1 = ov["w0"], ov["w1"]
+    ahg5, ahg3 = w0 & 0x1FFFFF, (w0 >> 21) & 0x1FFFFF
+    bhg5, bhg3 = w1 & 0x1FFFFF, (w1 >> 21) & 0x1FFFFF
+    flipped = (w0 >> 54) & 1
+    assert np.array_equal(ov["a"], rec["a"]) and np.array_equal(ov["b"], rec["b"])
+    assert np.array_equal(ahg5, rec["a_bgn"]) and np.array_equal(ahg3, rec["a_len"] - rec["a_end"])
+    o = rec["o"].astype(bool)
+    assert np.array_equal(flipped.astype(bool), o)
+    want_b5 = np.where(o, rec["b_len"] - rec["b_end"], rec["b_bgn"])
+    want_b3 = np.where(o, rec["b_bgn"], rec["b_len"] - rec["b_end"])
+    assert np.array_equal(bhg5, want_b5) and np.array_equal(bhg3, want_b3)
+    # for*: forUTG/forOBT/forDUP all set (mhapConvert.C:131-133)
+    assert np.all((w0 >> 55) & 7 == 7)
+
+
+# ------------------------------------------------------------------------------- GPU ----
+
+def _gpu(rs, P, filt=None):
+    m = mhap.Mhap(P, device=0)
+    rec = m.run(rs, filter_kmers=filt)
+    st = m.stats()
+    m.close()
+    return rec, st
+
+
+def _same(got, want):
+    assert got.shape == want.shape, (got.shape, want.shape)
+    for f in FIELDS:
+        assert np.array_equal(got[f].astype(np.int64), want[f].astype(np.int64)), f
+    assert np.max(np.abs(got["erate"] - want["erate"]), initial=0.0) <= 1e-6
+
+
+CASES = {
+    "normal": (dict(), mhap.MhapParameters()),
+    "high_ragged_ns": (dict(n=80, L=3000, err=0.05, seed=5, len_jitter=0.5, n_rate=0.002),
+                       mhap.MhapParameters.sensitivity("high", min_olap=300)),
+    "low_k14": (dict(n=70, L=5000, err=0.03, seed=6),
+                mhap.MhapParameters.sensitivity("low", min_olap=500)),
+    "utg_small_k": (dict(n=60, L=2500, err=0.02, seed=7),
+                    mhap.MhapParameters(k=12, num_hashes=128, num_min_matches=5,
+                                        ordered_kmer_size=18, ordered_sketch_size=700,
+                                        min_olap_length=200, threshold=0.8)),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_gpu_matches_oracle(built, name):
+    kw, P = CASES[name]
+    rs = _reads(**kw)
+    got, st = _gpu(rs, P)
+    want = M.run(rs, P.as_oracle())
+    assert len(want) > 20
+    _same(got, want)
+    assert st["overlaps"] == len(want)
+
+
+@pytest.mark.gpu
+def test_gpu_filter_kmers(built, small):
+    """-f: frequent k-mers never enter a sketch."""
+    P = mhap.MhapParameters()
+    r0 = small.read(0).decode()
+    filt = [r0[i:i + 16] for i in range(0, 3000, 7)]
+    got, _ = _gpu(small, P, filt)
+    want = M.run(small, P.as_oracle(), skip_kmers=filt)
+    _same(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_shards_and_text(built, small, small_oracle, tmp_path):
+    """Query-range shards (the multi-GPU split) union to the whole job, and the text the
+    library writes is byte-identical to the oracle records' lines (and, where built, goes
+    through the reference mhapConvert)."""
+    P = mhap.MhapParameters()
+    m = mhap.Mhap(P, device=0)
+    m.load_reads(small)
+    m.sketch()
+    m.build_index()
+    parts = []
+    for lo, hi in ((1, 30), (31, 60), (61, small.nreads)):
+        m.compare(lo, hi)
+        parts.append(m.fetch())
+    m.compare()
+    path = str(tmp_path / "all.mhap")
+    m.write_text(path, 1, small.nreads, 1)
+    m.close()
+    whole = np.concatenate(parts)
+    _same(whole, small_oracle)
+    want = "".join(mhap.format_line(r, 1, small.nreads, 1) + "\n" for r in small_oracle)
+    assert open(path).read() == want
+    if oracle.mhap_convert_available():
+        assert len(oracle.mhap_convert(small, path)) == len(small_oracle)
+
+
+@pytest.mark.gpu
+def test_gpu_sketch_rows_match_oracle(built, small):
+    """Stage outputs directly: the MinHash rows and ordered-sketch rows in HBM."""
+    import ctypes
+    P = mhap.MhapParameters()
+    m = mhap.Mhap(P, device=0)
+    m.load_reads(small)
+    m.sketch()
+    pmh, pord, pcnt = m.sketch_buffers()
+    n, H, S = small.nreads, P.num_hashes, P.ordered_sketch_size
+    mh = np.zeros((n, H), dtype=np.int32)
+    od = np.zeros((n, S), dtype=np.uint64)
+    oc = np.zeros(n, dtype=np.uint32)
+    hip = ctypes.CDLL("libamdhip64.so")        # hipMemcpy D2H (synchronous) of the rows
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(mh.ctypes.data, pmh, mh.nbytes, 2) == 0
+    assert hip.hipMemcpy(od.ctypes.data, pord, od.nbytes, 2) == 0
+    assert hip.hipMemcpy(oc.ctypes.data, pcnt, oc.nbytes, 2) == 0
+    m.close()
+    assert np.array_equal(mh, M.sketch(small, P.as_oracle()))
+    for i in range(0, n, 7):
+        h, pos, s = M.ordered_sketch(small, i, P.as_oracle())
+        assert oc[i] == h.shape[0]
+        key = (h.astype(np.uint64) << np.uint64(32)) | (pos.astype(np.uint64) << np.uint64(1)) \
+            | s.astype(np.uint64)
+        assert np.array_equal(od[i, :oc[i]], key), i
