@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench_mhap.py -- the MHAP stage on MI355X: overlaps/sec on BASELINE configs[3]
+(200k synthetic raw-ONT-like reads x 15 kb, MinHash sketch + two-stage filter).
+
+One step = one whole MHAP job over the resident read set: sketch every read (MinHash and
+ordered sketches), build the MinHash index, compare every query against every later read
+(each pair once).  With --gpus N (torchrun, one process per GPU): every rank generates 1/N
+of the reads and the read store is all-gathered at setup (as bench.py does); in the timed
+step each rank sketches its 1/N of the reads, the sketch rows are ALL-GATHERED over RCCL
+(xGMI) -- the shared MinHash index of BASELINE configs[3] -- every rank sorts the index and
+compares its own query range (ranges balanced by pair count), independent output.
+
+Prints ONE JSON line (rank 0).  The overlapInCore headline is bench.py; this is the second
+stage the north star names (src/mhap).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "overlaps/sec + Gbp-vs-Gbp/sec, MHAP sketch+filter, 200k x 15 kb reads"
+HBM_PEAK_GBS = 8000.0
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 1024 SIMDs x 32 lanes/clk
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=200_000)
+    ap.add_argument("--read-len", type=int, default=15_000)
+    ap.add_argument("--coverage", type=float, default=25.0)
+    ap.add_argument("--read-error", type=float, default=0.05)
+    ap.add_argument("--sensitivity", default="normal")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample-reads", type=int, default=300)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from canu_amd.synth import synth_reads, random_genome
+    from canu_amd.mhap import Mhap, MhapParameters
+    from canu_amd.dist import gather_read_store, query_shards, read_slices, all_gather_rows
+
+    n = args.reads
+    genome_len = int(n * args.read_len / args.coverage)
+    gen_kw = dict(n_reads=n, read_len=args.read_len, genome_len=genome_len,
+                  error_rate=args.read_error, seed=args.seed)
+    t_setup = time.time()
+    genome = random_genome(np.random.default_rng(args.seed), genome_len)
+    lo, hi = read_slices(n, world)[rank]
+    part = synth_reads(genome=genome, read_range=(lo, hi), **gen_kw)
+    dev = torch.device("cuda", local)
+    if world == 1:
+        bases = torch.from_numpy(part.bases).to(dev)
+        lengths = part.lengths
+    else:
+        bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(dev), part.lengths,
+                                           dist, dev)
+    del part
+    offsets = np.zeros(n, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    d_offsets = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    total_bases = int(lengths.sum(dtype=np.uint64))
+
+    P = MhapParameters.sensitivity(args.sensitivity)
+    m = Mhap(P, device=local)
+    m.load_reads_device(1, bases.data_ptr(), d_offsets.data_ptr(), lengths)
+    H, S = P.num_hashes, P.ordered_sketch_size
+    if world > 1:
+        mh_l = torch.empty((hi - lo, H), dtype=torch.int32, device=dev)
+        od_l = torch.empty((hi - lo, S), dtype=torch.int64, device=dev)
+        oc_l = torch.empty((hi - lo,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    q_lo, q_hi = query_shards(n, world)[rank]
+    setup_s = time.time() - t_setup
+    ms = {"sketch": 0.0, "index": 0.0, "candidates": 0.0, "compare": 0.0, "gather": 0.0}
+
+    def step() -> int:
+        m.sketch(lo + 1, hi)
+        st = m.stats()
+        ms["sketch"] += st["ms_sketch"]
+        if world > 1:
+            t0 = time.perf_counter()
+            m.copy_sketches(lo + 1, hi - lo, mh_l.data_ptr(), od_l.data_ptr(), oc_l.data_ptr(),
+                            False)
+            mh = all_gather_rows(mh_l, n, dist)
+            od = all_gather_rows(od_l, n, dist)
+            oc = all_gather_rows(oc_l, n, dist)
+            torch.cuda.synchronize()
+            m.copy_sketches(1, n, mh.data_ptr(), od.data_ptr(), oc.data_ptr(), True)
+            del mh, od, oc
+            ms["gather"] += 1000.0 * (time.perf_counter() - t0)
+        m.build_index()
+        nrec = m.compare(q_lo, q_hi) if q_lo <= q_hi else 0
+        st = m.stats()
+        ms["index"] += st["ms_index"]
+        ms["candidates"] += st["ms_candidates"]
+        ms["compare"] += st["ms_compare"]
+        return nrec
+
+    for _ in range(args.warmup):
+        step()
+    for k in ms:
+        ms[k] = 0.0
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nrec = 0
+    for _ in range(args.steps):
+        nrec = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = m.stats()
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    nr = torch.tensor([nrec, st["candidates"]], dtype=torch.int64, device=dev)
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(nr, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_ovl, total_cand = int(nr[0].item()), int(nr[1].item())
+    value = total_ovl * args.steps / elapsed
+    gbp = total_bases / 1e9
+
+    # Dominant kernel: the MinHash sketch (integer VALU: per k-mer and hash function one
+    # 64-bit xorshift = 3 shifts + 3 xors on 32-bit halves, plus a min).  HBM roofline:
+    # bases read once (1 B/base) + the sketch rows written (4 B x H per read).
+    kmers = st["sketch_kmers"]
+    sk_ms = ms["sketch"] / args.steps
+    sk_bytes = total_bases / world + 4.0 * H * (hi - lo)
+    roof = {"bound": "hbm", "kernel": "k_mh_sketch + k_mh_ordered",
+            "achieved": round(sk_bytes / (sk_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "traffic": None,
+            "algorithmic_bytes_per_launch": int(sk_bytes), "avg_launch_ms": round(sk_ms, 3),
+            "limiter": "integer VALU (H xorshift64 hash functions per k-mer)",
+            "valu": {"lane_ops": int(kmers * H * 9),
+                     "achieved_tops": round(kmers * H * 9 / (sk_ms * 1e-3) / 1e12, 2),
+                     "peak_tops": round(VALU_PEAK_TOPS, 1),
+                     "frac": round(kmers * H * 9 / (sk_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}}
+    roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, P)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "overlaps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 2),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u8 bases, int32/u64 hash sketches", "data": "synthetic",
+            "config": {"workload": "configs[3]: MHAP MinHash sketch+filter, synthetic reads, "
+                                   "all-vs-all", "reads": n, "read_len": args.read_len,
+                       "coverage": args.coverage, "read_error": args.read_error,
+                       "sensitivity": args.sensitivity, "num_hashes": H,
+                       "ordered_sketch": S, "k": P.k, "ordered_k": P.ordered_kmer_size,
+                       "parallelism": f"query-shard{world}"},
+            "overlaps_per_step": total_ovl, "candidates_per_step": total_cand,
+            "gbp_vs_gbp_per_sec": round(gbp * gbp / 2.0 * args.steps / elapsed, 3),
+            "breakdown_ms": {k: round(v / args.steps, 2) for k, v in ms.items()},
+            "setup_s": round(setup_s, 1), "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    m.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, P) -> dict | None:
+    """The numpy restatement (oracle/mhap_oracle.py, one core) on a bounded sample of the
+    same workload: fewer reads, same read length / error / coverage."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import mhap_oracle
+        from canu_amd.synth import synth_reads
+    except Exception:
+        return None
+    ns = args.cpu_sample_reads
+    gl = int(ns * args.read_len / args.coverage)
+    rs = synth_reads(ns, args.read_len, gl, args.read_error, seed=args.seed + 1000)
+    t0 = time.perf_counter()
+    rec = mhap_oracle.run(rs, P.as_oracle())
+    secs = time.perf_counter() - t0
+    return {"value": round(len(rec) / secs, 2), "unit": "overlaps/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{ns} reads x {args.read_len} bp at {args.coverage:.0f}x (genome {gl} bp), "
+                      f"numpy restatement {secs:.1f}s, {len(rec)} overlaps"}
+
+
+if __name__ == "__main__":
+    main()

@@ -39,7 +39,7 @@
 namespace mh {
 
 constexpr int32_t I32MAX = 0x7FFFFFFF;
-constexpr int RK = 16;            // k-mers per thread per round in k_mh_sketch
+constexpr int RK = 32;            // k-mers per thread per round in k_mh_sketch
 constexpr int OCAP = 4096;        // collected ordered-sketch entries per read (LDS)
 constexpr int NBIN = 4096;        // histogram bins (hash >> 20)
 constexpr int TSLOTS = 1024;      // candidate table slots per wave
@@ -166,9 +166,20 @@ __global__ void __launch_bounds__(256) k_mh_sketch(SketchArgs A) {
     }
     nk += __builtin_popcount(vm);
     if (__builtin_amdgcn_ballot_w64(vm != 0) == 0) continue;   // wave has nothing here
+    // invalid slots take a copy of a valid k-mer's state (min is idempotent), so the
+    // per-function loop needs no per-slot masking; a thread with no valid k-mer at all
+    // contributes INT32_MAX
+    {
+      uint64_t x0 = 0;
+#pragma unroll
+      for (int i = RK - 1; i >= 0; i--) x0 = (vm >> i) & 1u ? X[i] : x0;
+#pragma unroll
+      for (int i = 0; i < RK; i++) X[i] = (vm >> i) & 1u ? X[i] : x0;
+    }
+    const bool live = vm != 0;
     int32_t *wm = s_min + wave * H;
     for (int32_t j = 0; j < H; j++) {
-      int32_t m = I32MAX;
+      int32_t v[RK];
 #pragma unroll
       for (int i = 0; i < RK; i++) {
         uint64_t x = X[i];
@@ -176,9 +187,17 @@ __global__ void __launch_bounds__(256) k_mh_sketch(SketchArgs A) {
         x ^= x >> 35;
         x ^= x << 4;
         X[i] = x;
-        const int32_t v = (vm >> i) & 1u ? (int32_t)(uint32_t)x : I32MAX;
-        m = v < m ? v : m;
+        v[i] = (int32_t)(uint32_t)x;
       }
+      // min over the slots as a min3 tree
+      int32_t m = v[0];
+#pragma unroll
+      for (int i = 1; i + 1 < RK; i += 2) {
+        const int32_t a = v[i] < v[i + 1] ? v[i] : v[i + 1];
+        m = m < a ? m : a;
+      }
+      if ((RK & 1) == 0) m = m < v[RK - 1] ? m : v[RK - 1];
+      m = live ? m : I32MAX;
       m = wave_min(m);
       if (lane == 0 && m < wm[j]) wm[j] = m;
     }
@@ -857,6 +876,29 @@ int mhap_sketch_buffers(mhap_ctx *c, void **d_minhash, void **d_ordered, void **
   *d_minhash = c->minhash.p;
   *d_ordered = c->ordered.p;
   *d_ocount = c->ocount.p;
+  return M_OK;
+}
+
+int mhap_copy_sketches(mhap_ctx *c, uint32_t first, uint32_t n, void *d_minhash,
+                       void *d_ordered, void *d_ocount, int to_ctx) {
+  if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
+  if (n == 0) return M_OK;
+  if (first < c->first_iid || (uint64_t)first + n > (uint64_t)c->first_iid + c->nreads)
+    return mfail(M_BAD_PARAM, "rows %u..%u outside the loaded reads", first, first + n - 1);
+  MHC(hipSetDevice(c->device));
+  const size_t r0 = first - c->first_iid;
+  const size_t H = c->P.num_hashes, S = c->P.ordered_sketch;
+  struct { void *ctx; void *user; size_t bytes; } parts[3] = {
+      {c->minhash.p + r0 * H, d_minhash, 4 * H * n},
+      {c->ordered.p + r0 * S, d_ordered, 8 * S * n},
+      {c->ocount.p + r0, d_ocount, 4ull * n}};
+  for (auto &pt : parts) {
+    if (!pt.user) return mfail(M_BAD_PARAM, "null buffer");
+    if (to_ctx) MHC(hipMemcpyAsync(pt.ctx, pt.user, pt.bytes, hipMemcpyDeviceToDevice, c->stream));
+    else        MHC(hipMemcpyAsync(pt.user, pt.ctx, pt.bytes, hipMemcpyDeviceToDevice, c->stream));
+  }
+  MHC(hipStreamSynchronize(c->stream));
+  if (to_ctx) c->indexed = false;
   return M_OK;
 }
 

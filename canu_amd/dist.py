@@ -60,3 +60,23 @@ def gather_read_store(bases_local, lengths_local: np.ndarray, dist, device):
     dist.all_gather(gl, lb)
     lengths = torch.cat([g[:k] for g, k in zip(gl, nls)]).cpu().numpy().astype(np.uint32)
     return bases, lengths
+
+
+def read_slices(n: int, world: int) -> list[tuple[int, int]]:
+    """[lo, hi) of the reads rank r generates / sketches: n * r // world .. n * (r+1) // world."""
+    return [(n * r // world, n * (r + 1) // world) for r in range(world)]
+
+
+def all_gather_rows(local, n: int, dist):
+    """All-gather a per-rank slice of rows (torch tensor [rows_r, ...], slices as
+    read_slices(n, world)) into the whole [n, ...] tensor, in rank order.  One collective:
+    slices are padded to the largest one (RCCL over xGMI on the GPUs, gloo on CPU)."""
+    import torch
+    world = dist.get_world_size()
+    sl = read_slices(n, world)
+    rmax = max(hi - lo for lo, hi in sl)
+    pad = torch.zeros((rmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    got = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(got, pad)
+    return torch.cat([g[:hi - lo] for g, (lo, hi) in zip(got, sl)])

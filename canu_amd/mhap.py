@@ -21,7 +21,8 @@ MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("count", "
 
 EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last_error",
            "mhap_abi_version", "mhap_load_reads", "mhap_load_reads_device",
-           "mhap_set_filter_kmers", "mhap_sketch", "mhap_sketch_buffers", "mhap_build_index",
+           "mhap_set_filter_kmers", "mhap_sketch", "mhap_sketch_buffers", "mhap_copy_sketches",
+           "mhap_build_index",
            "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
 
 
@@ -66,6 +67,7 @@ def load_library(path: str | None = None):
     lib.mhap_set_filter_kmers.argtypes = [V, ctypes.c_char_p, U64]
     lib.mhap_sketch.argtypes = [V, U32, U32]
     lib.mhap_sketch_buffers.argtypes = [V, P(V), P(V), P(V)]
+    lib.mhap_copy_sketches.argtypes = [V, U32, U32, V, V, V, ctypes.c_int]
     lib.mhap_build_index.argtypes = [V]
     lib.mhap_compare.argtypes = [V, U32, U32, P(U64)]
     lib.mhap_fetch.argtypes = [V, V, U64, P(U64)]
@@ -214,6 +216,13 @@ class Mhap:
         self._check(self.lib.mhap_sketch_buffers(self.ctx, ctypes.byref(a), ctypes.byref(b),
                                                  ctypes.byref(c)))
         return a.value, b.value, c.value
+
+    def copy_sketches(self, first_iid: int, n: int, d_minhash: int, d_ordered: int,
+                      d_ocount: int, to_ctx: bool) -> None:
+        """Export (to_ctx=False) / import (True) the sketch rows of n reads from first_iid
+        to / from caller device buffers (e.g. torch tensors' data_ptr())."""
+        self._check(self.lib.mhap_copy_sketches(self.ctx, first_iid, n, d_minhash, d_ordered,
+                                                d_ocount, 1 if to_ctx else 0))
 
     def build_index(self) -> None:
         self._check(self.lib.mhap_build_index(self.ctx))

@@ -106,6 +106,14 @@ int         mhap_sketch(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);
 int         mhap_sketch_buffers(mhap_ctx *ctx, void **d_minhash, void **d_ordered,
                                 void **d_ocount);
 
+/* Copy the sketch rows of reads first_iid .. first_iid+n-1 between the context and caller
+ * device buffers laid out like mhap_sketch_buffers() (rows of those reads only):
+ * to_ctx = 0 exports the context's rows, to_ctx = 1 imports the caller's (e.g. after an
+ * RCCL all-gather of every rank's exported slice).  Device-to-device, on the context's
+ * stream; returns after it completes. */
+int         mhap_copy_sketches(mhap_ctx *ctx, uint32_t first_iid, uint32_t n, void *d_minhash,
+                               void *d_ordered, void *d_ocount, int to_ctx);
+
 /* Build the MinHash index over all loaded reads' sketches. */
 int         mhap_build_index(mhap_ctx *ctx);
 

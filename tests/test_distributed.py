@@ -66,3 +66,53 @@ def test_gloo_world2_gather_and_shards():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert ok_store and ok_union and n > 0
+
+
+def _mhap_worker(rank, world, port, q):
+    """MHAP's multi-GPU split on CPU: each rank sketches its slice of the reads, the sketch
+    rows are all-gathered (bench_mhap.py does this over RCCL), each rank compares its own
+    query shard; the gathered rows equal the whole job's and the shards union to it."""
+    import torch
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import mhap_oracle as M
+    from canu_amd.dist import all_gather_rows, query_shards, read_slices
+    from canu_amd.synth import ReadSet, synth_reads
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, L = 41, 3000
+    rs = synth_reads(n, L, n * L // 12, 0.04, seed=9)
+    p = M.default_params(num_hashes=128, ordered_sketch=600, min_olap=300)
+    lo, hi = read_slices(n, world)[rank]
+    part = ReadSet(bases=rs.bases, offsets=rs.offsets[lo:hi], lengths=rs.lengths[lo:hi])
+    mine = torch.from_numpy(M.sketch(part, p))
+    full = all_gather_rows(mine, n, dist).numpy()
+    q_lo, q_hi = query_shards(n, world)[rank]
+    recs = M.run(rs, p, q_range=(q_lo - 1, q_hi))
+    got = [None] * world
+    dist.all_gather_object(got, recs.tobytes())
+    if rank == 0:
+        whole = M.run(rs, p)
+        union = np.concatenate([np.frombuffer(b, dtype=M.MHAP_DTYPE) for b in got])
+        union = union[np.lexsort((union["b"], union["a"]))]
+        q.put((np.array_equal(full, M.sketch(rs, p)), np.array_equal(union, whole), len(whole)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_mhap_sketch_gather_and_shards():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mhap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok_rows, ok_union, n = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert ok_rows and ok_union and n > 0
