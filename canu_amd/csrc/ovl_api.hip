@@ -641,6 +641,18 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     if (nb > 0) stg_lds = std::max<size_t>(stg_lds, (160 * 1024) / nb - 256);
   }
   ext_waves = (ext_waves / 8) * 8;
+  if (staged) {
+    // persistent grid: as many 512-thread blocks as are resident at once (registers and
+    // LDS), so no block starts only after the work queue has drained
+    int bpc = 0;
+    const bool l16 = c->max_len < 16384;
+    hipError_t oe = l16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                              &bpc, reinterpret_cast<const void *>(k_extend<true, true>), 64 * stg_wpb, stg_lds)
+                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                              &bpc, reinterpret_cast<const void *>(k_extend<true, false>), 64 * stg_wpb, stg_lds);
+    if (oe == hipSuccess && bpc > 0)
+      ext_waves = std::min<uint32_t>(ext_waves, (uint32_t)bpc * stg_wpb * c->n_cu);
+  }
   uint32_t chain_waves = 16u * c->n_cu;
   const uint32_t DONE_CAP = 4096;
   if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");

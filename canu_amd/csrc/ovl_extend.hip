@@ -499,6 +499,8 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
   g_ci32 *rows = (g_ci32 *)WM.rows;
   typedef __attribute__((address_space(1))) const int16_t g_ci16;
   g_ci16 *rows16 = (g_ci16 *)WM.rows;
+  typedef __attribute__((address_space(1))) int32_t g_i32;
+  g_i32 *gdst = (g_i32 *)dst;                  // global, not flat (see wave_ped_reg's log)
   vm_sync();                                  // the log is complete
   int32_t d = __builtin_amdgcn_readfirstlane(tb_d);
   last = __builtin_amdgcn_readfirstlane(last);
@@ -526,12 +528,12 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
       if (pm > mx) { from = -1; mx = pm; }
       if (1 + pp > mx) { from = 1; mx = 1 + pp; }
       if (from < 0) {
-        if (lane == 0) dst[nd] = mx - last - 1;
+        if (lane == 0) gdst[nd] = mx - last - 1;
         nd++;
         last = pm;
         d--;
       } else if (from > 0) {
-        if (lane == 0) dst[nd] = last - (mx - 1);
+        if (lane == 0) gdst[nd] = last - (mx - 1);
         nd++;
         last = pp;
         d++;
@@ -600,7 +602,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   // 64*J-cell stripe at e * 64J, cell = d mod 64J (the window holds 64J consecutive
   // diagonals, so the index is unique and needs no per-row base).  Row 0 is logged here.
   typedef typename std::conditional<L16, int16_t, int32_t>::type cell_t;
-  cell_t *clog = (cell_t *)rows;
+  // global (not flat) stores: a flat store also counts against lgkmcnt, so every LDS wait
+  // of the next row would wait for the log stores too
+  typedef __attribute__((address_space(1))) cell_t g_cell_t;
+  g_cell_t *clog = (g_cell_t *)rows;
   clog[(B + (int32_t)lane) & (64 * J - 1)] = (cell_t)R[0];
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
@@ -704,10 +709,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
                                                      (uint32_t)pt);
       const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
       const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
-      // k = min(run, lim) when lim > 0, else 0  (run >= 0)
+      // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
-      NR[j] = r + (k > 0 ? k : 0);
-      need[j] = __builtin_amdgcn_ballot_w64((mm == 0u) & (lim > 32));
+      NR[j] = r + k;                           // lim >= 0 on active lanes, 0 elsewhere
+      need[j] = __builtin_amdgcn_ballot_w64(mm == 0u) & __builtin_amdgcn_ballot_w64(lim > 32);
     }
 #ifdef OVL_PROFILE
     pc_nch += (jr + 1 > JU ? jr + 1 : JU);
@@ -743,7 +748,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t r = NR[j];
-      em[j] = __builtin_amdgcn_ballot_w64((r == m) | (r + d == n)) & actm[j];
+      em[j] = (__builtin_amdgcn_ballot_w64(r == m) | __builtin_amdgcn_ballot_w64(r + d == n)) &
+              actm[j];
       km[j] = __builtin_amdgcn_ballot_w64(r + (d > 0 ? d : 0) >= ML) & actm[j];
       endany |= em[j];
     }
@@ -817,7 +823,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     int32_t mx = NEG;
     const uint32_t kspan = (uint32_t)(nr - nl);
     const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
-    cell_t *crow = clog + (size_t)e * (64 * J);
+    g_cell_t *crow = clog + (size_t)e * (64 * J);
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jrs) break;
