@@ -805,7 +805,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.dbg = nullptr;
     if (getenv("OVL_DEBUG")) {
       static DBuf<unsigned long long> dbgbuf;
-      if (!dbgbuf.p) { (void)dbgbuf.alloc(16); (void)hipMemset(dbgbuf.p, 0, 128); }
+      if (!dbgbuf.p) { (void)dbgbuf.alloc(32); (void)hipMemset(dbgbuf.p, 0, 256); }
       EA.dbg = dbgbuf.p;
       dbg_ptr_for_print = dbgbuf.p;
     }
@@ -861,8 +861,10 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   unsigned long long hs[8];
   HIPC(hipMemcpy(hs, d_stats.p, 64, hipMemcpyDeviceToHost));
   if (dbg_ptr_for_print) {
-    unsigned long long dd[16];
-    (void)hipMemcpy(dd, dbg_ptr_for_print, 128, hipMemcpyDeviceToHost);
+    unsigned long long dd[32];
+    (void)hipMemcpy(dd, dbg_ptr_for_print, 256, hipMemcpyDeviceToHost);
+    fprintf(stderr, "OVL_DEBUG cyc_A=%llu cyc_B=%llu cyc_cont=%llu cyc_C=%llu\n", dd[16], dd[17],
+            dd[18], dd[19]);
     fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu slide_iters=%llu tb=%llu iters=%llu "
             "cyc_chunks=%llu cyc_tb=%llu pairs=%llu maxrows=%llu cyc_rest=%llu cyc_ped=%llu "
             "cyc_calls=%llu cyc_pair=%llu cyc_stage=%llu cyc_extend=%llu\n",

@@ -475,6 +475,17 @@ __device__ __forceinline__ int32_t dpp_from_lower(int32_t v, int32_t lane0) {   
 __device__ __forceinline__ int32_t dpp_from_upper(int32_t v, int32_t lane63) {  // lane l <- l+1
   return __builtin_amdgcn_update_dpp(lane63, v, 0x130, 0xf, 0xf, false);
 }
+// Chunk-boundary neighbours without a readlane: lane l <- v[l-1], lane 0 <- prev[63]
+// (wave_ror:1 of prev supplies lane 0, then wave_shr:1 of v overwrites lanes 1..63), and
+// lane l <- v[l+1], lane 63 <- next[0] (wave_rol:1, then wave_shl:1).
+__device__ __forceinline__ int32_t dpp_lower_across(int32_t v, int32_t prev) {
+  const int32_t u = __builtin_amdgcn_update_dpp(0, prev, 0x13C, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(u, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int32_t dpp_upper_across(int32_t v, int32_t next) {
+  const int32_t u = __builtin_amdgcn_update_dpp(0, next, 0x134, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(u, v, 0x130, 0xf, 0xf, false);
+}
 
 // Set_Right_Delta / Set_Left_Delta over the code log of wave_ped_reg: cell (k, d) holds
 // (r << 2 | code), r = max(1 + L[k-1][d], L[k-1][d-1], 1 + L[k-1][d+1]) and code = which
@@ -593,6 +604,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   const int32_t mbed = X.min_branch_end_dist;
   const double mbts = X.min_branch_tail_slope;
 #ifdef OVL_PROFILE
+  unsigned long long pc_a = 0, pc_b = 0, pc_cont = 0, pc_c = 0;
   unsigned long long pc_chunks = 0, pc_rest = 0, pc_rows = 0, pc_nch = 0, pc_slide = 0,
                      pc_recenter = 0;
   PROF_T(pt_begin);
@@ -667,16 +679,15 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     int32_t NR[J], LM[J];
     uint64_t actm[J];
     {
-      int32_t carry = -2;                      // row e-1 at diagonal B+64j-1
 #pragma unroll
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
         const int32_t d = B + 64 * j + (int32_t)lane;
         const int32_t p0 = R[j];
-        const int32_t nxt = (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
-        const int32_t pm = dpp_from_lower(p0, carry);
-        const int32_t pp = dpp_from_upper(p0, nxt);
-        carry = __builtin_amdgcn_readlane(p0, 63);
+        // row e-1 at d-1 and d+1 (diagonal B-1 and B+64J are outside the band: -2)
+        const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, R[j > 0 ? j - 1 : 0]);
+        const int32_t pp = (j + 1 < J) ? dpp_upper_across(p0, R[j + 1 < J ? j + 1 : j])
+                                       : dpp_from_upper(p0, -2);
         const int32_t r0 = 1 + p0, r2 = 1 + pp;
         const int32_t r = (pm > r0 ? pm : r0) > r2 ? (pm > r0 ? pm : r0) : r2;
         const bool act = (uint32_t)(d - left) <= span;
@@ -687,6 +698,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       }
     }
 
+    PROF_T(pt_a);
+    PROF_ADD(pc_a, pt_row, pt_a);
     // ---- B: first 32-base slide step of every lane, branch-free (the kernel is VALU
     // bound: no batching copies, one chunk at a time) ------------------------------------
     uint64_t need[J];
@@ -717,6 +730,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #ifdef OVL_PROFILE
     pc_nch += (jr + 1 > JU ? jr + 1 : JU);
 #endif
+    PROF_T(pt_b);
+    PROF_ADD(pc_b, pt_a, pt_b);
     // lanes that matched all 32 bases continue (the on-path diagonals): one loop over all
     // chunks so their LDS loads overlap
     {
@@ -741,6 +756,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       }
     }
 
+    PROF_T(pt_cont);
+    PROF_ADD(pc_cont, pt_b, pt_cont);
     // ---- C: end test (first d in order) and Edit_Match_Limit pruning -----------------
     uint64_t em[J], km[J], endany = 0;
 #pragma unroll
@@ -787,6 +804,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 
     PROF_T(pt_chunks);
     PROF_ADD(pc_chunks, pt_row, pt_chunks);
+    PROF_ADD(pc_c, pt_cont, pt_chunks);
 #ifdef OVL_PROFILE
     pc_rows++;
 #endif
@@ -881,6 +899,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     atomicAdd(&X.dbg[7], pt_tb1 - pt_tb0);
     atomicAdd(&X.dbg[10], pc_rest);
     atomicAdd(&X.dbg[11], pt_tb1 - pt_begin);
+    atomicAdd(&X.dbg[16], pc_a);
+    atomicAdd(&X.dbg[17], pc_b);
+    atomicAdd(&X.dbg[18], pc_cont);
+    atomicAdd(&X.dbg[19], pc_c);
     (void)pc_recenter;
   }
 #endif
