@@ -485,7 +485,18 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   F.max_distinct = misc.p + 2;
   F.cb_bits = cb;
   F.fb_bits = fb;
-  hipLaunchKernelGGL(k_fine, dim3(ncb), dim3(OVL_FINE_WAVES * 64), 0, s, F);
+  {
+    // per-wave sort buffer: twice the mean fine bucket, power of 2, 64..1024 records
+    uint64_t mean = per_cb / nfb + 1;
+    uint32_t cap = 64;
+    while (cap < 2 * mean && cap < 1024) cap <<= 1;
+    F.cap = cap;
+  }
+  const size_t fine_lds = 2ull * OVL_FINE_WAVES * F.cap * 8 + 2ull * nfb * 4;
+  if (fine_lds > 65536)
+    HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_fine),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)fine_lds));
+  hipLaunchKernelGGL(k_fine, dim3(ncb), dim3(OVL_FINE_WAVES * 64), fine_lds, s, F);
   HIPC(hipGetLastError());
   uint32_t hm[4];
   HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));

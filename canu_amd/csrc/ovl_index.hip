@@ -196,7 +196,6 @@ __device__ void wave_bitonic(uint64_t *sM, uint64_t *sP, uint32_t n2, uint32_t l
 }
 
 #define OVL_FINE_WAVES  8
-#define OVL_FINE_CAP    1024      // records a wave sorts in LDS (16 KB)
 #define OVL_FB_MAX      4096
 
 struct FineArgs {
@@ -208,16 +207,20 @@ struct FineArgs {
   uint32_t *big_list, *big_n;    // fine buckets too large for LDS
   uint32_t *max_distinct;
   uint32_t cb_bits, fb_bits;
+  uint32_t cap;                  // records a wave sorts in LDS (power of 2); larger fine
+                                 // buckets go to k_fine_big
 };
 
 __global__ void __launch_bounds__(OVL_FINE_WAVES * 64)
 k_fine(FineArgs A) {
-  __shared__ uint32_t h[OVL_FB_MAX];
-  __shared__ uint32_t cur[OVL_FB_MAX];
-  __shared__ uint64_t sM[OVL_FINE_WAVES][OVL_FINE_CAP];
-  __shared__ uint64_t sP[OVL_FINE_WAVES][OVL_FINE_CAP];
-  uint32_t cb = blockIdx.x;
+  // dynamic LDS sized to the fine buckets (2^fb bins, cap records per wave) so that
+  // several blocks share a CU: [sM: 8 x cap u64][sP: 8 x cap u64][h: nf u32][cur: nf u32]
+  extern __shared__ uint64_t s_fine[];
   uint32_t nf = 1u << A.fb_bits;
+  const uint32_t cap = A.cap;
+  uint32_t *h = (uint32_t *)(s_fine + 2 * OVL_FINE_WAVES * cap);
+  uint32_t *cur = h + nf;
+  uint32_t cb = blockIdx.x;
   uint32_t n = A.ccnt[cb], s0 = A.cstart[cb];
   uint32_t shift = 64 - A.cb_bits - A.fb_bits;
   for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) h[i] = 0;
@@ -246,12 +249,12 @@ k_fine(FineArgs A) {
   __syncthreads();
 
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint64_t *wM = sM[wave], *wP = sP[wave];
+  uint64_t *wM = s_fine + (size_t)wave * cap, *wP = s_fine + (size_t)(OVL_FINE_WAVES + wave) * cap;
   for (uint32_t f = wave; f < nf; f += OVL_FINE_WAVES) {
     uint32_t fn = h[f];
     if (fn == 0) continue;
     uint32_t fs = s0 + cur[f] - fn;              // cur[] now holds the fine bucket end
-    if (fn > OVL_FINE_CAP) {
+    if (fn > cap) {
       if (lane == 0) {
         uint32_t j = atomicAdd(A.big_n, 1u);
         A.big_list[2 * j] = fs;
