@@ -49,13 +49,20 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (1-GPU box): CANU_DEVICE pins every rank to one device,
+    # CANU_DIST_BACKEND=gloo replaces RCCL; the driver's multi-GPU runs use neither
+    local = int(os.environ.get("CANU_DEVICE", local))
+    backend = os.environ.get("CANU_DIST_BACKEND", "nccl")
 
     import torch
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from canu_amd.synth import synth_reads, random_genome
     from canu_amd.overlap_in_core import OicParameters, OverlapInCore
@@ -114,8 +121,9 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     st = oic.stats()
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    nr = torch.tensor([nrec], dtype=torch.int64, device=dev)
+    red = dev if backend == "nccl" else torch.device("cpu")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=red)
+    nr = torch.tensor([nrec], dtype=torch.int64, device=red)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(nr, op=dist.ReduceOp.SUM)

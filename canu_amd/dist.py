@@ -33,6 +33,18 @@ def query_shards(n: int, world: int, first: int = 1) -> list[tuple[int, int]]:
     return out
 
 
+def _all_gather(dist, out_list, t):
+    """all_gather that also works on a CPU-only backend (gloo) with device tensors: those
+    are staged through host memory (rehearsals only; RCCL gathers in HBM)."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        host = [o.cpu() for o in out_list]
+        dist.all_gather(host, t.cpu())
+        for o, h in zip(out_list, host):
+            o.copy_(h)
+    else:
+        dist.all_gather(out_list, t)
+
+
 def gather_read_store(bases_local, lengths_local: np.ndarray, dist, device):
     """All-gather every rank's slice of the read store (rank order = read order).
 
@@ -45,19 +57,19 @@ def gather_read_store(bases_local, lengths_local: np.ndarray, dist, device):
     n_l = torch.tensor([lengths_local.shape[0]], device=device, dtype=torch.int64)
     all_nb = [torch.zeros_like(n_b) for _ in range(world)]
     all_nl = [torch.zeros_like(n_l) for _ in range(world)]
-    dist.all_gather(all_nb, n_b)
-    dist.all_gather(all_nl, n_l)
+    _all_gather(dist, all_nb, n_b)
+    _all_gather(dist, all_nl, n_l)
     nbs = [int(x.item()) for x in all_nb]
     nls = [int(x.item()) for x in all_nl]
     buf = torch.zeros(max(nbs), dtype=torch.uint8, device=device)
     buf[:bases_local.numel()] = bases_local
     got = [torch.empty(max(nbs), dtype=torch.uint8, device=device) for _ in range(world)]
-    dist.all_gather(got, buf)
+    _all_gather(dist, got, buf)
     bases = torch.cat([g[:k] for g, k in zip(got, nbs)])
     lb = torch.zeros(max(nls), dtype=torch.int64, device=device)
     lb[:lengths_local.shape[0]] = torch.from_numpy(lengths_local.astype(np.int64)).to(device)
     gl = [torch.empty(max(nls), dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(gl, lb)
+    _all_gather(dist, gl, lb)
     lengths = torch.cat([g[:k] for g, k in zip(gl, nls)]).cpu().numpy().astype(np.uint32)
     return bases, lengths
 
@@ -78,5 +90,5 @@ def all_gather_rows(local, n: int, dist):
     pad = torch.zeros((rmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
     got = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(got, pad)
+    _all_gather(dist, got, pad)
     return torch.cat([g[:hi - lo] for g, (lo, hi) in zip(got, sl)])
