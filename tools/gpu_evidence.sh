@@ -1,3 +1,4 @@
+# Round evidence: full GPU test suite, rocprofv3 passes (kernel stats, FETCH/WRITE, issue) and the bench line.
 # full evidence pass for the current tree (round 1, tag r01d)
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,3 +1,4 @@
+# MHAP GPU tests, bench_mhap.py at configs[3] and its rocprofv3 kernel stats.
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_mhap.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/mhap_gpu.log 2>&1; rc=$?

@@ -1,3 +1,4 @@
+# GPU parity + golden tests, then 10k- and 50k-read bench timings.
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_golden.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/par.log 2>&1; rc=$?
