@@ -144,6 +144,8 @@ struct ovl_ctx {
   std::vector<uint64_t> h_wofs;
   DBuf<uint64_t> d_fwd, d_rc, d_wofs;
   DBuf<uint32_t> d_fwdN, d_rcNul, d_len, d_flags, d_rcFirstNul;
+  DBuf<uint8_t> d_qual;          // -w only: read r base i at wofs[r] * 32 + i
+  bool have_qual = false;
   uint32_t max_len = 0;
 
   // skip k-mers (both strands, deduplicated codes)
@@ -185,6 +187,7 @@ struct ovl_ctx {
     R.len = d_len.p;
     R.flags = d_flags.p;
     R.rcFirstNul = d_rcFirstNul.p;
+    R.qual = have_qual ? d_qual.p : nullptr;
     R.first_iid = first_iid;
     R.nreads = nreads;
     return R;
@@ -224,8 +227,6 @@ int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
   if (p->kmer_len > 31) return fail(OVL_ERR_BAD_PARAM, "kmer length must be <= 31");
   if (!(p->max_erate > 0.0) || p->max_erate >= 1.0)
     return fail(OVL_ERR_BAD_PARAM, "maxErate out of range");
-  if (p->use_window_filter && p->max_erate <= 0.06)
-    return fail(OVL_ERR_UNSUPPORTED, "-w (window filter) is not implemented on the GPU path");
   if (p->frag_olap_limit != UINT64_MAX)
     return fail(OVL_ERR_UNSUPPORTED, "-l (frag olap limit) is not implemented on the GPU path");
   int ndev = 0;
@@ -328,19 +329,46 @@ static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const ui
   return OVL_OK;
 }
 
+// Qualities (-w) into the packed layout: read r base i at wofs[r] * 32 + i.
+__global__ void k_pack_quals(const uint8_t *q, const uint64_t *offs, const uint32_t *lens,
+                             const uint64_t *wofs, uint8_t *out) {
+  const uint32_t r = blockIdx.x;
+  const uint64_t o = offs[r], w = wofs[r] * 32;
+  for (uint32_t i = threadIdx.x; i < lens[r]; i += blockDim.x) out[w + i] = q[o + i];
+}
+
+static int load_quals(ovl_ctx *c, const uint8_t *d_quals, const uint64_t *d_offsets) {
+  c->have_qual = false;
+  if (!d_quals) return OVL_OK;
+  uint64_t words = c->h_wofs.empty() ? 0 : c->h_wofs.back() + (c->h_len.back() + 31) / 32 + 1;
+  if (c->d_qual.alloc(words * 32 + 64)) return fail(OVL_ERR_OOM, "qualities");
+  hipLaunchKernelGGL(k_pack_quals, dim3(c->nreads), dim3(256), 0, c->stream, d_quals, d_offsets,
+                     c->d_len.p, c->d_wofs.p, c->d_qual.p);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  c->have_qual = true;
+  return OVL_OK;
+}
+
 int ovl_load_reads(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const uint8_t *bases,
                    const uint64_t *offsets, const uint32_t *lengths, const uint8_t *quals) {
   if (!c) return fail(OVL_ERR_STATE, "null context");
-  (void)quals;
   HIPC(hipSetDevice(c->device));
   uint64_t total = 0;
   for (uint32_t i = 0; i < nreads; i++) total = std::max(total, offsets[i] + lengths[i]);
-  DBuf<uint8_t> db;
+  DBuf<uint8_t> db, dq;
   DBuf<uint64_t> doff;
   if (db.alloc(total + 64) || doff.alloc(nreads + 1)) return fail(OVL_ERR_OOM, "staging");
   HIPC(hipMemcpyAsync(db.p, bases, total, hipMemcpyHostToDevice, c->stream));
   HIPC(hipMemcpyAsync(doff.p, offsets, 8ull * nreads, hipMemcpyHostToDevice, c->stream));
   int rc = load_common(c, first_iid, nreads, db.p, doff.p, lengths);
+  if (rc == OVL_OK && quals) {
+    if (dq.alloc(total + 64)) return fail(OVL_ERR_OOM, "quality staging");
+    HIPC(hipMemcpyAsync(dq.p, quals, total, hipMemcpyHostToDevice, c->stream));
+    rc = load_quals(c, dq.p, doff.p);
+  } else if (rc == OVL_OK) {
+    c->have_qual = false;
+  }
   (void)hipStreamSynchronize(c->stream);
   return rc;
 }
@@ -349,9 +377,10 @@ int ovl_load_reads_device(ovl_ctx *c, uint32_t first_iid, uint32_t nreads,
                           const uint8_t *d_bases, const uint64_t *d_offsets,
                           const uint32_t *h_lengths, const uint8_t *d_quals) {
   if (!c) return fail(OVL_ERR_STATE, "null context");
-  (void)d_quals;
   HIPC(hipSetDevice(c->device));
-  return load_common(c, first_iid, nreads, d_bases, d_offsets, h_lengths);
+  int rc = load_common(c, first_iid, nreads, d_bases, d_offsets, h_lengths);
+  if (rc == OVL_OK) rc = load_quals(c, d_quals, d_offsets);
+  return rc;
 }
 
 static uint64_t kmer_code(const char *s, uint32_t k, bool *ok) {
@@ -614,13 +643,19 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   auto &d_pnodes = c->fb.pnodes;
   auto &d_pairs = c->fb.pairs;
   auto &d_stats = c->fb.stats;
-  if (d_ctr.alloc(16) || d_stats.alloc(8)) return fail(OVL_ERR_OOM, "counters");
-  HIPC(hipMemsetAsync(d_stats.p, 0, 64, s));
+  const bool window = c->P.use_window_filter && c->P.max_erate <= 0.06;
+  if (window && !c->have_qual)
+    return fail(OVL_ERR_BAD_PARAM, "-w (window filter) needs the reads' qualities");
+  if (d_ctr.alloc(16) || d_stats.alloc(16)) return fail(OVL_ERR_OOM, "counters");
+  HIPC(hipMemsetAsync(d_stats.p, 0, 128, s));
 
   // extension scratch per wave
   int32_t e_cap = c->h_error_bound[std::min<uint32_t>(c->max_len, AS_MAX_READLEN)] + 2;
   // generic kernel: band-compact rows, <= (e_cap+2)^2; staged kernel: 64*OVL_RJ cells per row
-  uint64_t rows_cap = std::max<uint64_t>((uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64,
+  // (the window filter reuses a wave's row scratch: 3 segment arrays + column prefix sums)
+  uint64_t rows_cap = std::max<uint64_t>(std::max<uint64_t>(
+                                             (uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64,
+                                             window ? 3ull * (e_cap + 9) + 2ull * c->max_len + 64 : 0),
                                          (uint64_t)(e_cap + 2) * 64 * OVL_RJ);
   uint64_t per_wave = rows_cap * 4 + 16ull * (e_cap + 2) + 16ull * (e_cap + 8);
   uint32_t ext_waves = 24u * c->n_cu;
@@ -631,7 +666,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   auto &d_deltas = c->fb.deltas;
   if (d_rows.alloc(rows_cap * ext_waves) ||
       d_rowdir.alloc((size_t)4 * (e_cap + 2) * ext_waves) ||
-      d_deltas.alloc((size_t)4 * (e_cap + 8) * ext_waves))
+      d_deltas.alloc((size_t)7 * (e_cap + 8) * ext_waves))
     return fail(OVL_ERR_OOM, "extension scratch");
   // LDS per extension wave (ovl_extend.hip k_extend).  Generic kernel: two row buffers, the
   // traceback window and the delta cache.  Staged kernel: both strands and a scratch.
@@ -812,6 +847,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.nout = d_ctr.p + 6;
     EA.out_cap = (uint32_t)std::min<uint64_t>(c->d_out.n, 0xFFFFFFF0ull);
     EA.stats = d_stats.p;
+    EA.window = window ? 1 : 0;
     EA.overflow = d_ctr.p + 7;
     EA.dbg = nullptr;
     if (getenv("OVL_DEBUG")) {
@@ -869,8 +905,8 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     c->nout = hc[6];
     u0 += nc;
   }
-  unsigned long long hs[8];
-  HIPC(hipMemcpy(hs, d_stats.p, 64, hipMemcpyDeviceToHost));
+  unsigned long long hs[16];
+  HIPC(hipMemcpy(hs, d_stats.p, 128, hipMemcpyDeviceToHost));
   if (dbg_ptr_for_print) {
     unsigned long long dd[32];
     (void)hipMemcpy(dd, dbg_ptr_for_print, 256, hipMemcpyDeviceToHost);
@@ -890,6 +926,8 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   c->stats.contained_overlaps = hs[5];
   c->stats.dovetail_overlaps = hs[6];
   c->stats.seed_hits = hs[7];
+  c->stats.bad_short_window = hs[8];
+  c->stats.bad_long_window = hs[9];
   c->stats.pairs = npairs_tot;
   c->stats.ms_seed = ms_probe + ms_chain;
   c->stats.ms_extend = ms_ext;

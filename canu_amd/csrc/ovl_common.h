@@ -27,6 +27,7 @@ struct ReadsDev {
   const uint32_t *len;      // read lengths
   const uint32_t *flags;    // bit0: read has an 'n'
   const uint32_t *rcFirstNul;  // first rc NUL at position >= k (len if none): ends the scan
+  const uint8_t  *qual;     // quality values (-w only): read r base i at wofs[r]*32 + i
   uint32_t        first_iid;
   uint32_t        nreads;
 };

@@ -50,6 +50,8 @@ struct ExtendArgs {
   uint32_t *nout;
   uint32_t out_cap;
   unsigned long long *stats;    // 0 without 1 with 2 skipped 3 multi 4 total 5 contained 6 dovetail
+                                // (7 seed hits: k_chain) 8 bad short window 9 bad long window
+  int32_t window;               // -w: Use_Window_Filter
   uint32_t *overflow;
   unsigned long long *dbg;      // optional counters (null: off)
 };
@@ -1134,9 +1136,11 @@ __device__ Rec output_partial(uint32_t s_id, uint32_t t_id, int dir, const OlapI
 #define SHIFT_SLACK 1
 
 // Add_Overlap (Process_String_Overlaps.C:222); wave-uniform
-__device__ void add_overlap(const ExtendArgs &X, int32_t s_lo, int32_t s_hi, int32_t t_lo,
-                            int32_t t_hi, double qual, int32_t delta_ct, OlapInfo *ol,
-                            int32_t &ct) {
+// Returns the entry whose alignment was replaced by this one (new entry or better quality),
+// i.e. whose Left_Delta the reference memcpy()s, or -1.
+__device__ int32_t add_overlap(const ExtendArgs &X, int32_t s_lo, int32_t s_hi, int32_t t_lo,
+                               int32_t t_hi, double qual, int32_t delta_ct, OlapInfo *ol,
+                               int32_t &ct) {
   if (!X.partial) {
     int32_t new_diag = t_lo - s_lo;
     for (int32_t i = 0; i < ct; i++) {
@@ -1155,12 +1159,13 @@ __device__ void add_overlap(const ExtendArgs &X, int32_t s_lo, int32_t s_hi, int
           ol[i].s_lo = s_lo; ol[i].s_hi = s_hi; ol[i].t_lo = t_lo; ol[i].t_hi = t_hi;
           ol[i].quality = qual;
           ol[i].delta_ct = delta_ct;
+          return i;
         }
-        return;
+        return -1;
       }
     }
   }
-  if (ct >= MAX_DISTINCT_OLAPS) return;
+  if (ct >= MAX_DISTINCT_OLAPS) return -1;
   OlapInfo &o = ol[ct];
   o.s_lo = o.slb = s_lo;
   o.s_hi = o.srb = s_hi;
@@ -1170,6 +1175,107 @@ __device__ void add_overlap(const ExtendArgs &X, int32_t s_lo, int32_t s_hi, int
   o.delta_ct = delta_ct;
   o.min_diag = o.max_diag = t_lo - s_lo;
   ct++;
+  return ct - 1;
+}
+
+// ---- the window filter (-w, Process_String_Overlaps.C:562-621) ------------------------
+#define OVL_QUALITY_CUTOFF 20                  // overlapInCore.H:190
+#define OVL_BAD_WINDOW_LEN 50                  // overlapInCore.H:80
+#define OVL_BAD_WINDOW_VALUE (8 * OVL_QUALITY_CUTOFF)
+
+struct BaseAt {
+  uint32_t code;
+  bool wild;     // 'n' (forward strands)
+  bool nul;      // NUL (reverse complement of an 'n')
+};
+__device__ __forceinline__ BaseAt base_at(const Strand &s, int32_t p) {
+  BaseAt b;
+  b.code = (uint32_t)(s.w[p >> 5] >> (2 * (p & 31))) & 3u;
+  b.wild = s.ex_wild && ((s.ex_wild[p >> 5] >> (p & 31)) & 1u);
+  b.nul = s.ex_nul && ((s.ex_nul[p >> 5] >> (p & 31)) & 1u);
+  return b;
+}
+
+// One olap's quality-difference string q (one value per alignment column: 0 on a match or
+// an 'n', else min(quality, quality, cutoff); an indel column takes the quality of the
+// base it skips) and Has_Bad_Window (:365) over it, lane-parallel: the columns are
+// generated from the delta by segment (prefix scans), their prefix sums go to scr, and
+// every window is one subtraction.  Returns 0 (kept), 1 (bad short window), 2 (bad long).
+__device__ int32_t window_reject(const ExtendArgs &X, const Unit &un, uint32_t tgt,
+                                 const OlapInfo &o, const int32_t *od, int32_t *scr,
+                                 uint32_t lane) {
+  typedef __attribute__((address_space(1))) int32_t g_i32;
+  g_i32 *segC = (g_i32 *)scr, *segI = segC + (o.delta_ct + 1), *segJ = segI + (o.delta_ct + 1);
+  g_i32 *P = segJ + (o.delta_ct + 1);
+  const Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
+  const Strand T = strand_fwd(X.R, tgt);
+  const uint8_t *sq = X.R.qual + X.R.wofs[un.r] * 32;
+  const uint8_t *tq = X.R.qual + X.R.wofs[tgt] * 32;
+  const int32_t SL = S.len;
+  const int32_t dct = o.delta_ct;
+  int32_t cc = 0, ci = o.s_lo, cj = o.t_lo;
+  for (int32_t k0 = 0; k0 < dct; k0 += 64) {
+    const int32_t k = k0 + (int32_t)lane;
+    const bool in = k < dct;
+    const int32_t v = in ? od[k] : 0;
+    const int32_t a = v < 0 ? -v : v;
+    const int32_t ic = in ? a : 0;
+    const int32_t ii = in ? a - 1 + (v > 0 ? 1 : 0) : 0;
+    const int32_t ij = in ? a - 1 + (v < 0 ? 1 : 0) : 0;
+    const int32_t sc = wave_incl_scan(ic), si = wave_incl_scan(ii), sj = wave_incl_scan(ij);
+    if (in) { segC[k] = cc + sc - ic; segI[k] = ci + si - ii; segJ[k] = cj + sj - ij; }
+    cc += __builtin_amdgcn_readlane(sc, 63);
+    ci += __builtin_amdgcn_readlane(si, 63);
+    cj += __builtin_amdgcn_readlane(sj, 63);
+  }
+  if (lane == 0) { segC[dct] = cc; segI[dct] = ci; segJ[dct] = cj; }
+  const int32_t tail = o.s_hi - ci + 1;
+  const int32_t n = cc + (tail > 0 ? tail : 0);
+  if (n < OVL_BAD_WINDOW_LEN) return 0;
+  vm_sync();
+  int32_t carry = 0;
+  if (lane == 0) P[0] = 0;
+  for (int32_t c0 = 0; c0 < n; c0 += 64) {
+    const int32_t c = c0 + (int32_t)lane;
+    int32_t q = 0;
+    if (c < n) {
+      int32_t lo = 0, hi = dct;               // last segment with segC <= c
+      while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        if (segC[mid] <= c) lo = mid; else hi = mid - 1;
+      }
+      const int32_t u = c - segC[lo];
+      const int32_t i = segI[lo] + u, j = segJ[lo] + u;
+      int32_t dv = 0;
+      if (lo < dct && u == (od[lo] < 0 ? -od[lo] : od[lo]) - 1) {
+        dv = od[lo] > 0 ? (int32_t)sq[un.dir ? SL - 1 - i : i] : (int32_t)tq[j];
+      } else {
+        const BaseAt bs = base_at(S, i), bt = base_at(T, j);
+        const bool same = !bs.wild && !bt.wild && !bs.nul && bs.code == bt.code;
+        if (!(same || bs.wild || bt.wild)) {
+          const int32_t qs = sq[un.dir ? SL - 1 - i : i], qt = tq[j];
+          dv = qs < qt ? qs : qt;
+        }
+      }
+      q = dv < OVL_QUALITY_CUTOFF ? dv : OVL_QUALITY_CUTOFF;
+    }
+    const int32_t sc = wave_incl_scan(q);
+    if (c < n) P[c + 1] = carry + sc;
+    carry += __builtin_amdgcn_readlane(sc, 63);
+  }
+  vm_sync();
+  bool bad = false;
+  for (int32_t p0 = 0; p0 + OVL_BAD_WINDOW_LEN <= n; p0 += 64) {
+    const int32_t p = p0 + (int32_t)lane;
+    if (p + OVL_BAD_WINDOW_LEN <= n && P[p + OVL_BAD_WINDOW_LEN] - P[p] >= OVL_BAD_WINDOW_VALUE)
+      bad = true;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad)) return 1;
+  for (int32_t p0 = 0; p0 + 100 <= n; p0 += 64) {
+    const int32_t p = p0 + (int32_t)lane;
+    if (p + 100 <= n && P[p + 100] - P[p] >= 240) bad = true;
+  }
+  return __builtin_amdgcn_ballot_w64(bad) ? 2 : 0;
 }
 
 __device__ bool lies_on_alignment(int32_t start, int32_t offset, int32_t s_lo, int32_t t_lo,
@@ -1266,8 +1372,14 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
       if (1 + S_Hi - S_Lo >= X.min_olap_len && 1 + T_Hi - T_Lo >= X.min_olap_len) {
         int32_t olap_len = 1 + ((S_Hi - S_Lo) < (T_Hi - T_Lo) ? (S_Hi - S_Lo) : (T_Hi - T_Lo));
         double quality = (double)eo.Errors / olap_len;
-        if (eo.Errors <= X.error_bound[olap_len])
-          add_overlap(X, S_Lo, S_Hi, T_Lo, T_Hi, quality, ld_len, ol, ct);
+        if (eo.Errors <= X.error_bound[olap_len]) {
+          const int32_t slot = add_overlap(X, S_Lo, S_Hi, T_Lo, T_Hi, quality, ld_len, ol, ct);
+          if (X.window && slot >= 0) {               // memcpy(olap[i].delta, Left_Delta)
+            int32_t *od = LD + (2 + slot) * (X.e_cap + 8);
+            for (int32_t i = lane; i < ld_len; i += 64) od[i] = LD[i];
+            vm_sync();
+          }
+        }
       }
     }
     if (consistent) break;
@@ -1385,6 +1497,11 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     }
     for (int32_t i = 0; i < ct; i++) {
       if (del[i]) continue;
+      if (X.window) {
+        const int32_t rej = window_reject(X, un, P.tgt, ol[i], LD + (2 + i) * (X.e_cap + 8),
+                                          WM.rows, lane);
+        if (rej) { st[6 + rej]++; continue; }      // Bad_Short / Bad_Long_Window_Ct
+      }
       Rec rec;
       int32_t bhg = 0;
       if (X.partial) rec = output_partial(S_ID, T_ID, un.dir, ol[i], S_Len, t_len);
@@ -1469,10 +1586,11 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
     WM.ldc = WM.tbw + TB_ROWS * TB_W;
     WM.ldcap = OVL_LDCAP;
   }
-  int32_t *stk = X.deltas + (size_t)gw * 4 * (X.e_cap + 8);
+  // per wave: stack | Right_Delta | Left_Delta | spare | the three olaps' delta copies (-w)
+  int32_t *stk = X.deltas + (size_t)gw * 7 * (X.e_cap + 8);
   int32_t *RD = stk + (X.e_cap + 8);
   int32_t *LD = RD + (X.e_cap + 8);
-  unsigned long long st[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   for (;;) {
     uint32_t pi = 0;
@@ -1511,8 +1629,8 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
     lds_sync();
   }
   if (lane == 0)
-    for (int i = 0; i < 7; i++)
-      if (st[i]) atomicAdd(&X.stats[i], st[i]);
+    for (int i = 0; i < 9; i++)
+      if (st[i]) atomicAdd(&X.stats[i < 7 ? i : i + 1], st[i]);
 }
 
 }  // namespace ovl

@@ -117,16 +117,15 @@ inline int write_ovb_file(const ovl_record *r, uint64_t n, const char *path, boo
 inline int write_stats_file(const ovl_stats &s, const char *path) {
   FILE *F = fopen(path, "w");
   if (!F) return -1;
-  // F_S64 = "%" PRId64 (AS_global.H:180); the window filter is not built, so its two
-  // rejection counters are 0
+  // F_S64 = "%" PRId64 (AS_global.H:180)
   fprintf(F, " Kmer hits without olaps = %" PRId64 "\n", (int64_t)s.kmer_hits_without_olap);
   fprintf(F, "    Kmer hits with olaps = %" PRId64 "\n", (int64_t)s.kmer_hits_with_olap);
   fprintf(F, "  Multiple overlaps/pair = %" PRId64 "\n", (int64_t)s.multi_overlaps);
   fprintf(F, " Total overlaps produced = %" PRId64 "\n", (int64_t)s.total_overlaps);
   fprintf(F, "      Contained overlaps = %" PRId64 "\n", (int64_t)s.contained_overlaps);
   fprintf(F, "       Dovetail overlaps = %" PRId64 "\n", (int64_t)s.dovetail_overlaps);
-  fprintf(F, "Rejected by short window = %" PRId64 "\n", (int64_t)0);
-  fprintf(F, " Rejected by long window = %" PRId64 "\n", (int64_t)0);
+  fprintf(F, "Rejected by short window = %" PRId64 "\n", (int64_t)s.bad_short_window);
+  fprintf(F, " Rejected by long window = %" PRId64 "\n", (int64_t)s.bad_long_window);
   return fclose(F) == 0 ? 0 : -1;
 }
 

@@ -53,7 +53,8 @@ class _Stats(ctypes.Structure):
         [("ms_index", ctypes.c_double), ("ms_seed", ctypes.c_double),
          ("ms_extend", ctypes.c_double), ("ms_probe_kernel", ctypes.c_double),
          ("probe_bytes", ctypes.c_uint64), ("probe_launches", ctypes.c_uint32),
-         ("extend_launches", ctypes.c_uint32)]
+         ("extend_launches", ctypes.c_uint32), ("bad_short_window", ctypes.c_uint64),
+         ("bad_long_window", ctypes.c_uint64)]
 
 
 # Every symbol include/canu_ovl.h declares (tests check the library exports them all).
@@ -254,9 +255,11 @@ class OverlapInCore:
         bases = np.ascontiguousarray(rs.bases, dtype=np.uint8)
         offs = np.ascontiguousarray(rs.offsets, dtype=np.uint64)
         lens = np.ascontiguousarray(rs.lengths, dtype=np.uint32)
+        quals = None if rs.quals is None else np.ascontiguousarray(rs.quals, dtype=np.uint8)
         self._check(self.lib.ovl_load_reads(self.ctx, rs.first_iid, rs.nreads,
                                             bases.ctypes.data, offs.ctypes.data,
-                                            lens.ctypes.data, None))
+                                            lens.ctypes.data,
+                                            None if quals is None else quals.ctypes.data))
         self.first_iid = rs.first_iid
         self.nreads = rs.nreads
 

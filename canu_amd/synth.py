@@ -89,7 +89,7 @@ def _mutate(rng: np.random.Generator, seg: np.ndarray, out_len: int, error_rate:
 def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
                 seed: int = 1, sub_frac: float = 0.4, ins_frac: float = 0.3,
                 len_jitter: float = 0.0, n_rate: float = 0.0, n_repeats: int = 0,
-                repeat_len: int = 0, with_quals: bool = False,
+                repeat_len: int = 0, with_quals: bool = False, bursts: int = 0,
                 genome: np.ndarray | None = None, read_range: tuple[int, int] | None = None
                 ) -> ReadSet:
     """Sample `n_reads` reads of about `read_len` bases from a random genome.
@@ -115,6 +115,16 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
         seg = genome[start:start + span]
         rd = _mutate(rng, seg, L, error_rate, sub_frac, ins_frac)
         starts[i - lo] = start
+        if bursts:
+            # low-quality stretches: 60 bases with 30 % substitutions (window-filter cases)
+            brng = np.random.default_rng([seed, i, 11])
+            rd = rd.copy()
+            for _ in range(bursts):
+                b0 = int(brng.integers(0, max(1, rd.shape[0] - 60)))
+                sel = b0 + np.nonzero(brng.random(60) < 0.3)[0]
+                sel = sel[sel < rd.shape[0]]
+                idx = np.searchsorted(_ACGT, rd[sel])
+                rd[sel] = _ACGT[(idx + brng.integers(1, 4, size=sel.size)) % 4]
         if rng.random() < 0.5:
             rd = _COMP[rd[::-1]]
             strands[i - lo] = 1

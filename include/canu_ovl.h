@@ -98,7 +98,8 @@ int         ovl_abi_version(void);
 
 /* Load reads first_iid .. first_iid+nreads-1 (gkStore IDs, 1-based in canu).
  *   bases    concatenated sequence bytes, read i at bases[offsets[i]] for lengths[i] bytes
- *   quals    same layout, or NULL (required only when use_window_filter is set)
+ *   quals    same layout, or NULL (required only when use_window_filter is set); quality
+ *            values as gkStore hands them out (numeric QVs)
  * The data are copied to device memory (2-bit packed + exception masks) once; every
  * later call works on the resident copy. */
 int         ovl_load_reads(ovl_ctx *ctx, uint32_t first_iid, uint32_t nreads,
@@ -148,6 +149,8 @@ typedef struct {
   uint64_t probe_bytes;            /* algorithmic bytes of the hash-probe kernel       */
   uint32_t probe_launches;         /* k_probe launches of the last find                */
   uint32_t extend_launches;        /* k_extend launches (staged + generic)             */
+  uint64_t bad_short_window;       /* -w rejections, Bad_Short_Window_Ct               */
+  uint64_t bad_long_window;        /* -w rejections, Bad_Long_Window_Ct                */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

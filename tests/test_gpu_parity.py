@@ -102,3 +102,23 @@ def test_pacbio_ecoli_scale(built):
     # full read count over a scaled genome so the oracle finishes in seconds
     rs = synth_reads(1000, 3000, 300_000, 0.02, seed=10)
     _check(rs, _params(minlen=500))
+
+
+@pytest.mark.parametrize("case", ["plain", "partial", "multi_ns"])
+def test_window_filter(built, case):
+    """-w: quality-difference windows along each overlap's alignment (Process_String_
+    Overlaps.C:562-621), on reads with low-quality error bursts so that many overlaps are
+    rejected; both orientations, 'n' bases (forward wildcards, reverse-complement NULs)."""
+    kw = dict(n_reads=90, read_len=2500, genome_len=20_000, error_rate=0.015, seed=51,
+              with_quals=True, bursts=1)
+    P = dict(k=20, Use_Window_Filter=True)
+    if case == "partial":
+        P["Doing_Partial_Overlaps"] = True
+    if case == "multi_ns":
+        kw.update(n_rate=0.003, len_jitter=0.4, bursts=2, seed=52)
+        P["Unique_Olap_Per_Pair"] = False
+    rs = synth_reads(**kw)
+    got = _check(rs, _params(**P))
+    nowin = oracle.run_oracle(rs, _params(**{k: v for k, v in P.items()
+                                              if k != "Use_Window_Filter"}).as_dict())
+    assert 0 < got.shape[0] < nowin.shape[0]      # the filter did reject overlaps

@@ -25,7 +25,8 @@ def load_golden(name):
     lengths = z["lengths"].astype(np.uint32)
     offsets = np.zeros(lengths.shape[0], dtype=np.uint64)
     offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
-    rs = ReadSet(bases=z["bases"], offsets=offsets, lengths=lengths,
+    quals = z["quals"] if "quals" in z.files and z["quals"].size else None
+    rs = ReadSet(bases=z["bases"], offsets=offsets, lengths=lengths, quals=quals,
                  first_iid=int(z["first_iid"]))
     rec = np.zeros(z["a"].shape[0], dtype=oracle.RECORD_DTYPE)
     for f in ("a", "b", "w0", "w1"):

@@ -8,6 +8,7 @@ output records and counters.  tests/test_golden.py checks the C restatement (ora
 on the GPU box, the HIP path against them -- /root/reference is not needed there.
 
     python tools/make_golden.py            # needs oracle/_ref/oic_ref (built by `make -C oracle`)
+    python tools/make_golden.py --only window   # (re)generate some cases only
 """
 from __future__ import annotations
 
@@ -48,15 +49,25 @@ CASES = {
     "no_hopeless": (dict(n_reads=40, read_len=2000, genome_len=12000, error_rate=0.02, seed=18),
                     dict(kmer_len=22, max_erate=0.06, min_olap_len=100, use_hopeless_check=0),
                     {}),
+    # -w: qualities + low-quality error bursts, so the window filter rejects overlaps
+    "window": (dict(n_reads=60, read_len=2500, genome_len=15000, error_rate=0.015, seed=41,
+                    with_quals=True, bursts=1),
+               dict(kmer_len=20, max_erate=0.06, min_olap_len=100, use_window_filter=1), {}),
 }
 
 
 def main() -> None:
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     if not oracle.reference_available():
         sys.exit("oracle/_ref/oic_ref is missing: run `make -C oracle` with /root/reference present")
     os.makedirs(OUT, exist_ok=True)
     index = {}
+    if only:
+        with open(os.path.join(OUT, "index.json")) as f:
+            index = json.load(f)
     for name, (rkw, pkw, extra) in CASES.items():
+        if only and name not in only:
+            continue
         rs = synth_reads(**rkw)
         p = oracle.default_params(**pkw)
         skip = None
@@ -77,6 +88,7 @@ def main() -> None:
             os.path.join(OUT, f"{name}.npz"),
             bases=rs.bases, lengths=rs.lengths, first_iid=np.uint32(rs.first_iid),
             skip=np.array([s.encode() for s in (skip or [])], dtype="S64"),
+            quals=(rs.quals if rs.quals is not None else np.zeros(0, np.uint8)),
             a=rec["a"], b=rec["b"], w0=rec["w0"], w1=rec["w1"])
         index[name] = {"params": {k: (v if k != "frag_olap_limit" else str(v))
                                   for k, v in p.items()},
