@@ -677,8 +677,16 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     return fail(OVL_ERR_UNSUPPORTED, "error limit %d needs more LDS than a CU has", e_cap);
   int32_t sw_words = (int32_t)((((uint64_t)c->max_len + 31) / 32 + 2) & ~1ull);
   size_t stg_lds_wave = 4ull * (4ull * sw_words + OVL_SCR);
-  const uint32_t stg_wpb = 8;                  // 512-thread blocks: one ML table per 8 waves
-  bool staged = stg_lds_wave * stg_wpb + ml_lds <= 64 * 1024;
+  // 512-thread blocks (one ML table per 8 waves) while they fit in 64 KB of LDS; longer
+  // reads take fewer waves per block and up to a CU's 160 KB (opt-in attribute below)
+  uint32_t stg_wpb = 8;
+  size_t stg_cap = 64 * 1024;
+  if (stg_lds_wave * 8 + ml_lds > stg_cap) {
+    stg_cap = 160 * 1024;
+    stg_wpb = (uint32_t)std::min<size_t>(8, (stg_cap - std::min(stg_cap, ml_lds)) / stg_lds_wave);
+  }
+  bool staged = stg_wpb >= 1 && stg_lds_wave * stg_wpb + ml_lds <= stg_cap;
+  if (!staged) stg_wpb = 1;
   // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the staged kernel's LDS so that at most that
   // many 512-thread blocks fit on a CU (occupancy studies); unset = natural occupancy
   size_t stg_lds = stg_lds_wave * stg_wpb + ml_lds;
@@ -688,6 +696,13 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   }
   ext_waves = (ext_waves / 8) * 8;
   if (staged) {
+    ext_waves = (ext_waves / stg_wpb) * stg_wpb;
+    if (stg_lds > 64 * 1024) {
+      HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_extend<true, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)stg_lds));
+      HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_extend<true, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)stg_lds));
+    }
     // persistent grid: as many 512-thread blocks as are resident at once (registers and
     // LDS), so no block starts only after the work queue has drained
     int bpc = 0;
@@ -863,6 +878,9 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     if (npairs) {
       size_t lds = gen_lds_wave * gen_wpb + ml_lds;
       const uint32_t ext_wpb = gen_wpb;
+      if (lds > 64 * 1024)
+        HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_extend<false, false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       if (staged) {
         // staged kernel for exception-free pairs; pairs touching an 'n' are deferred to
         // the generic kernel below

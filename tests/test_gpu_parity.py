@@ -122,3 +122,12 @@ def test_window_filter(built, case):
     nowin = oracle.run_oracle(rs, _params(**{k: v for k, v in P.items()
                                               if k != "Use_Window_Filter"}).as_dict())
     assert 0 < got.shape[0] < nowin.shape[0]      # the filter did reject overlaps
+
+
+@pytest.mark.parametrize("L", [24_000, 45_000])
+def test_long_reads(built, L):
+    """Reads past 16,384 bases (32-bit code log) and long enough that the staged kernel
+    takes fewer waves per block and more than 64 KB of LDS; ragged lengths."""
+    rs = synth_reads(16, L, int(16 * L / 6), 0.015, seed=61, len_jitter=0.3)
+    got = _check(rs, _params(minlen=500))
+    assert got.shape[0] > 10
