@@ -6,6 +6,7 @@
 //   k_probe -> k_chain -> k_extend
 // over (query, orientation) units.  There is no CPU fallback for any of it.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cerrno>
@@ -165,7 +166,8 @@ struct ovl_ctx {
     DBuf<Unit> units;
     DBuf<uint64_t> rbase;
     DBuf<Probe> probe;
-    DBuf<uint32_t> uhits, uflags, ctr, done, defer;
+    DBuf<uint32_t> uhits, uflags, ctr, done, defer, okey, oidx, okey2, oidx2;
+    DBuf<uint8_t> otmp;
     DBuf<Node> pool, pnodes;
     DBuf<PairRec> pairs;
     DBuf<unsigned long long> stats;
@@ -327,6 +329,16 @@ static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const ui
     return fail(OVL_ERR_BAD_INPUT,
                 "reads hold characters other than ACGTN; the GPU path cannot represent them");
   return OVL_OK;
+}
+
+// Work-order keys for the extension queue: a pair's match-node count (its extension work
+// grows with it), so the longest pairs start first and the kernel's tail is short.
+__global__ void k_pair_order_keys(const PairRec *pairs, uint32_t n, uint32_t *keys,
+                                  uint32_t *idx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    keys[i] = pairs[i].node_cnt;
+    idx[i] = i;
+  }
 }
 
 // Qualities (-w) into the packed layout: read r base i at wofs[r] * 32 + i.
@@ -873,6 +885,25 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     }
     EA.list = nullptr;
     EA.defer = nullptr;
+    if (npairs > 1) {
+      // longest-first work order (node count descending; ties keep pair order)
+      auto &fb = c->fb;
+      if (fb.okey.alloc(npairs) || fb.oidx.alloc(npairs) || fb.okey2.alloc(npairs) ||
+          fb.oidx2.alloc(npairs))
+        return fail(OVL_ERR_OOM, "work order");
+      hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
+                         dim3(256), 0, s, d_pairs.p, npairs, fb.okey.p, fb.oidx.p);
+      HIPC(hipGetLastError());
+      size_t tmp = 0;
+      HIPC(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, fb.okey.p, fb.okey2.p,
+                                                        fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
+                                                        32, s));
+      if (fb.otmp.alloc(tmp)) return fail(OVL_ERR_OOM, "work order scratch");
+      HIPC(hipcub::DeviceRadixSort::SortPairsDescending(fb.otmp.p, tmp, fb.okey.p, fb.okey2.p,
+                                                        fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
+                                                        32, s));
+      EA.list = fb.oidx2.p;
+    }
     EA.ndefer = d_ctr.p + 8;
     HIPC(hipEventRecord(c->ev[6], s));
     if (npairs) {
