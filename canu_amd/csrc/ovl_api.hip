@@ -641,8 +641,8 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   // A batch is sized by seed hits (node pool + list-ordered copy: 32 B per hit); the probe
   // window budget adapts to the hits-per-window ratio seen so far so that a batch's probe
   // results are all consumed (units beyond the hit budget would otherwise be re-probed).
-  const uint64_t HIT_BUDGET = 1280ull << 20;    // seed hits per batch
-  uint64_t WIN_BUDGET = 256ull << 20;           // probe slots per batch (8 B each)
+  const uint64_t HIT_BUDGET = 1792ull << 20;    // seed hits per batch (the node pool stays < 2^32)
+  uint64_t WIN_BUDGET = 512ull << 20;           // probe slots per batch (8 B each)
   auto &d_units = c->fb.units;
   auto &d_rbase = c->fb.rbase;
   auto &d_probe = c->fb.probe;
