@@ -378,7 +378,12 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
         uint32_t o = base + lane;
         Probe p;
         p.off = 0; p.cnt = 0;
-        if (o < nw) p = pr[o];
+        if (o < nw) {
+          p = pr[o];
+          // only the qualifying prefix (target iid > query, Find_Overlaps.C:328) is staged:
+          // lists are iid-descending, so it is found by a short search of the list itself
+          if (p.cnt) p.cnt = qualifying(A.occ, p.off, p.cnt, a_iid);
+        }
         uint32_t incl = p.cnt;                       // wave inclusive scan
         for (int d = 1; d < 64; d <<= 1) {
           uint32_t v = __shfl_up(incl, d);
