@@ -74,31 +74,67 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
   uint32_t kbits = (1u << A.k) - 1u;
   Probe *out = A.out + A.rbase[u];
   uint32_t hits = 0, flags = 0;
-  for (uint32_t o = lane; o < nw; o += 64) {
-    Probe pr;
-    pr.off = 0;
-    pr.cnt = 0;
-    bool ok = (int32_t)(o + A.k) <= L;
-    if (ok && bad) ok = (mask_at(bad, (int32_t)o) & kbits) == 0;
-    if (ok) {
-      uint64_t kmer = bases_at(S.w, (int32_t)o) & A.X.kmask;
-      const TabEntry *e = index_find(A.X, kmer);
-      if (e) {
-        uint32_t c = e->cnt;
-        if (c & OVL_FLAG_SKIP) {
-          // Hash_Find found an Empty entry: hi_hits (Find_Overlaps.C:321-366)
-          if (o < 90) flags |= 2u;
-          if (o > 0 && L - (int32_t)o - (int32_t)A.k + 1 < 90) flags |= 4u;
-        } else {
-          // whole occurrence list; the chain kernel drops targets with iid <= query
-          // (the qualifying prefix, Find_Overlaps.C:328) as it stages them
-          pr.off = e->off;
-          pr.cnt = c & OVL_CNT_MASK;
-          hits += pr.cnt;
-        }
+  // PU windows per lane per step: their table slots are computed first and their first
+  // 16-B entries loaded together, so each lane keeps PU random loads in flight (the
+  // lookups are latency-bound); the rare longer probe sequences continue one by one.
+  constexpr int PU = 4;
+  const uint64_t smask = (1ull << A.X.slice_bits) - 1;
+  for (uint32_t o0 = 0; o0 < nw; o0 += 64 * PU) {
+    uint64_t M[PU], slot0[PU];
+    bool ok[PU];
+#pragma unroll
+    for (int q = 0; q < PU; q++) {
+      const uint32_t o = o0 + 64 * q + lane;
+      ok[q] = o < nw && (int32_t)(o + A.k) <= L;
+      if (ok[q] && bad) ok[q] = (mask_at(bad, (int32_t)o) & kbits) == 0;
+      M[q] = 0;
+      slot0[q] = 0;
+      if (ok[q]) {
+        M[q] = mix64(bases_at(S.w, (int32_t)o) & A.X.kmask);
+        slot0[q] = M[q] >> (64 - A.X.tab_bits);
       }
     }
-    out[o] = pr;
+    TabEntry e[PU];
+#pragma unroll
+    for (int q = 0; q < PU; q++) {
+      e[q].key = 0; e[q].off = 0; e[q].cnt = 0;
+      if (ok[q]) e[q] = A.X.tab[slot0[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < PU; q++) {
+      const uint32_t o = o0 + 64 * q + lane;
+      if (o >= nw) continue;
+      Probe pr;
+      pr.off = 0;
+      pr.cnt = 0;
+      if (ok[q]) {
+        // index_find's linear probe within the slice, from the entry already loaded
+        TabEntry t = e[q];
+        bool found = false;
+        const uint64_t base = slot0[q] & ~smask;
+        for (uint64_t i = 1;; i++) {
+          if (t.cnt == 0) break;
+          if (t.key == M[q]) { found = true; break; }
+          if (i > smask) break;
+          t = A.X.tab[base | ((slot0[q] + i) & smask)];
+        }
+        if (found) {
+          const uint32_t c = t.cnt;
+          if (c & OVL_FLAG_SKIP) {
+            // Hash_Find found an Empty entry: hi_hits (Find_Overlaps.C:321-366)
+            if (o < 90) flags |= 2u;
+            if (o > 0 && L - (int32_t)o - (int32_t)A.k + 1 < 90) flags |= 4u;
+          } else {
+            // whole occurrence list; the chain kernel keeps its qualifying prefix
+            // (targets with iid > query, Find_Overlaps.C:328)
+            pr.off = t.off;
+            pr.cnt = c & OVL_CNT_MASK;
+            hits += pr.cnt;
+          }
+        }
+      }
+      out[o] = pr;
+    }
   }
   for (int s = 32; s > 0; s >>= 1) {
     hits += __shfl_xor(hits, s);
