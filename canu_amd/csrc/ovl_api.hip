@@ -726,7 +726,7 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     if (oe == hipSuccess && bpc > 0)
       ext_waves = std::min<uint32_t>(ext_waves, (uint32_t)bpc * stg_wpb * c->n_cu);
   }
-  uint32_t chain_waves = 16u * c->n_cu;
+  uint32_t chain_waves = 24u * c->n_cu;      // 6 blocks of 4 waves per CU (80 VGPRs, 21 KB LDS)
   const uint32_t DONE_CAP = 4096;
   if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");
 

@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
 
 // ---------------------------------------------------------------------------------------
 
-#define OVL_HCAP   512           // staged occurrences per wave
+#define OVL_HCAP   256           // staged occurrences per wave
 #define OVL_MAXT   128           // targets per pass (2 per lane)
 #define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
 
@@ -361,7 +361,7 @@ __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
   } while (0)
 
-__global__ void __launch_bounds__(256) k_chain(ChainArgs A) {
+__global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
   __shared__ uint64_t s_hb[4][OVL_HCAP];
   __shared__ uint8_t  s_hw[4][OVL_HCAP];      // window (0..63) of each staged occurrence
   __shared__ uint8_t  s_hs[4][OVL_HCAP];      // its target slot (0..127), 0xFF: none
