@@ -156,7 +156,8 @@ struct ovl_ctx {
   // index
   bool have_index = false;
   uint32_t hash_bgn_iid = 0, hash_end_iid = 0;
-  DBuf<uint64_t> d_occ, d_tmpM, d_tmpP, d_tmpM2;
+  DBuf<uint64_t> d_occ, d_tmpM2;
+  DBuf<Rec2> d_tmpR, d_midR;     // build scratch: coarse- and fine-bucketed records
   DBuf<TabEntry> d_tab;
   uint32_t tab_bits = 0, slice_bits = 0;
 
@@ -484,7 +485,7 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   uint32_t fb = std::min<uint32_t>(11, ceil_log2((per_cb + 255) / 256));
   uint32_t ncb = 1u << cb, nfb = 1u << fb, nfine = ncb * nfb;
 
-  if (c->d_tmpM.alloc(P) || c->d_tmpP.alloc(P) || c->d_tmpM2.alloc(P) || c->d_occ.alloc(P))
+  if (c->d_tmpR.alloc(P) || c->d_midR.alloc(P) || c->d_tmpM2.alloc(P) || c->d_occ.alloc(P))
     return fail(OVL_ERR_OOM, "index records (%llu)", (unsigned long long)P);
   DBuf<uint32_t> hist, cstart, cursor, fstart, fcnt, misc, big;
   if (hist.alloc(ncb) || cstart.alloc(ncb) || cursor.alloc(ncb) || fstart.alloc(nfine) ||
@@ -510,11 +511,10 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   hipLaunchKernelGGL(k_coarse_hist, dim3(nblk), dim3(256), 0, s, A, hist.p);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, hist.p, cstart.p, ncb, misc.p + 0);
   HIPC(hipMemcpyAsync(cursor.p, cstart.p, 4 * ncb, hipMemcpyDeviceToDevice, s));
-  hipLaunchKernelGGL(k_coarse_scatter, dim3(nblk), dim3(256), 0, s, A, cursor.p, c->d_tmpM.p,
-                     c->d_tmpP.p);
+  hipLaunchKernelGGL(k_coarse_scatter, dim3(nblk), dim3(256), 0, s, A, cursor.p, c->d_tmpR.p);
   FineArgs F;
-  F.inM = c->d_tmpM.p;
-  F.inP = c->d_tmpP.p;
+  F.inR = c->d_tmpR.p;
+  F.midR = c->d_midR.p;
   F.outM = c->d_tmpM2.p;
   F.outP = c->d_occ.p;
   F.cstart = cstart.p;
@@ -589,8 +589,8 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   float ms = 0;
   (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
   c->stats.ms_index = ms;
-  c->d_tmpM.release();
-  c->d_tmpP.release();
+  c->d_tmpR.release();
+  c->d_midR.release();
   c->have_index = true;
   return OVL_OK;
 }

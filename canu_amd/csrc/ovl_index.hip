@@ -147,8 +147,13 @@ __global__ void k_coarse_hist(BuildArgs A, uint32_t *hist) {
     if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-__global__ void k_coarse_scatter(BuildArgs A, uint32_t *cursor, uint64_t *outM,
-                                 uint64_t *outP) {
+// A (mix(kmer), position) record as one 16-B store: the scatter passes write whole
+// records, half the transactions of two 8-B arrays.
+struct __attribute__((aligned(16))) Rec2 {
+  uint64_t m, p;
+};
+
+__global__ void k_coarse_scatter(BuildArgs A, uint32_t *cursor, Rec2 *outR) {
   __shared__ uint32_t h[OVL_CB_MAX];
   __shared__ uint32_t base[OVL_CB_MAX];
   uint32_t nb = 1u << A.cb_bits;
@@ -167,8 +172,10 @@ __global__ void k_coarse_scatter(BuildArgs A, uint32_t *cursor, uint64_t *outM,
     uint64_t M = mix64(kmer);
     uint32_t b = (uint32_t)(M >> (64 - A.cb_bits));
     uint32_t slot = base[b] + atomicAdd(&h[b], 1u);
-    outM[slot] = M;
-    outP[slot] = pos;
+    Rec2 r;
+    r.m = M;
+    r.p = pos;
+    outR[slot] = r;
   });
 }
 
@@ -199,8 +206,9 @@ __device__ void wave_bitonic(uint64_t *sM, uint64_t *sP, uint32_t n2, uint32_t l
 #define OVL_FB_MAX      4096
 
 struct FineArgs {
-  const uint64_t *inM, *inP;     // coarse-bucketed records
-  uint64_t *outM, *outP;         // fine-bucketed, sorted records
+  const Rec2 *inR;               // coarse-bucketed records
+  Rec2 *midR;                    // fine-bucketed (unsorted) records
+  uint64_t *outM, *outP;         // fine-bucketed, sorted records (big buckets: unsorted)
   const uint32_t *cstart;        // coarse bucket start (exclusive scan of hist)
   const uint32_t *ccnt;          // coarse bucket counts
   uint32_t *fstart, *fcnt;       // fine bucket start / count (global index)
@@ -226,7 +234,7 @@ k_fine(FineArgs A) {
   for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) h[i] = 0;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-    atomicAdd(&h[(uint32_t)(A.inM[s0 + i] >> shift) & (nf - 1)], 1u);
+    atomicAdd(&h[(uint32_t)(A.inR[s0 + i].m >> shift) & (nf - 1)], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {                        // nf <= 4096: serial scan is cheap
     uint32_t acc = 0;
@@ -239,11 +247,10 @@ k_fine(FineArgs A) {
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    uint64_t M = A.inM[s0 + i];
-    uint32_t f = (uint32_t)(M >> shift) & (nf - 1);
+    const Rec2 r = A.inR[s0 + i];
+    uint32_t f = (uint32_t)(r.m >> shift) & (nf - 1);
     uint32_t slot = atomicAdd(&cur[f], 1u);
-    A.outM[s0 + slot] = M;
-    A.outP[s0 + slot] = A.inP[s0 + i];
+    A.midR[s0 + slot] = r;
   }
   __threadfence_block();
   __syncthreads();
@@ -255,6 +262,12 @@ k_fine(FineArgs A) {
     if (fn == 0) continue;
     uint32_t fs = s0 + cur[f] - fn;              // cur[] now holds the fine bucket end
     if (fn > cap) {
+      // too large for the LDS sort: copy out unsorted, k_fine_big sorts it in place
+      for (uint32_t i = lane; i < fn; i += 64) {
+        const Rec2 r = A.midR[fs + i];
+        A.outM[fs + i] = r.m;
+        A.outP[fs + i] = r.p;
+      }
       if (lane == 0) {
         uint32_t j = atomicAdd(A.big_n, 1u);
         A.big_list[2 * j] = fs;
@@ -265,7 +278,7 @@ k_fine(FineArgs A) {
     uint32_t n2 = 1;
     while (n2 < fn) n2 <<= 1;
     for (uint32_t i = lane; i < n2; i += 64) {
-      if (i < fn) { wM[i] = A.outM[fs + i]; wP[i] = A.outP[fs + i]; }
+      if (i < fn) { const Rec2 r = A.midR[fs + i]; wM[i] = r.m; wP[i] = r.p; }
       else        { wM[i] = ~0ull;          wP[i] = 0; }
     }
     __builtin_amdgcn_wave_barrier();
