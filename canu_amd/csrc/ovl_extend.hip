@@ -624,17 +624,20 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
   constexpr int JU = 1;
+  constexpr int WB = 9;                        // log2(64 * J): window offset bits of a key
+  static_assert(64 * J == (1 << WB), "key layout assumes a 512-diagonal window");
+  const int32_t lkey = 64 * J - 1 - (int32_t)lane;
 
   for (int32_t e = 1; e <= limit; e++) {
     PROF_T(pt_row);
     const int32_t ML = WM.mlim[e];
-    const int32_t left = pl - 1, right = pr + 1;
+    const int32_t right = pr + 1;
     // The window is anchored at the band: B <= pl-3 < B+16, so the row's chunks are
     // 0..jr with little waste in chunk 0.  When pl-3 leaves [B, B+16) the window moves to
     // B = pl-9: whole chunks by register moves, the rest by one ds_bpermute per chunk
     // (about one row in ten).  It must also hold pr+3 (the reads of this row and the log
     // of the next).
-    if (pl - 3 < B || pl - 3 - B >= 16) {
+    if ((uint32_t)(pl - 3 - B) >= 16u) {
       const int32_t nb = pl - 9;
       int32_t sft = nb - B;
       while (sft >= 64) {
@@ -675,41 +678,30 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       return out;
     }
     const int32_t jr = (right - B) >> 6;
-    const uint32_t span = (uint32_t)(right - left);
 
-    // ---- A: neighbours from row e-1 for every chunk (DPP, no LDS) --------------------
+    // ---- A+B per chunk: neighbours from row e-1 (DPP, no LDS), then the first 32-base
+    // slide step of every lane, branch-free (one pass: each unrolled chunk costs a scalar
+    // compare-and-branch on jr) --------------------------------------------------------
     int32_t NR[J], LM[J];
-    uint64_t actm[J];
-    {
-#pragma unroll
-      for (int j = 0; j < J; j++) {
-        if (j >= JU && j > jr) break;
-        const int32_t d = B + 64 * j + (int32_t)lane;
-        const int32_t p0 = R[j];
-        // row e-1 at d-1 and d+1 (diagonal B-1 and B+64J are outside the band: -2)
-        const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, R[j > 0 ? j - 1 : 0]);
-        const int32_t pp = (j + 1 < J) ? dpp_upper_across(p0, R[j + 1 < J ? j + 1 : j])
-                                       : dpp_from_upper(p0, -2);
-        const int32_t r0 = 1 + p0, r2 = 1 + pp;
-        const int32_t r = (pm > r0 ? pm : r0) > r2 ? (pm > r0 ? pm : r0) : r2;
-        const bool act = (uint32_t)(d - left) <= span;
-        actm[j] = __builtin_amdgcn_ballot_w64(act);
-        const int32_t l1 = m - r, l2 = n - r - d;
-        NR[j] = r;
-        LM[j] = act ? (l1 < l2 ? l1 : l2) : 0;
-      }
-    }
-
-    PROF_T(pt_a);
-    PROF_ADD(pc_a, pt_row, pt_a);
-    // ---- B: first 32-base slide step of every lane, branch-free (the kernel is VALU
-    // bound: no batching copies, one chunk at a time) ------------------------------------
     uint64_t need[J];
+    uint64_t any = 0;
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
-      const int32_t r = NR[j], lim = LM[j];
+      const int32_t p0 = R[j];
+      // row e-1 at d-1 and d+1 (diagonal B-1 and B+64J are outside the band: -2)
+      const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, R[j > 0 ? j - 1 : 0]);
+      const int32_t pp = (j + 1 < J) ? dpp_upper_across(p0, R[j + 1 < J ? j + 1 : j])
+                                     : dpp_from_upper(p0, -2);
+      const int32_t r0 = 1 + p0, r2 = 1 + pp;
+      const int32_t r = (pm > r0 ? pm : r0) > r2 ? (pm > r0 ? pm : r0) : r2;
+      // d outside [left, right] sees only -2 sentinels, so r == -1 there (inside, r >= 1):
+      // its limit is hugely negative, so it never slides, ends or survives pruning
+      const int32_t l1 = m - r, l2 = n - r - d;
+      const int32_t lim = r >= 0 ? (l1 < l2 ? l1 : l2) : -(1 << 30);
+      LM[j] = lim;
+
       const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
       const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
       const int32_t ia = pa >> 5, it = pt >> 5;
@@ -726,33 +718,28 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
-      NR[j] = r + k;                           // lim >= 0 on active lanes, 0 elsewhere
+      NR[j] = r + k;                           // lim >= 0 inside the band
       need[j] = __builtin_amdgcn_ballot_w64(mm == 0u) & __builtin_amdgcn_ballot_w64(lim > 32);
+      any |= need[j];
     }
 #ifdef OVL_PROFILE
     pc_nch += (jr + 1 > JU ? jr + 1 : JU);
 #endif
     PROF_T(pt_b);
-    PROF_ADD(pc_b, pt_a, pt_b);
+    PROF_ADD(pc_a, pt_row, pt_b);
     // lanes that matched all 32 bases continue (the on-path diagonals): one loop over all
     // chunks so their LDS loads overlap
-    {
-      uint64_t any = 0;
+    if (any) {
 #pragma unroll
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
-        any |= need[j];
-      }
-      if (any) {
-#pragma unroll
-        for (int j = 0; j < J; j++) {
-          if (j >= JU && j > jr) break;
+        if (need[j]) {
           if (need[j] & (1ull << lane)) {
             const int32_t d = B + 64 * j + (int32_t)lane;
             NR[j] += slide_any<DIR>(A, a0, T, t0, NR[j], d, LM[j] - 32);
           }
 #ifdef OVL_PROFILE
-          if (need[j]) pc_slide++;
+          pc_slide++;
 #endif
         }
       }
@@ -760,47 +747,34 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 
     PROF_T(pt_cont);
     PROF_ADD(pc_cont, pt_b, pt_cont);
-    // ---- C: end test (first d in order) and Edit_Match_Limit pruning -----------------
-    uint64_t em[J], km[J], endany = 0;
+    // ---- C: end test (first d in order) and Edit_Match_Limit pruning, one pass ----------
+    // (every unrolled chunk costs a scalar compare-and-branch on jr, so the end test and
+    // the kept range share the loop: nl from the first chunk with a kept lane, nr from the
+    // last)
+    bool ended = false;
+    int32_t end_d = 0, end_row = 0, end_pp = 0;
+    int32_t nl = NONE, nr = NEG;
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t r = NR[j];
-      em[j] = (__builtin_amdgcn_ballot_w64(r == m) | __builtin_amdgcn_ballot_w64(r + d == n)) &
-              actm[j];
-      km[j] = __builtin_amdgcn_ballot_w64(r + (d > 0 ? d : 0) >= ML) & actm[j];
-      endany |= em[j];
-    }
-    bool ended = false;
-    int32_t end_d = 0, end_row = 0, end_pp = 0;
-    int32_t nl = NONE, nr = NEG;
-    if (endany) {
-#pragma unroll
-      for (int j = 0; j < J; j++) {
-        if (j >= JU && j > jr) break;
-        if (em[j]) {
-          const int32_t l = (int32_t)__builtin_ctzll(em[j]);
-          end_d = B + 64 * j + l;
-          end_row = __builtin_amdgcn_readlane(NR[j], l);
-          // row e-1 at d+1 (R still holds row e-1)
-          end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
-                 : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
-          ended = true;
-          break;
-        }
+      const uint64_t em = __builtin_amdgcn_ballot_w64(r == m) |
+                          __builtin_amdgcn_ballot_w64(r + d == n);
+      if (em) {
+        const int32_t l = (int32_t)__builtin_ctzll(em);
+        end_d = B + 64 * j + l;
+        end_row = __builtin_amdgcn_readlane(r, l);
+        // row e-1 at d+1 (R still holds row e-1)
+        end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
+               : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
+        ended = true;
+        break;
       }
-    }
-    if (!ended) {
-#pragma unroll
-      for (int j = J - 1; j >= 0; j--) {       // first chunk with a kept lane, from the top
-        if (j >= JU && j > jr) continue;
-        if (km[j]) nl = B + 64 * j + (int32_t)__builtin_ctzll(km[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < J; j++) {            // last chunk with a kept lane
-        if (j >= JU && j > jr) break;
-        if (km[j]) nr = B + 64 * j + 63 - (int32_t)__builtin_clzll(km[j]);
+      const uint64_t km = __builtin_amdgcn_ballot_w64(r + (d > 0 ? d : 0) >= ML);
+      if (km) {
+        if (nl == NONE) nl = B + 64 * j + (int32_t)__builtin_ctzll(km);
+        nr = B + 64 * j + 63 - (int32_t)__builtin_clzll(km);
       }
     }
 
@@ -839,8 +813,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     if (nl == NONE) break;                     // Left > Right
 
     // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
-    // traceback (cells up to nr+2 are read), longest row with the first d on ties
-    int32_t mx = NEG;
+    // traceback (cells up to nr+2 are read), longest row with the first d on ties: one
+    // wave max over keys (value << WB | 64J-1 - window offset), so a larger value wins and
+    // among equal values the smaller d (values < 2^21 and -2 keep the order in 32 bits)
+    int32_t kmx = NEG;
     const uint32_t kspan = (uint32_t)(nr - nl);
     const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
     g_cell_t *crow = clog + (size_t)e * (64 * J);
@@ -850,19 +826,16 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
       R[j] = v;
-      mx = v > mx ? v : mx;
+      const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
+      kmx = key > kmx ? key : kmx;
       crow[(d & (64 * J - 1))] = (cell_t)v;
     }
-    const int32_t M = wave_max(mx);
+    const int32_t K = wave_max(kmx);
+    const int32_t M = K >> WB;
     if (M > longest) {
-      int32_t bd = NONE;
-#pragma unroll
-      for (int j = 0; j < J; j++) {
-        if (j >= JU && j > jr) break;
-        const uint64_t b = __builtin_amdgcn_ballot_w64(R[j] == M);
-        if (b) { bd = B + 64 * j + (int32_t)__builtin_ctzll(b); break; }
-      }
-      longest = M; best_d = bd; best_e = e;
+      longest = M;
+      best_d = B + (64 * J - 1) - (K & (64 * J - 1));
+      best_e = e;
     }
     double score = longest * bmv - e;
     if (score > max_score) {
