@@ -557,6 +557,24 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
   nd_out = nd;
 }
 
+// Scalar copies of wave-uniform values: arguments of a non-inlined function arrive in
+// VGPRs, so without these a loop bound or branch on them is compiled as divergent
+// (exec-mask bookkeeping on every row).
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+template <typename P>
+__device__ __forceinline__ P *uni_ptr(P *p) {
+  const uint64_t b = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)b);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(b >> 32));
+  return (P *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double uni(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)b);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 template <int DIR, typename SS, bool L16>
 __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
                                                          int32_t a0, int32_t m, const SS &T,
@@ -601,7 +619,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   int32_t pl = 0, pr = 0;
   int32_t tb_e = -1, tb_d = 0, tb_last = 0;
   bool finished = false;
-  const double bmv = X.branch_match_value;
+  const double bmv = uni(X.branch_match_value);
   const bool partial = X.partial != 0;
   const int32_t mbed = X.min_branch_end_dist;
   const double mbts = X.min_branch_tail_slope;
@@ -619,7 +637,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   // global (not flat) stores: a flat store also counts against lgkmcnt, so every LDS wait
   // of the next row would wait for the log stores too
   typedef __attribute__((address_space(1))) cell_t g_cell_t;
-  g_cell_t *clog = (g_cell_t *)rows;
+  g_cell_t *clog = uni_ptr((g_cell_t *)rows);     // scalar base: stores use saddr + offset
   clog[(B + (int32_t)lane) & (64 * J - 1)] = (cell_t)R[0];
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
@@ -682,7 +700,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     // ---- A+B per chunk: neighbours from row e-1 (DPP, no LDS), then the first 32-base
     // slide step of every lane, branch-free (one pass: each unrolled chunk costs a scalar
     // compare-and-branch on jr) --------------------------------------------------------
-    int32_t NR[J], LM[J];
+    int32_t NR[J], RM[J];   // row value; lanes: bases left before the end (0 = end)
     uint64_t need[J];
     uint64_t any = 0;
 #pragma unroll
@@ -699,8 +717,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       // d outside [left, right] sees only -2 sentinels, so r == -1 there (inside, r >= 1):
       // its limit is hugely negative, so it never slides, ends or survives pruning
       const int32_t l1 = m - r, l2 = n - r - d;
-      const int32_t lim = r >= 0 ? (l1 < l2 ? l1 : l2) : -(1 << 30);
-      LM[j] = lim;
+      const int32_t lmin = l1 < l2 ? l1 : l2;
+      const int32_t lim = r >= 0 ? lmin : -(1 << 30);
 
       const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
       const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
@@ -719,6 +737,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
       NR[j] = r + k;                           // lim >= 0 inside the band
+      RM[j] = lmin - k;                        // inside: lim - k >= 0; outside: > 0
       need[j] = __builtin_amdgcn_ballot_w64(mm == 0u) & __builtin_amdgcn_ballot_w64(lim > 32);
       any |= need[j];
     }
@@ -736,7 +755,9 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
         if (need[j]) {
           if (need[j] & (1ull << lane)) {
             const int32_t d = B + 64 * j + (int32_t)lane;
-            NR[j] += slide_any<DIR>(A, a0, T, t0, NR[j], d, LM[j] - 32);
+            const int32_t sl = slide_any<DIR>(A, a0, T, t0, NR[j], d, RM[j]);
+            NR[j] += sl;
+            RM[j] -= sl;
           }
 #ifdef OVL_PROFILE
           pc_slide++;
@@ -747,36 +768,48 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 
     PROF_T(pt_cont);
     PROF_ADD(pc_cont, pt_b, pt_cont);
-    // ---- C: end test (first d in order) and Edit_Match_Limit pruning, one pass ----------
-    // (every unrolled chunk costs a scalar compare-and-branch on jr, so the end test and
-    // the kept range share the loop: nl from the first chunk with a kept lane, nr from the
-    // last)
-    bool ended = false;
-    int32_t end_d = 0, end_row = 0, end_pp = 0;
-    int32_t nl = NONE, nr = NEG;
+    // ---- C: end test and Edit_Match_Limit pruning, one pass ---------------------------
+    // (scalar work per chunk kept minimal: the end masks are only OR-ed -- the end row is
+    // rare and re-scanned below -- and the kept range is a min/max of window offsets:
+    // s_ff1 / s_flbit give -1 on an empty mask, so an empty chunk contributes ~0u to the
+    // min, and an empty chunk's 0 to the max is harmless because the max only matters
+    // when some chunk has a kept lane, at an offset >= 0)
+    uint64_t endany = 0;
+    uint32_t nlo = 0xffffffffu;
+    int32_t nro = -1;
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
-      const int32_t r = NR[j];
-      const uint64_t em = __builtin_amdgcn_ballot_w64(r == m) |
-                          __builtin_amdgcn_ballot_w64(r + d == n);
-      if (em) {
-        const int32_t l = (int32_t)__builtin_ctzll(em);
-        end_d = B + 64 * j + l;
-        end_row = __builtin_amdgcn_readlane(r, l);
-        // row e-1 at d+1 (R still holds row e-1)
-        end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
-               : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
-        ended = true;
-        break;
-      }
-      const uint64_t km = __builtin_amdgcn_ballot_w64(r + (d > 0 ? d : 0) >= ML);
-      if (km) {
-        if (nl == NONE) nl = B + 64 * j + (int32_t)__builtin_ctzll(km);
-        nr = B + 64 * j + 63 - (int32_t)__builtin_clzll(km);
+      endany |= __builtin_amdgcn_ballot_w64(RM[j] == 0);
+      const uint64_t km = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
+      const uint32_t f = (uint32_t)__builtin_ctzg(km, -1);
+      const uint32_t c = f | (uint32_t)(64 * j);
+      nlo = c < nlo ? c : nlo;
+      const int32_t l = __builtin_clzg(km, -1);
+      nro = km ? 64 * j + 63 - l : nro;
+    }
+    bool ended = false;
+    int32_t end_d = 0, end_row = 0, end_pp = 0;
+    if (endany) {                              // the first d in order that reached the end
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        if (j >= JU && j > jr) break;
+        const uint64_t em = __builtin_amdgcn_ballot_w64(RM[j] == 0);
+        if (em) {
+          const int32_t l = (int32_t)__builtin_ctzll(em);
+          end_d = B + 64 * j + l;
+          end_row = __builtin_amdgcn_readlane(NR[j], l);
+          // row e-1 at d+1 (R still holds row e-1)
+          end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
+                 : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
+          ended = true;
+          break;
+        }
       }
     }
+    const int32_t nl = (nlo == 0xffffffffu) ? NONE : B + (int32_t)nlo;
+    const int32_t nr = B + nro;
 
     PROF_T(pt_chunks);
     PROF_ADD(pc_chunks, pt_row, pt_chunks);
