@@ -583,6 +583,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
                                                          uint32_t lane) {
   constexpr int J = OVL_RJ;
   static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
+  limit = uni(limit);
   int32_t *rows = WM.rows, *rowdir = WM.rowdir;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
@@ -646,7 +647,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   static_assert(64 * J == (1 << WB), "key layout assumes a 512-diagonal window");
   const int32_t lkey = 64 * J - 1 - (int32_t)lane;
 
-  for (int32_t e = 1; e <= limit; e++) {
+  int32_t e = 1;
+  bool ended = false;
+  int32_t end_d = 0, end_row = 0, end_pp = 0;
+  for (; e <= limit; e++) {
     PROF_T(pt_row);
     const int32_t ML = WM.mlim[e];
     const int32_t right = pr + 1;
@@ -693,7 +697,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     }
     if (pr + 3 > B + 64 * J - 1) {
       out.ovf = 1;
-      return out;
+      break;
     }
     const int32_t jr = (right - B) >> 6;
 
@@ -789,8 +793,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const int32_t l = __builtin_clzg(km, -1);
       nro = km ? 64 * j + 63 - l : nro;
     }
-    bool ended = false;
-    int32_t end_d = 0, end_row = 0, end_pp = 0;
     if (endany) {                              // the first d in order that reached the end
 #pragma unroll
       for (int j = 0; j < J; j++) {
@@ -817,33 +819,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #ifdef OVL_PROFILE
     pc_rows++;
 #endif
-    if (ended) {
-      double  score = end_row * bmv - e;
-      int32_t tail_len = end_row - max_score_len;
-      double  slope = (double)(max_score - score) / tail_len;
-      bool    abort_here = false;
-      if (partial && score < max_score) abort_here = true;
-      if (e > mbed / 2 && tail_len >= mbed && slope >= mbts) abort_here = true;
-      if (abort_here) {
-        out.err = max_score_best_e;
-        out.a_len = max_score_len;
-        out.t_len = max_score_len + max_score_best_d;
-        out.mte = 0;
-        tb_e = max_score_best_e; tb_d = max_score_best_d;
-      } else {
-        int32_t d = end_d;
-        // forward.C:212 -- force the last error to be a mismatch rather than an insertion
-        if (DIR > 0 && end_row == m && 1 + end_pp == end_row && d < right) d++;
-        out.err = e;
-        out.a_len = end_row;
-        out.t_len = end_row + d;
-        out.mte = 1;
-        tb_e = e; tb_d = d; tb_last = end_row;
-      }
-      finished = true;
-      break;
-    }
-    if (nl == NONE) break;                     // Left > Right
+    if (ended || nl == NONE) break;            // end reached, or Left > Right
 
     // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
     // traceback (cells up to nr+2 are read), longest row with the first d on ties: one
@@ -881,6 +857,32 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     pr = nr;
     PROF_T(pt_rest);
     PROF_ADD(pc_rest, pt_chunks, pt_rest);
+  }
+  if (out.ovf) return out;
+  if (ended) {                               // forward.C:177-232, at row e
+    double  score = end_row * bmv - e;
+    int32_t tail_len = end_row - max_score_len;
+    double  slope = (double)(max_score - score) / tail_len;
+    bool    abort_here = false;
+    if (partial && score < max_score) abort_here = true;
+    if (e > mbed / 2 && tail_len >= mbed && slope >= mbts) abort_here = true;
+    if (abort_here) {
+      out.err = max_score_best_e;
+      out.a_len = max_score_len;
+      out.t_len = max_score_len + max_score_best_d;
+      out.mte = 0;
+      tb_e = max_score_best_e; tb_d = max_score_best_d;
+    } else {
+      int32_t d = end_d;
+      // forward.C:212 -- force the last error to be a mismatch rather than an insertion
+      if (DIR > 0 && end_row == m && 1 + end_pp == end_row && d < pr + 1) d++;
+      out.err = e;
+      out.a_len = end_row;
+      out.t_len = end_row + d;
+      out.mte = 1;
+      tb_e = e; tb_d = d; tb_last = end_row;
+    }
+    finished = true;
   }
   if (!finished) {
     out.err = max_score_best_e;
