@@ -615,8 +615,11 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   if (lane == 3) R[0] = row0;
 
   double  max_score = 0.0;
-  int32_t max_score_len = 0, max_score_best_d = 0, max_score_best_e = 0;
-  int32_t best_d = 0, best_e = 0, longest = 0;
+  int32_t max_score_len = 0, max_score_best_e = 0;
+  // Max_Score_Best_d is kept as the row key and window base it decodes from (decoded once,
+  // after the loop): B + 64J-1 - (key & 64J-1)
+  int32_t ms_key = 64 * J - 1, ms_B = 0;
+  int32_t longest = 0;
   int32_t pl = 0, pr = 0;
   int32_t tb_e = -1, tb_d = 0, tb_last = 0;
   bool finished = false;
@@ -841,17 +844,18 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     }
     const int32_t K = wave_max(kmx);
     const int32_t M = K >> WB;
-    if (M > longest) {
+    if (M > longest) {                         // Longest, Best_d, Best_e of this row
       longest = M;
-      best_d = B + (64 * J - 1) - (K & (64 * J - 1));
-      best_e = e;
-    }
-    double score = longest * bmv - e;
-    if (score > max_score) {
-      max_score = score;
-      max_score_len = longest;
-      max_score_best_d = best_d;
-      max_score_best_e = best_e;
+      // the score can only beat Max_Score on a row whose Longest grew: otherwise it is the
+      // previous row's score minus one (monotone in double too), and that was <= Max_Score
+      const double score = longest * bmv - e;
+      if (score > max_score) {
+        max_score = score;
+        max_score_len = longest;
+        ms_key = K;
+        ms_B = B;
+        max_score_best_e = e;
+      }
     }
     pl = nl;
     pr = nr;
@@ -859,6 +863,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     PROF_ADD(pc_rest, pt_chunks, pt_rest);
   }
   if (out.ovf) return out;
+  const int32_t max_score_best_d = ms_B + (64 * J - 1) - (ms_key & (64 * J - 1));
   if (ended) {                               // forward.C:177-232, at row e
     double  score = end_row * bmv - e;
     int32_t tail_len = end_row - max_score_len;
