@@ -152,8 +152,9 @@ def main() -> None:
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": _traffic(traffic, "k_extend"), "kernel": "k_extend",
-                "limiter": "latency of the greedy O(ND) row recurrence (integer VALU/LDS "
-                           "dependency chains; no MFMA shape, HBM nearly idle)",
+                "limiter": "instruction issue of the greedy O(ND) rows: the per-row scalar "
+                           "control (SALU, shared by a CU's 4 SIMDs) first, then integer VALU; "
+                           "no MFMA shape, HBM far from busy",
                 "issue": traffic.get("k_extend", {}).get("issue"),
                 "algorithmic_bytes_per_launch": int(per_launch), "launches": n_ext,
                 "avg_launch_ms": round(avg_ms, 3)}
