@@ -480,12 +480,13 @@ __device__ __forceinline__ int32_t dpp_from_upper(int32_t v, int32_t lane63) {  
 // Chunk-boundary neighbours without a readlane: lane l <- v[l-1], lane 0 <- prev[63]
 // (wave_ror:1 of prev supplies lane 0, then wave_shr:1 of v overwrites lanes 1..63), and
 // lane l <- v[l+1], lane 63 <- next[0] (wave_rol:1, then wave_shl:1).
+// (a rotate writes every lane, so it needs no old value and no initialising move)
 __device__ __forceinline__ int32_t dpp_lower_across(int32_t v, int32_t prev) {
-  const int32_t u = __builtin_amdgcn_update_dpp(0, prev, 0x13C, 0xf, 0xf, false);
+  const int32_t u = __builtin_amdgcn_mov_dpp(prev, 0x13C, 0xf, 0xf, false);
   return __builtin_amdgcn_update_dpp(u, v, 0x138, 0xf, 0xf, false);
 }
 __device__ __forceinline__ int32_t dpp_upper_across(int32_t v, int32_t next) {
-  const int32_t u = __builtin_amdgcn_update_dpp(0, next, 0x134, 0xf, 0xf, false);
+  const int32_t u = __builtin_amdgcn_mov_dpp(next, 0x134, 0xf, 0xf, false);
   return __builtin_amdgcn_update_dpp(u, v, 0x130, 0xf, 0xf, false);
 }
 
