@@ -171,6 +171,12 @@ def main() -> None:
                       "traffic": _traffic(traffic, "k_probe"), "kernel": "k_probe",
                       "algorithmic_bytes_per_launch": int(per_launch), "launches": n_pr,
                       "avg_launch_ms": round(avg_ms, 3)}
+        # the same launch against the roofline in the bytes it actually moves (PMC traffic
+        # per launch over this run's launch time): one 64-B sector per 16-B slot probed
+        tb = probe_roof["traffic"]
+        if tb:
+            probe_roof["traffic_gbs"] = round(tb / (avg_ms * 1e-3) / 1e9, 1)
+            probe_roof["traffic_frac"] = round(probe_roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -720,16 +720,17 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, R[j > 0 ? j - 1 : 0]);
       const int32_t pp = (j + 1 < J) ? dpp_upper_across(p0, R[j + 1 < J ? j + 1 : j])
                                      : dpp_from_upper(p0, -2);
-      const int32_t r0 = 1 + p0, r2 = 1 + pp;
-      const int32_t r = (pm > r0 ? pm : r0) > r2 ? (pm > r0 ? pm : r0) : r2;
-      // d outside [left, right] sees only -2 sentinels, so r == -1 there (inside, r >= 1):
+      // q = Row - 1 = max(pm - 1, p0, pp): the +1 of the max3 folds into the constants
+      const int32_t pm1 = pm - 1;
+      const int32_t q = (pm1 > p0 ? pm1 : p0) > pp ? (pm1 > p0 ? pm1 : p0) : pp;
+      // d outside [left, right] sees only -2 sentinels, so Row == -1 there (inside, >= 1):
       // its limit is hugely negative, so it never slides, ends or survives pruning
-      const int32_t l1 = m - r, l2 = n - r - d;
+      const int32_t l1 = (m - 1) - q, l2 = (n - 1) - q - d;
       const int32_t lmin = l1 < l2 ? l1 : l2;
-      const int32_t lim = r >= 0 ? lmin : -(1 << 30);
+      const int32_t lim = q >= -1 ? lmin : -(1 << 30);
 
-      const int32_t pa = (DIR > 0) ? a0 + r : a0 - r - 31;
-      const int32_t pt = (DIR > 0) ? t0 + r + d : t0 - r - d - 31;
+      const int32_t pa = (DIR > 0) ? (a0 + 1) + q : (a0 - 32) - q;
+      const int32_t pt = (DIR > 0) ? (t0 + 1) + q + d : (t0 - 32) - q - d;
       const int32_t ia = pa >> 5, it = pt >> 5;
       const uint64_t wa0 = A.w[ia], wa1 = A.w[ia + 1];
       const uint64_t wt0 = T.w[it], wt1 = T.w[it + 1];
@@ -741,12 +742,15 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const uint32_t xt1 = __builtin_amdgcn_alignbit((uint32_t)(wt1 >> 32), (uint32_t)(wt0 >> 32),
                                                      (uint32_t)pt);
       const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
-      const int32_t run = (DIR > 0) ? run_fwd(mm) : run_bwd(mm);
+      // the first step examines 31 bases (a sentinel mismatch in the 32nd: no clamp of
+      // the bit scan), lanes that matched all 31 with more left continue below
+      const int32_t run = (DIR > 0) ? (int32_t)__builtin_ctz(mm | 0x80000000u)
+                                    : (int32_t)__builtin_clz(mm | 1u);
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
-      NR[j] = r + k;                           // lim >= 0 inside the band
+      NR[j] = q + 1 + k;                       // lim >= 0 inside the band
       RM[j] = lmin - k;                        // inside: lim - k >= 0; outside: > 0
-      need[j] = __builtin_amdgcn_ballot_w64(mm == 0u) & __builtin_amdgcn_ballot_w64(lim > 32);
+      need[j] = __builtin_amdgcn_ballot_w64(run == 31) & __builtin_amdgcn_ballot_w64(lim > 31);
       any |= need[j];
     }
 #ifdef OVL_PROFILE
@@ -754,7 +758,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
 #endif
     PROF_T(pt_b);
     PROF_ADD(pc_a, pt_row, pt_b);
-    // lanes that matched all 32 bases continue (the on-path diagonals): one loop over all
+    // lanes that matched all 31 bases continue (the on-path diagonals): one loop over all
     // chunks so their LDS loads overlap
     if (any) {
 #pragma unroll
