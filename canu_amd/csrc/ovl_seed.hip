@@ -371,6 +371,7 @@ __global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
   __shared__ uint32_t s_off[4][64];
   __shared__ uint32_t s_tgt[4][OVL_MAXT];
   __shared__ uint32_t s_alloc[4][2];
+  __shared__ uint64_t s_lmask[4][OVL_MAXT];   // stable scatter: lanes of each slot
   __shared__ uint32_t s_over[4];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t *hb = s_hb[wave];
@@ -381,6 +382,8 @@ __global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
   uint32_t *seg = s_seg[wave];
   uint32_t *soff = s_off[wave];
   uint32_t *tgt = s_tgt[wave];
+  uint64_t *lmask = s_lmask[wave];
+  for (uint32_t i = lane; i < OVL_MAXT; i += 64) lmask[i] = 0;
   WaveAlloc W;
   W.cur = &s_alloc[wave][0];
   W.end = &s_alloc[wave][1];
@@ -491,27 +494,27 @@ __global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
             cnt[OVL_MAXT + 2 * lane + 1] = 0;
           }
           WAVE_SYNC();
-          // stable scatter: within each 64-entry step, rank the lanes of each slot in
-          // lane order (one ballot per distinct slot), so every slot's list keeps the
-          // staged (window, chain) order
+          // stable scatter: within each 64-entry step a lane's rank among the lanes of its
+          // slot is the popcount of the lower lanes in the slot's lane mask (one LDS OR per
+          // lane), so every slot's list keeps the staged (window, chain) order
           for (uint32_t b0 = p0; b0 < p1; b0 += 64) {
             uint32_t idx = b0 + lane;
             uint32_t slot = (idx < p1) ? hs[idx - p0] : 0xFFu;
-            uint64_t todo = __ballot(slot != 0xFFu);
-            while (todo) {
-              uint32_t leader = (uint32_t)__builtin_ctzll(todo);
-              uint32_t sl = __builtin_amdgcn_readlane(slot, leader);
-              uint64_t grp = __ballot(slot == sl) & todo;
-              uint32_t run = cnt[OVL_MAXT + sl];
-              if ((grp >> lane) & 1ull) {
-                uint32_t rank = __builtin_popcountll(grp & ((1ull << lane) - 1));
-                sx[cnt[sl] + run + rank] = (uint16_t)(idx - p0);
-              }
-              WAVE_SYNC();
-              if (lane == leader) cnt[OVL_MAXT + sl] = run + __builtin_popcountll(grp);
-              WAVE_SYNC();
-              todo &= ~grp;
+            const bool has = slot != 0xFFu;
+            if (has) atomicOr(&lmask[slot], 1ull << lane);
+            WAVE_SYNC();
+            uint64_t mk = 0;
+            if (has) {
+              mk = lmask[slot];
+              uint32_t rank = __builtin_popcountll(mk & ((1ull << lane) - 1));
+              sx[cnt[slot] + cnt[OVL_MAXT + slot] + rank] = (uint16_t)(idx - p0);
             }
+            WAVE_SYNC();
+            if (has && lane == (uint32_t)__builtin_ctzll(mk)) {   // the slot's first lane
+              cnt[OVL_MAXT + slot] += __builtin_popcountll(mk);
+              lmask[slot] = 0;
+            }
+            WAVE_SYNC();
           }
           WAVE_SYNC();
           uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
