@@ -208,7 +208,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
                            const SS &T, int32_t t0, int32_t n, int32_t limit,
                            const WaveMem &WM, int32_t *dst, uint32_t lane) {
   int32_t *rows = WM.rows, *rowdir = WM.rowdir;
-  lds_i32 *tbw = WM.tbw;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;
@@ -585,7 +584,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   constexpr int J = OVL_RJ;
   static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
   limit = uni(limit);
-  int32_t *rows = WM.rows, *rowdir = WM.rowdir;
+  int32_t *rows = WM.rows;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;

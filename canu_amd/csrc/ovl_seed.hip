@@ -69,7 +69,6 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
   Strand S = un.dir ? strand_rc(A.R, un.r) : strand_fwd(A.R, un.r);
   const uint32_t *bad = un.dir ? S.ex_nul : S.ex_wild;
   uint32_t nw = unit_windows(A.R, un, A.k);
-  uint32_t a_iid = A.R.first_iid + un.r;
   int32_t L = S.len;
   uint32_t kbits = (1u << A.k) - 1u;
   Probe *out = A.out + A.rbase[u];
