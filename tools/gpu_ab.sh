@@ -1,5 +1,6 @@
 # A/B timing of library variants (canu_amd/lib/ab_*.so, built beforehand) on the
-# 10k-read workload: per-variant breakdown, twice each in alternating order; with
+# 10k-read workload (AB_READS, AB_STEPS override): per-variant breakdown, twice each in
+# alternating order; with
 # AB_PMC=1 also one rocprofv3 issue-counter pass per variant (k_extend instruction mix).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -7,7 +8,7 @@ mkdir -p $R/gpurun_out
 for pass in 1 2; do
   for f in $R/canu_amd/lib/ab_*.so; do
     n=$(basename $f .so)
-    CANU_OVL_LIB=$f timeout -k 10 240 python $R/bench.py --reads 10000 --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/$n.log 2>&1 || exit 1
+    CANU_OVL_LIB=$f timeout -k 10 240 python $R/bench.py --reads ${AB_READS:-10000} --steps ${AB_STEPS:-3} --warmup 1 --no-cpu-baseline > $R/gpurun_out/$n.log 2>&1 || exit 1
     echo "$pass $n $(grep -o '"breakdown_ms": {[^}]*}' $R/gpurun_out/$n.log)"
   done
 done
