@@ -589,8 +589,8 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   float ms = 0;
   (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
   c->stats.ms_index = ms;
-  c->d_tmpR.release();
-  c->d_midR.release();
+  // the build scratch (2 x 16 B per window) stays allocated for the next build: freeing and
+  // re-allocating gigabytes per job costs tens of ms on some hosts (and HBM is plentiful)
   c->have_index = true;
   return OVL_OK;
 }

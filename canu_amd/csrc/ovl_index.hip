@@ -257,6 +257,10 @@ k_fine(FineArgs A) {
 
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t *wM = s_fine + (size_t)wave * cap, *wP = s_fine + (size_t)(OVL_FINE_WAVES + wave) * cap;
+  __shared__ uint32_t s_runmax;                  // distinct k-mers of the block's largest bucket
+  if (threadIdx.x == 0) s_runmax = 0;
+  __syncthreads();
+  uint32_t wave_max_runs = 0;
   for (uint32_t f = wave; f < nf; f += OVL_FINE_WAVES) {
     uint32_t fn = h[f];
     if (fn == 0) continue;
@@ -291,10 +295,15 @@ k_fine(FineArgs A) {
       runs += (i == 0 || wM[i] != wM[i - 1]) ? 1u : 0u;
     }
     for (int o = 32; o > 0; o >>= 1) runs += __shfl_xor(runs, o);
-    if (lane == 0) atomicMax(A.max_distinct, runs);
+    wave_max_runs = runs > wave_max_runs ? runs : wave_max_runs;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
+  // one global atomic per block: a per-bucket atomic on the single max_distinct word
+  // serialises thousands of blocks in the L2
+  if (lane == 0) atomicMax(&s_runmax, wave_max_runs);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_runmax) atomicMax(A.max_distinct, s_runmax);
 }
 
 // Fine buckets larger than the LDS sort: one workgroup each, bitonic in global memory over
