@@ -378,17 +378,39 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t fs = A.fstart[f], fn = A.fcnt[f];
   uint32_t pshift = 64 - A.tab_bits;
+  // Run starts come from one ballot per 64 records, with a virtual start at fn; a run ends
+  // at the next start: in the same batch, in the next one (looked ahead), or -- for a run
+  // longer than a batch -- found by the whole wave scanning on.
+  auto starts = [&](uint32_t j0, uint64_t &Mj) -> uint64_t {
+    const uint32_t j = j0 + lane;
+    bool st = j == fn;
+    Mj = 0;
+    if (j < fn) {
+      Mj = A.M[fs + j];
+      st = (j == 0) || (A.M[fs + j - 1] != Mj);
+    }
+    return __builtin_amdgcn_ballot_w64(st);
+  };
+  uint64_t Mnext = 0;
+  uint64_t cur_m = fn ? starts(0, Mnext) : 0;
   for (uint32_t i0 = 0; i0 < fn; i0 += 64) {
     uint32_t i = i0 + lane;
-    bool start = false;
-    uint64_t M = 0;
-    if (i < fn) {
-      M = A.M[fs + i];
-      start = (i == 0) || (A.M[fs + i - 1] != M);
+    const uint64_t M = Mnext;
+    const uint64_t nxt_m = (i0 + 64 <= fn) ? starts(i0 + 64, Mnext) : 0;
+    const bool start = i < fn && ((cur_m >> lane) & 1ull);
+    const uint64_t above = cur_m & ~((2ull << lane) - 1ull);   // starts after this lane
+    const bool far = start && !above && !nxt_m;
+    uint32_t efar = 0;
+    if (__builtin_amdgcn_ballot_w64(far)) {    // a run longer than the next batch
+      for (uint32_t j0 = i0 + 128;; j0 += 64) {
+        uint64_t dummy;
+        const uint64_t m = starts(j0, dummy);
+        if (m) { efar = j0 + (uint32_t)__builtin_ctzll(m); break; }
+      }
     }
     if (start) {
-      uint32_t e = i + 1;                      // run end
-      while (e < fn && A.M[fs + e] == M) e++;
+      const uint32_t e = above ? i0 + (uint32_t)__builtin_ctzll(above)
+                       : nxt_m ? i0 + 64 + (uint32_t)__builtin_ctzll(nxt_m) : efar;
       uint32_t off = fs + i, cnt = e - i, flags = 0;
       if (A.P[off] == OVL_SKIP_POS) {          // marker sorts first (position descending)
         flags = OVL_FLAG_SKIP;
@@ -413,6 +435,7 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
       key[slot] = M;
       oc[2 * slot] = off;
     }
+    cur_m = nxt_m;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -73,6 +73,13 @@ def test_ns_repeats_ragged(built):
     _check(rs, _params())
 
 
+def test_long_kmer_runs(built):
+    # a repeat in 80 copies at ~10x coverage: its k-mers occur up to ~260 times, so their
+    # occurrence runs in the index span several 64-record batches (k_table's far path)
+    rs = synth_reads(150, 2000, 30_000, 0.02, seed=12, n_repeats=80, repeat_len=300)
+    _check(rs, _params(Unique_Olap_Per_Pair=False))
+
+
 def test_skip_kmers(built):
     rs = synth_reads(120, 2000, 30_000, 0.02, seed=6, n_repeats=5, repeat_len=200)
     skip = [rs.read(0)[i:i + 22].decode() for i in range(0, 1900, 10)]
