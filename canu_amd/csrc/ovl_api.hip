@@ -482,7 +482,7 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
 
   uint32_t cb = std::min<uint32_t>(12, std::max<uint32_t>(4, ceil_log2(P / 2048 + 1)));
   uint64_t per_cb = (P >> cb) + 1;
-  uint32_t fb = std::min<uint32_t>(11, ceil_log2((per_cb + 255) / 256));
+  uint32_t fb = std::min<uint32_t>(11, ceil_log2((per_cb + 127) / 128));   // ~128 per fine bucket
   uint32_t ncb = 1u << cb, nfb = 1u << fb, nfine = ncb * nfb;
 
   if (c->d_tmpR.alloc(P) || c->d_midR.alloc(P) || c->d_tmpM2.alloc(P) || c->d_occ.alloc(P))
