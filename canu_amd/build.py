@@ -47,6 +47,31 @@ def build_mhap(force: bool = False, verbose: bool = True) -> str:
     return MHAP_OUT
 
 
+BIN_DIR = os.path.join(HERE, "bin")
+CLI_OUT = os.path.join(BIN_DIR, "overlapInCore")
+CLI_DEPS = [os.path.join(CSRC, "oic_main.cpp"), os.path.join(CSRC, "gkp_store.h"),
+            os.path.join(HERE, "..", "include", "canu_ovl.h")]
+
+
+def build_cli(force: bool = False, verbose: bool = True) -> str:
+    """canu_amd/bin/overlapInCore: the overlapInCore-compatible executable (host C++ over
+    libcanu_ovl.so, found next to it through the rpath)."""
+    lib = build(verbose=verbose)
+    if not force and os.path.exists(CLI_OUT) and \
+            all(os.path.getmtime(d) <= os.path.getmtime(CLI_OUT) for d in CLI_DEPS + [lib]):
+        return CLI_OUT
+    os.makedirs(BIN_DIR, exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-o", CLI_OUT + ".tmp",
+           os.path.join(CSRC, "oic_main.cpp"), "-L" + OUT_DIR, "-lcanu_ovl",
+           "-Wl,-rpath,$ORIGIN/../lib", "-Wl,--allow-shlib-undefined"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(CLI_OUT + ".tmp", CLI_OUT)
+    return CLI_OUT
+
+
 def build(force: bool = False, verbose: bool = True, profile: bool = False) -> str:
     """profile=True builds the instrumented variant (in-kernel cycle stamps, OVL_DEBUG=1
     prints them) as libcanu_ovl_prof.so; load it with CANU_OVL_LIB."""
@@ -68,3 +93,4 @@ if __name__ == "__main__":
     build(force="--force" in sys.argv, profile="--profile" in sys.argv)
     if "--profile" not in sys.argv:
         build_mhap(force="--force" in sys.argv)
+        build_cli(force="--force" in sys.argv)

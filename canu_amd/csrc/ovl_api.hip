@@ -175,10 +175,17 @@ struct ovl_ctx {
     DBuf<int32_t> rows, rowdir, deltas;
   } fb;
 
+  // library IDs (-H / -R filters); empty = every read in library 0
+  std::vector<uint32_t> h_lib;
+  bool nohash_set = false;       // some read carries OVL_RFLAG_NOHASH
+  uint32_t stats_hash_lib_lo = 0, stats_hash_lib_hi = UINT32_MAX;   // -H of the index
+  uint64_t index_records = 0;    // records of the current index (windows + skip markers)
+
   // results
   DBuf<Rec> d_out;
   uint64_t nout = 0;
   ovl_stats stats;
+  DBuf<unsigned long long> dbg;  // OVL_DEBUG counters of this context's extension kernels
 
   ReadsDev reads() const {
     ReadsDev R;
@@ -287,26 +294,35 @@ void ovl_ctx_destroy(ovl_ctx *c) {
 
 static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const uint8_t *d_bases,
                        const uint64_t *d_offsets, const uint32_t *h_lengths) {
-  c->first_iid = first_iid;
-  c->nreads = nreads;
+  // Until every check and allocation has passed the context holds no reads, so a failed
+  // load leaves nothing for a later build / find to run over (they return OVL_ERR_STATE).
+  c->nreads = 0;
   c->have_index = false;
-  c->h_len.assign(h_lengths, h_lengths + nreads);
-  c->h_wofs.resize(nreads + 1);
+  c->have_qual = false;
+  c->h_lib.clear();
+  c->nohash_set = false;
+  if (first_iid == 0 && nreads) return fail(OVL_ERR_BAD_PARAM, "read IDs start at 1");
+  if ((uint64_t)first_iid + nreads > 0xFFFFFFFFull)
+    return fail(OVL_ERR_BAD_PARAM, "read IDs past 2^32");
+  std::vector<uint64_t> wofs(nreads + 1);
   uint64_t w = 0;
-  c->max_len = 0;
+  uint32_t max_len = 0;
   for (uint32_t i = 0; i < nreads; i++) {
     if (h_lengths[i] > AS_MAX_READLEN)
       return fail(OVL_ERR_BAD_INPUT, "read %u longer than AS_MAX_READLEN", first_iid + i);
-    c->h_wofs[i] = w;
+    wofs[i] = w;
     w += (h_lengths[i] + 31) / 32 + 1;
-    c->max_len = std::max(c->max_len, h_lengths[i]);
+    max_len = std::max(max_len, h_lengths[i]);
   }
-  c->h_wofs[nreads] = w;
+  wofs[nreads] = w;
   w += 2;
   if (c->d_fwd.alloc(w) || c->d_rc.alloc(w) || c->d_fwdN.alloc(w) || c->d_rcNul.alloc(w) ||
       c->d_wofs.alloc(nreads + 1) || c->d_len.alloc(nreads) || c->d_flags.alloc(nreads) ||
       c->d_rcFirstNul.alloc(nreads))
     return fail(OVL_ERR_OOM, "read buffers (%llu words)", (unsigned long long)w);
+  c->h_len.assign(h_lengths, h_lengths + nreads);
+  c->h_wofs.swap(wofs);
+  c->max_len = max_len;
   HIPC(hipMemsetAsync(c->d_fwd.p, 0, 8 * w, c->stream));
   HIPC(hipMemsetAsync(c->d_rc.p, 0, 8 * w, c->stream));
   HIPC(hipMemsetAsync(c->d_fwdN.p, 0, 4 * w, c->stream));
@@ -329,6 +345,8 @@ static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const ui
   if (h_err)
     return fail(OVL_ERR_BAD_INPUT,
                 "reads hold characters other than ACGTN; the GPU path cannot represent them");
+  c->first_iid = first_iid;
+  c->nreads = nreads;
   return OVL_OK;
 }
 
@@ -439,7 +457,17 @@ int ovl_set_skip_kmers(ovl_ctx *c, const char *kmers, uint64_t n) {
 
 static __global__ void k_clear_screen(uint32_t *flags, uint32_t n) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) flags[i] &= 1u;
+  if (i < n) flags[i] &= ~6u;                 // the screened-end bits of the last index
+}
+
+// OVL_RFLAG_NOHASH from a per-read byte (1 = not hashed); nohash == null clears it.
+static __global__ void k_set_nohash(uint32_t *flags, const uint8_t *nohash, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    uint32_t f = flags[i] & ~OVL_RFLAG_NOHASH;
+    if (nohash && nohash[i]) f |= OVL_RFLAG_NOHASH;
+    flags[i] = f;
+  }
 }
 
 static uint32_t ceil_log2(uint64_t x) {
@@ -448,16 +476,37 @@ static uint32_t ceil_log2(uint64_t x) {
   return b;
 }
 
-int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
-  if (!c) return fail(OVL_ERR_STATE, "null context");
-  if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
-  HIPC(hipSetDevice(c->device));
+static uint32_t read_lib(const ovl_ctx *c, uint32_t r) { return c->h_lib.empty() ? 0 : c->h_lib[r]; }
+
+// Mark the reads outside [lo, hi] as not hashed (device flag), or clear every mark.
+static int apply_hash_libs(ovl_ctx *c, uint32_t lo, uint32_t hi) {
+  bool any = false;
+  std::vector<uint8_t> nh;
+  if (!c->h_lib.empty() && (lo > 0 || hi < UINT32_MAX)) {
+    nh.resize(c->nreads);
+    for (uint32_t r = 0; r < c->nreads; r++) {
+      nh[r] = (c->h_lib[r] < lo || c->h_lib[r] > hi) ? 1 : 0;
+      any |= nh[r] != 0;
+    }
+  }
+  if (!any && !c->nohash_set) return OVL_OK;
+  DBuf<uint8_t> d;
+  if (any) {
+    if (d.alloc(c->nreads)) return fail(OVL_ERR_OOM, "library flags");
+    HIPC(hipMemcpyAsync(d.p, nh.data(), c->nreads, hipMemcpyHostToDevice, c->stream));
+  }
+  hipLaunchKernelGGL(k_set_nohash, dim3((c->nreads + 255) / 256), dim3(256), 0, c->stream,
+                     c->d_flags.p, any ? d.p : nullptr, c->nreads);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  c->nohash_set = any;
+  return OVL_OK;
+}
+
+// The index over hash reads bgn..end (clipped to the loaded reads by the callers).
+static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   hipStream_t s = c->stream;
   uint32_t k = c->P.kmer_len;
-  if (bgn < 1) bgn = 1;
-  if (bgn < c->first_iid) bgn = c->first_iid;
-  uint32_t last = c->first_iid + c->nreads - 1;
-  if (end > last) end = last;
   c->hash_bgn_iid = bgn;
   c->hash_end_iid = end;
   c->have_index = false;
@@ -468,7 +517,8 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   uint32_t h0 = bgn - c->first_iid, h1 = (end >= bgn) ? end - c->first_iid + 1 : h0;
   uint64_t P = 0;
   for (uint32_t r = h0; r < h1; r++)
-    if ((int32_t)c->h_len[r] >= c->P.min_olap_len && c->h_len[r] >= k)
+    if ((int32_t)c->h_len[r] >= c->P.min_olap_len && c->h_len[r] >= k && !(c->nohash_set &&
+        (read_lib(c, r) < c->stats_hash_lib_lo || read_lib(c, r) > c->stats_hash_lib_hi)))
       P += c->h_len[r] - k + 1;
   uint32_t n_skip = (uint32_t)c->h_skip.size();
   P += n_skip;
@@ -588,14 +638,158 @@ int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   HIPC(hipStreamSynchronize(s));
   float ms = 0;
   (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
-  c->stats.ms_index = ms;
+  c->stats.ms_index += ms;
+  c->index_records = hm[0];
   // the build scratch (2 x 16 B per window) stays allocated for the next build: freeing and
   // re-allocating gigabytes per job costs tens of ms on some hosts (and HBM is plentiful)
   c->have_index = true;
   return OVL_OK;
 }
 
-static unsigned long long *dbg_ptr_for_print = nullptr;
+static int clip_hash_range(ovl_ctx *c, uint32_t &bgn, uint32_t &end) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
+  HIPC(hipSetDevice(c->device));
+  if (bgn < 1) bgn = 1;
+  if (bgn < c->first_iid) bgn = c->first_iid;
+  uint32_t last = c->first_iid + c->nreads - 1;
+  if (end > last) end = last;
+  return OVL_OK;
+}
+
+int ovl_build_hash_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
+  int rc = clip_hash_range(c, bgn, end);
+  if (rc) return rc;
+  c->stats_hash_lib_lo = 0;
+  c->stats_hash_lib_hi = UINT32_MAX;
+  if ((rc = apply_hash_libs(c, 0, UINT32_MAX))) return rc;
+  c->stats.ms_index = 0;
+  return build_index(c, bgn, end);
+}
+
+int ovl_set_read_libraries(ovl_ctx *c, const uint32_t *lib_ids) {
+  if (!c) return fail(OVL_ERR_STATE, "null context");
+  if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
+  if (!lib_ids) { c->h_lib.clear(); return OVL_OK; }
+  c->h_lib.assign(lib_ids, lib_ids + c->nreads);
+  c->have_index = false;
+  return OVL_OK;
+}
+
+void ovl_hash_limits_init(ovl_hash_limits *l) {
+  l->max_hash_strings = 10000;
+  l->max_hash_data_len = 100000000ull;
+  l->hash_mask_bits = 22;
+  l->max_hash_load = 0.6;
+  l->min_lib_hash = 0;
+  l->max_lib_hash = UINT32_MAX;
+}
+
+void ovl_driver_params_init(ovl_driver_params *d) {
+  d->bgn_hash_iid = 1;
+  d->end_hash_iid = UINT32_MAX;
+  d->bgn_ref_iid = 1;
+  d->end_ref_iid = UINT32_MAX;
+  d->min_lib_ref = 0;
+  d->max_lib_ref = UINT32_MAX;
+  d->num_threads = 1;
+  d->store_num_reads = 0;
+  ovl_hash_limits_init(&d->limits);
+}
+
+static const uint32_t ENTRIES_PER_BUCKET = 21;          // overlapInCore.H:102
+static const uint64_t MAX_STRING_NUM = (1ull << 31) - 1; // overlapInCore.C:57-63
+
+// Build_Hash_Index's loading loop (overlapInCore-Build_Hash_Index.C:495-541): before each
+// read it requires String_Ct < Max_Hash_Strings, total_len < Max_Hash_Data_Len and
+// Hash_Entries < hash_entry_limit.  String_Ct counts every ID (skipped reads too);
+// total_len grows by len + 1 per loaded read; Hash_Entries by the k-mers a read brings
+// that no earlier read of the batch holds.  The first two are known from the lengths; the
+// third needs the batch's k-mers, so the index is built over the first two's range and its
+// first-occurrence histogram decides -- rebuilding the shorter batch when the table load
+// stops it earlier.
+static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_hash_limits *L,
+                            uint32_t *last_iid) {
+  int rc = clip_hash_range(c, bgn, end);
+  if (rc) return rc;
+  if (!L) return fail(OVL_ERR_BAD_PARAM, "null limits");
+  if (L->max_hash_strings == 0) return fail(OVL_ERR_BAD_PARAM, "no memory model (--hashstrings 0)");
+  if (L->hash_mask_bits == 0 || L->hash_mask_bits > 40)
+    return fail(OVL_ERR_BAD_PARAM, "--hashbits %u", L->hash_mask_bits);
+  if (end < bgn) return fail(OVL_ERR_BAD_PARAM, "empty hash range %u-%u", bgn, end);
+  const uint32_t k = c->P.kmer_len;
+  auto loadable = [&](uint32_t r) {
+    uint32_t lib = read_lib(c, r);
+    return lib >= L->min_lib_hash && lib <= L->max_lib_hash &&
+           (int64_t)c->h_len[r] >= (int64_t)c->P.min_olap_len;
+  };
+  // :495-523 -- the allocation pass counts every loadable read up to endID; the reference
+  // asserts when that exceeds the data limit by more than one maximal read
+  uint64_t max_alloc = 0;
+  for (uint32_t id = bgn; id <= end && id >= bgn; id++)
+    if (loadable(id - c->first_iid)) max_alloc += c->h_len[id - c->first_iid] + 1;
+  if (max_alloc >= L->max_hash_data_len + AS_MAX_READLEN)
+    return fail(OVL_ERR_BAD_PARAM,
+                "hash range %u-%u holds %llu bases, more than --hashdatalen %llu + "
+                "AS_MAX_READLEN (Build_Hash_Index.C:523 asserts)", bgn, end,
+                (unsigned long long)max_alloc, (unsigned long long)L->max_hash_data_len);
+  // strings and bases
+  uint32_t e = end;
+  uint64_t total = 0, windows = 0;
+  for (uint32_t id = bgn;; id++) {
+    uint32_t r = id - c->first_iid;
+    if (loadable(r)) {
+      total += c->h_len[r] + 1;
+      if (c->h_len[r] >= k) windows += c->h_len[r] - k + 1;
+    }
+    if (id == end) break;
+    if ((uint64_t)(id + 1 - bgn) >= L->max_hash_strings || total >= L->max_hash_data_len) {
+      e = id;
+      break;
+    }
+  }
+  c->stats_hash_lib_lo = L->min_lib_hash;
+  c->stats_hash_lib_hi = L->max_lib_hash;
+  if ((rc = apply_hash_libs(c, L->min_lib_hash, L->max_lib_hash))) return rc;
+  if ((rc = build_index(c, bgn, e))) return rc;
+  // table load: at most one entry per window, so only a batch with more windows than the
+  // limit can be stopped by it
+  const uint64_t entry_limit =
+      (uint64_t)(L->max_hash_load * (double)(1ull << L->hash_mask_bits) * (double)ENTRIES_PER_BUCKET);
+  if (windows >= entry_limit && e > bgn) {
+    hipStream_t s = c->stream;
+    uint32_t nr = e - bgn + 1;
+    DBuf<uint32_t> hist;
+    if (hist.alloc(nr)) return fail(OVL_ERR_OOM, "first-read histogram");
+    HIPC(hipMemsetAsync(hist.p, 0, 4ull * nr, s));
+    uint32_t n = (uint32_t)c->index_records;
+    if (n)
+      hipLaunchKernelGGL(k_first_reads, dim3(std::min<uint32_t>((n + 255) / 256, 16384)), dim3(256),
+                         0, s, c->d_tmpM2.p, c->d_occ.p, n, bgn, hist.p);
+    HIPC(hipGetLastError());
+    std::vector<uint32_t> h(nr);
+    HIPC(hipMemcpyAsync(h.data(), hist.p, 4ull * nr, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    uint64_t entries = 0;
+    uint32_t el = e;
+    for (uint32_t i = 0; i < nr; i++) {
+      entries += h[i];
+      if (entries >= entry_limit) { el = bgn + i; break; }
+    }
+    if (el < e) {
+      e = el;
+      if ((rc = build_index(c, bgn, e))) return rc;
+    }
+  }
+  *last_iid = e;
+  return OVL_OK;
+}
+
+int ovl_build_hash_batch(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_hash_limits *L,
+                         uint32_t *last_iid) {
+  if (c) c->stats.ms_index = 0;
+  return build_batch_impl(c, bgn, end, L, last_iid);
+}
 
 IndexDev index_dev(const ovl_ctx *c) {
   IndexDev X;
@@ -608,7 +802,11 @@ IndexDev index_dev(const ovl_ctx *c) {
   return X;
 }
 
-int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+// Process_Overlaps (overlapInCore-Process_Overlaps.C:101-137) over ref reads bgn..end of
+// libraries [lib_lo, lib_hi] against the current index.  append: keep the records and
+// counters already held (the driver's later hash batches).
+static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, uint32_t lib_hi,
+                     bool append, uint64_t *n_out) {
   if (!c) return fail(OVL_ERR_STATE, "null context");
   if (!c->have_index) return fail(OVL_ERR_STATE, "ovl_build_hash_index() first");
   HIPC(hipSetDevice(c->device));
@@ -622,20 +820,29 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   // units: (query, FORWARD), (query, REVERSE) -- Process_Overlaps.C:124-128
   std::vector<Unit> units;
   std::vector<uint64_t> uwin;
+  uint64_t nref = 0;
   for (uint32_t a = bgn; a <= end && a >= bgn; a++) {
     uint32_t r = a - c->first_iid;
     int32_t L = (int32_t)c->h_len[r];
-    if (L < c->P.min_olap_len || L < (int32_t)k) continue;
+    uint32_t lib = read_lib(c, r);
+    if (lib < lib_lo || lib > lib_hi) continue;  // -R (Process_Overlaps.C:108)
+    if (L < c->P.min_olap_len) continue;         // :114
+    nref++;
+    if (L < (int32_t)k) continue;
     if (a >= c->hash_end_iid) continue;          // no hash read with a larger ID
     units.push_back(Unit{r, 0});
     units.push_back(Unit{r, 1});
     uwin.push_back((uint64_t)(L - (int32_t)k + 1));
     uwin.push_back((uint64_t)(L - (int32_t)k + 1));
   }
-  ovl_stats keep_idx = c->stats;
-  memset(&c->stats, 0, sizeof(c->stats));
-  c->stats.ms_index = keep_idx.ms_index;
-  c->nout = 0;
+  if (!append) {
+    ovl_stats keep_idx = c->stats;
+    memset(&c->stats, 0, sizeof(c->stats));
+    c->stats.ms_index = keep_idx.ms_index;
+    c->stats.hash_batches = 1;
+    c->nout = 0;
+  }
+  c->stats.ref_reads += nref;
 
   // per-context device buffers, sized per batch
   // A batch is sized by seed hits (node pool + list-ordered copy: 32 B per hit); the probe
@@ -878,10 +1085,11 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     EA.overflow = d_ctr.p + 7;
     EA.dbg = nullptr;
     if (getenv("OVL_DEBUG")) {
-      static DBuf<unsigned long long> dbgbuf;
-      if (!dbgbuf.p) { (void)dbgbuf.alloc(32); (void)hipMemset(dbgbuf.p, 0, 256); }
-      EA.dbg = dbgbuf.p;
-      dbg_ptr_for_print = dbgbuf.p;
+      if (!c->dbg.p) {
+        if (c->dbg.alloc(32)) return fail(OVL_ERR_OOM, "debug counters");
+        HIPC(hipMemsetAsync(c->dbg.p, 0, 256, s));
+      }
+      EA.dbg = c->dbg.p;
     }
     EA.list = nullptr;
     EA.defer = nullptr;
@@ -956,9 +1164,9 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   }
   unsigned long long hs[16];
   HIPC(hipMemcpy(hs, d_stats.p, 128, hipMemcpyDeviceToHost));
-  if (dbg_ptr_for_print) {
+  if (c->dbg.p) {
     unsigned long long dd[32];
-    (void)hipMemcpy(dd, dbg_ptr_for_print, 256, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(dd, c->dbg.p, 256, hipMemcpyDeviceToHost);
     fprintf(stderr, "OVL_DEBUG cyc_A=%llu cyc_B=%llu cyc_cont=%llu cyc_C=%llu\n", dd[16], dd[17],
             dd[18], dd[19]);
     fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu slide_iters=%llu tb=%llu iters=%llu "
@@ -967,23 +1175,87 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
             dd[0], dd[1], dd[2], dd[3], dd[4], dd[5], dd[6], dd[7], dd[8], dd[9], dd[10], dd[11],
             dd[12], dd[13], dd[14], dd[15]);
   }
-  c->stats.kmer_hits_without_olap = hs[0];
-  c->stats.kmer_hits_with_olap = hs[1];
-  c->stats.kmer_hits_skipped = hs[2];
-  c->stats.multi_overlaps = hs[3];
-  c->stats.total_overlaps = hs[4];
-  c->stats.contained_overlaps = hs[5];
-  c->stats.dovetail_overlaps = hs[6];
-  c->stats.seed_hits = hs[7];
-  c->stats.bad_short_window = hs[8];
-  c->stats.bad_long_window = hs[9];
-  c->stats.pairs = npairs_tot;
-  c->stats.ms_seed = ms_probe + ms_chain;
-  c->stats.ms_extend = ms_ext;
-  c->stats.ms_probe_kernel = ms_probe;
-  c->stats.probe_bytes = probe_bytes;
-  c->stats.probe_launches = n_probe_launch;
-  c->stats.extend_launches = n_ext_launch;
+  // counters add up over the driver's hash batches (the reference sums its per-thread
+  // counters into globals, Process_Overlaps.C:156-163)
+  c->stats.kmer_hits_without_olap += hs[0];
+  c->stats.kmer_hits_with_olap += hs[1];
+  c->stats.kmer_hits_skipped += hs[2];
+  c->stats.multi_overlaps += hs[3];
+  c->stats.total_overlaps += hs[4];
+  c->stats.contained_overlaps += hs[5];
+  c->stats.dovetail_overlaps += hs[6];
+  c->stats.seed_hits += hs[7];
+  c->stats.bad_short_window += hs[8];
+  c->stats.bad_long_window += hs[9];
+  c->stats.pairs += npairs_tot;
+  c->stats.ms_seed += ms_probe + ms_chain;
+  c->stats.ms_extend += ms_ext;
+  c->stats.ms_probe_kernel += ms_probe;
+  c->stats.probe_bytes += probe_bytes;
+  c->stats.probe_launches += n_probe_launch;
+  c->stats.extend_launches += n_ext_launch;
+  *n_out = c->nout;
+  return OVL_OK;
+}
+
+int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+  return find_impl(c, bgn, end, 0, UINT32_MAX, false, n_out);
+}
+
+// OverlapDriver (overlapInCore.C:190-300).
+int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) {
+  if (!c || !d || !n_out) return fail(OVL_ERR_STATE, "null argument");
+  if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
+  const ovl_hash_limits &L = d->limits;
+  if (L.max_hash_strings == 0)                                    // main() :423
+    return fail(OVL_ERR_BAD_PARAM, "No memory model supplied; -M needed!");
+  if (L.max_hash_strings > MAX_STRING_NUM)                        // :429
+    return fail(OVL_ERR_BAD_PARAM, "Too many strings (--hashstrings), must be less than %llu",
+                (unsigned long long)MAX_STRING_NUM);
+  HIPC(hipSetDevice(c->device));
+  const uint32_t last_loaded = c->first_iid + c->nreads - 1;
+  const uint32_t num_reads = d->store_num_reads ? d->store_num_reads : last_loaded;
+  uint32_t g_bgn_hash = std::max<uint32_t>(d->bgn_hash_iid, 1);          // :208-212
+  uint32_t g_end_hash = std::min<uint32_t>(d->end_hash_iid, num_reads);
+  uint32_t g_bgn_ref = std::max<uint32_t>(d->bgn_ref_iid, 1);            // :237-241
+  uint32_t g_end_ref = std::min<uint32_t>(d->end_ref_iid, num_reads);
+  // every read the job touches must be loaded
+  if ((g_bgn_hash < g_end_hash && (g_bgn_hash < c->first_iid || g_end_hash > last_loaded)) ||
+      (g_bgn_ref < g_end_ref && (g_bgn_ref < c->first_iid || g_end_ref > last_loaded)))
+    return fail(OVL_ERR_BAD_PARAM, "-h %u-%u / -r %u-%u reach past the loaded reads %u-%u",
+                g_bgn_hash, g_end_hash, g_bgn_ref, g_end_ref, c->first_iid, last_loaded);
+  // Process_Overlaps' block schedule (:249-269, Process_Overlaps.C:86-171): blocks of
+  // perThread reads from bgnRefID on, each searched only while it starts below endRefID --
+  // the reads before endRefID always, endRefID itself unless a block starts on it.
+  uint32_t ref_last = 0;
+  bool any_ref = false;
+  if (g_bgn_ref < g_end_ref) {
+    uint32_t T = std::max<uint32_t>(d->num_threads, 1);
+    uint32_t per = 1 + (g_end_ref - g_bgn_ref) / T / 8;
+    ref_last = ((g_end_ref - g_bgn_ref) % per == 0) ? g_end_ref - 1 : g_end_ref;
+    any_ref = true;
+  }
+  memset(&c->stats, 0, sizeof(c->stats));
+  c->nout = 0;
+  uint32_t bgn = g_bgn_hash;
+  uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
+  uint64_t batches = 0;
+  while (bgn < g_end_hash) {                                             // :222
+    if (end > g_end_hash) end = g_end_hash;
+    uint32_t loaded = 0;
+    int rc = build_batch_impl(c, bgn, end, &L, &loaded);
+    if (rc) return rc;
+    end = loaded;
+    batches++;
+    if (any_ref) {
+      uint64_t n = 0;
+      if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n)))
+        return rc;
+    }
+    bgn = end + 1;
+    end = bgn + L.max_hash_strings - 1;
+  }
+  c->stats.hash_batches = batches;
   *n_out = c->nout;
   return OVL_OK;
 }

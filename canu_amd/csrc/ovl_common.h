@@ -189,6 +189,11 @@ __device__ __host__ __forceinline__ uint64_t mix64(uint64_t z) {
 // occurrences plus flags (OVL_PRESENT on every filled slot, OVL_FLAG_SKIP).  Occurrence lists hold
 // (iid << 32 | offset) sorted DESCENDING, i.e. in Hash_Insert's chain order
 // (Build_Hash_Index.C:320-323 pushes every new entry in front).
+// Per-read flags (ReadsDev::flags): bit 0 the read holds an 'n'; bits 1 / 2 its left /
+// right end is screened (String_Info lfrag/rfrag_end_screened); bit 3 the read is not
+// hashed (outside the -H libraries).
+#define OVL_RFLAG_NOHASH 8u
+
 #define OVL_CNT_MASK    0x3FFFFFFFu
 #define OVL_PRESENT     0x40000000u
 #define OVL_FLAG_SKIP   0x80000000u      // k-mer from the -k skip list (Empty entry)

@@ -116,7 +116,8 @@ __device__ __forceinline__ void for_block_windows(const BuildArgs &A, F &&fn) {
   if (re > A.h1) re = A.h1;
   for (uint32_t r = rb; r < re; r++) {
     int32_t L = (int32_t)A.R.len[r];
-    if (L < A.min_len || L < (int32_t)A.k) continue;
+    // shorter than --minlength, or outside the -H libraries (Build_Hash_Index.C:554-561)
+    if (L < A.min_len || L < (int32_t)A.k || (A.R.flags[r] & OVL_RFLAG_NOHASH)) continue;
     uint64_t wo = A.R.wofs[r];
     const uint64_t *w = A.R.fwd + wo;
     const uint32_t *nm = (A.R.flags[r] & 1u) ? A.R.fwdN + wo : nullptr;
@@ -446,6 +447,21 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
     e.off = oc[2 * i];
     e.cnt = oc[2 * i + 1];
     dst[i] = e;
+  }
+}
+
+// Hash_Entries of Build_Hash_Index (Hash_Insert :336-341): a distinct k-mer takes a table
+// entry when its first occurrence is loaded, i.e. at the lowest read ID that holds it.  A
+// sorted run (one k-mer) ends at its lowest position, so the run's last record names that
+// read; runs of skip markers alone are not k-mers of the batch.  hist[r - h0] counts the
+// k-mers whose first read is r.
+__global__ void k_first_reads(const uint64_t *__restrict__ M, const uint64_t *__restrict__ P,
+                              uint32_t n, uint32_t h0_iid, uint32_t *hist) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t p = P[i];
+    if (p == OVL_SKIP_POS) continue;
+    if (i + 1 < n && M[i + 1] == M[i]) continue;
+    atomicAdd(&hist[(uint32_t)(p >> 32) - h0_iid], 1u);
   }
 }
 

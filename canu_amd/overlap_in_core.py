@@ -54,7 +54,22 @@ class _Stats(ctypes.Structure):
          ("ms_extend", ctypes.c_double), ("ms_probe_kernel", ctypes.c_double),
          ("probe_bytes", ctypes.c_uint64), ("probe_launches", ctypes.c_uint32),
          ("extend_launches", ctypes.c_uint32), ("bad_short_window", ctypes.c_uint64),
-         ("bad_long_window", ctypes.c_uint64)]
+         ("bad_long_window", ctypes.c_uint64), ("hash_batches", ctypes.c_uint64),
+         ("ref_reads", ctypes.c_uint64)]
+
+
+class _HashLimits(ctypes.Structure):
+    _fields_ = [("max_hash_strings", ctypes.c_uint32), ("max_hash_data_len", ctypes.c_uint64),
+                ("hash_mask_bits", ctypes.c_uint32), ("max_hash_load", ctypes.c_double),
+                ("min_lib_hash", ctypes.c_uint32), ("max_lib_hash", ctypes.c_uint32)]
+
+
+class _DriverParams(ctypes.Structure):
+    _fields_ = [("bgn_hash_iid", ctypes.c_uint32), ("end_hash_iid", ctypes.c_uint32),
+                ("bgn_ref_iid", ctypes.c_uint32), ("end_ref_iid", ctypes.c_uint32),
+                ("min_lib_ref", ctypes.c_uint32), ("max_lib_ref", ctypes.c_uint32),
+                ("num_threads", ctypes.c_uint32), ("store_num_reads", ctypes.c_uint32),
+                ("limits", _HashLimits)]
 
 
 # Every symbol include/canu_ovl.h declares (tests check the library exports them all).
@@ -62,7 +77,9 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
            "ovl_last_error", "ovl_abi_version", "ovl_load_reads", "ovl_load_reads_device",
            "ovl_set_skip_kmers", "ovl_build_hash_index", "ovl_find_overlaps",
            "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream", "ovl_write_ovb",
-           "ovl_ctx_write_ovb", "ovl_ctx_write_stats"]
+           "ovl_ctx_write_ovb", "ovl_ctx_write_stats", "ovl_set_read_libraries",
+           "ovl_hash_limits_init", "ovl_build_hash_batch", "ovl_driver_params_init",
+           "ovl_overlap_driver"]
 
 _lib = None
 
@@ -99,6 +116,12 @@ def load_library(path: str | None = None):
     lib.ovl_write_ovb.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
     lib.ovl_ctx_write_ovb.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.ovl_ctx_write_stats.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.ovl_set_read_libraries.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.ovl_hash_limits_init.argtypes = [P(_HashLimits)]
+    lib.ovl_build_hash_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                         P(_HashLimits), P(ctypes.c_uint32)]
+    lib.ovl_driver_params_init.argtypes = [P(_DriverParams)]
+    lib.ovl_overlap_driver.argtypes = [ctypes.c_void_p, P(_DriverParams), P(ctypes.c_uint64)]
     _lib = lib
     return lib
 
@@ -119,6 +142,15 @@ class OicParameters:
     endHashID: int = 0xFFFFFFFF
     bgnRefID: int = 1
     endRefID: int = 0xFFFFFFFF
+    minLibToHash: int = 0
+    maxLibToHash: int = 0xFFFFFFFF
+    minLibToRef: int = 0
+    maxLibToRef: int = 0xFFFFFFFF
+    Hash_Mask_Bits: int = 22
+    Max_Hash_Load: float = 0.6
+    Max_Hash_Strings: int = 10000
+    Max_Hash_Data_Len: int = 100000000
+    Num_PThreads: int = 1
 
     def finalize(self) -> "OicParameters":
         """main()'s fix-ups after option parsing (overlapInCore.C:416-421)."""
@@ -135,6 +167,20 @@ class OicParameters:
                        use_hopeless_check=int(self.Use_Hopeless_Check),
                        frag_olap_limit=self.Frag_Olap_Limit,
                        filter_by_kmer_count=self.Filter_By_Kmer_Count)
+
+    def driver_c(self, store_num_reads: int = 0) -> _DriverParams:
+        d = _DriverParams()
+        load_library().ovl_driver_params_init(ctypes.byref(d))
+        d.bgn_hash_iid, d.end_hash_iid = self.bgnHashID, min(self.endHashID, 0xFFFFFFFF)
+        d.bgn_ref_iid, d.end_ref_iid = self.bgnRefID, min(self.endRefID, 0xFFFFFFFF)
+        d.min_lib_ref, d.max_lib_ref = self.minLibToRef, self.maxLibToRef
+        d.num_threads = self.Num_PThreads
+        d.store_num_reads = store_num_reads
+        L = d.limits
+        L.max_hash_strings, L.max_hash_data_len = self.Max_Hash_Strings, self.Max_Hash_Data_Len
+        L.hash_mask_bits, L.max_hash_load = self.Hash_Mask_Bits, self.Max_Hash_Load
+        L.min_lib_hash, L.max_lib_hash = self.minLibToHash, self.maxLibToHash
+        return d
 
     def as_dict(self) -> dict:
         return dict(kmer_len=self.Kmer_Len, max_erate=self.maxErate,
@@ -158,7 +204,7 @@ def parse_overlapInCore_args(argv: list[str]) -> tuple[OicParameters, dict]:
     """Parse overlapInCore's command line (overlapInCore.C:316-412) the way main() does:
     --maxerate through strtof (a float), --minkmers evaluated where it appears."""
     P = OicParameters()
-    extra = {"skip_file": None, "store": None, "output": None, "threads": 1}
+    extra = {"skip_file": None, "store": None, "output": None, "threads": 1, "stats": None}
     i = 0
     while i < len(argv):
         a = argv[i]
@@ -168,6 +214,20 @@ def parse_overlapInCore_args(argv: list[str]) -> tuple[OicParameters, dict]:
             i += 1; P.bgnHashID, P.endHashID = _decode_range(argv[i])
         elif a == "-r":
             i += 1; P.bgnRefID, P.endRefID = _decode_range(argv[i])
+        elif a == "-H":
+            i += 1; P.minLibToHash, P.maxLibToHash = _decode_range(argv[i])
+        elif a == "-R":
+            i += 1; P.minLibToRef, P.maxLibToRef = _decode_range(argv[i])
+        elif a == "--hashbits":
+            i += 1; P.Hash_Mask_Bits = int(argv[i])
+        elif a == "--hashstrings":
+            i += 1; P.Max_Hash_Strings = int(argv[i])
+        elif a == "--hashdatalen":
+            i += 1; P.Max_Hash_Data_Len = int(argv[i])
+        elif a == "--hashload":
+            i += 1; P.Max_Hash_Load = float(argv[i])
+        elif a == "-s":
+            i += 1; extra["stats"] = argv[i]
         elif a == "-k":
             i += 1
             v = argv[i]
@@ -197,10 +257,9 @@ def parse_overlapInCore_args(argv: list[str]) -> tuple[OicParameters, dict]:
         elif a == "-o":
             i += 1; extra["output"] = argv[i]
         elif a == "-t":
-            i += 1; extra["threads"] = int(argv[i])
-        elif a in ("--hashbits", "--hashstrings", "--hashdatalen", "--hashload", "-s",
-                   "--maxreadlen", "-H", "-R"):
-            i += 1      # CPU hash-table sizing / stats options: not needed on this path
+            i += 1; extra["threads"] = P.Num_PThreads = int(argv[i])
+        elif a == "--maxreadlen":
+            i += 1      # the CPU table's bit packing of (read, offset); no limit here
         else:
             extra["store"] = a
         i += 1
@@ -313,6 +372,33 @@ class OverlapInCore:
     def write_stats(self, path: str) -> None:
         """overlapInCore's -s statistics file."""
         self._check(self.lib.ovl_ctx_write_stats(self.ctx, path.encode()))
+
+    def set_read_libraries(self, libs) -> None:
+        lib = np.ascontiguousarray(libs, dtype=np.uint32)
+        assert lib.shape[0] == self.nreads
+        self._check(self.lib.ovl_set_read_libraries(self.ctx, lib.ctypes.data))
+
+    def build_hash_batch(self, bgn: int, end: int) -> int:
+        """Build_Hash_Index(gkpStore, bgn, end): returns the last ID the batch loaded."""
+        d = self.params.driver_c()
+        last = ctypes.c_uint32()
+        self._check(self.lib.ovl_build_hash_batch(self.ctx, bgn, min(end, 0xFFFFFFFF),
+                                                  ctypes.byref(d.limits), ctypes.byref(last)))
+        return last.value
+
+    def overlap_driver(self, store_num_reads: int = 0) -> int:
+        """OverlapDriver(): every hash batch of the -h range searched by the -r reads."""
+        d = self.params.driver_c(store_num_reads)
+        n = ctypes.c_uint64()
+        self._check(self.lib.ovl_overlap_driver(self.ctx, ctypes.byref(d), ctypes.byref(n)))
+        return n.value
+
+    def run_driver(self, rs, skip_kmers=None) -> np.ndarray:
+        """The whole overlapInCore job (hash batches, Process_Overlaps' ref schedule)."""
+        self.load_reads(rs)
+        if skip_kmers:
+            self.set_skip_kmers(skip_kmers)
+        return self.fetch(self.overlap_driver())
 
     def run(self, rs, skip_kmers=None) -> np.ndarray:
         """OverlapDriver() for one hash batch: load, index, search, fetch (sorted)."""

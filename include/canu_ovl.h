@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 1
+#define OVL_ABI_VERSION 2
 
 typedef enum {
   OVL_OK               =  0,
@@ -116,8 +116,58 @@ int         ovl_load_reads_device(ovl_ctx *ctx, uint32_t first_iid, uint32_t nre
  * screened, as the reference does. Must be called before ovl_build_hash_index(). */
 int         ovl_set_skip_kmers(ovl_ctx *ctx, const char *kmers, uint64_t n_kmers);
 
-/* Build the k-mer index over hash reads bgn_iid..end_iid (inclusive, like -h). */
+/* Build the k-mer index over hash reads bgn_iid..end_iid (inclusive, like -h), all of them
+ * in one index (no batch limits). */
 int         ovl_build_hash_index(ovl_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);
+
+/* Library IDs of the loaded reads (gkRead_libraryID), for the -H / -R filters of the
+ * driver below.  Without this call every read is in library 0.  lib_ids: one per loaded
+ * read, in load order. */
+int         ovl_set_read_libraries(ovl_ctx *ctx, const uint32_t *lib_ids);
+
+/* How much of the -h range one hash batch holds: the loading rules of Build_Hash_Index
+ * (overlapInCore-Build_Hash_Index.C:495-541, defaults oicParameters::initialize(),
+ * overlapInCore.H:447-450). */
+typedef struct {
+  uint32_t max_hash_strings;      /* --hashstrings  G.Max_Hash_Strings  (10000)          */
+  uint64_t max_hash_data_len;     /* --hashdatalen  G.Max_Hash_Data_Len (100000000)      */
+  uint32_t hash_mask_bits;        /* --hashbits     G.Hash_Mask_Bits    (22)             */
+  double   max_hash_load;         /* --hashload     G.Max_Hash_Load     (0.6)            */
+  uint32_t min_lib_hash;          /* -H             G.minLibToHash      (0)              */
+  uint32_t max_lib_hash;          /*                G.maxLibToHash      (UINT32_MAX)     */
+} ovl_hash_limits;
+
+void        ovl_hash_limits_init(ovl_hash_limits *l);
+
+/* Build_Hash_Index(gkpStore, bgnID, endID) (overlapInCore-Build_Hash_Index.C:443): index
+ * hash reads from bgn_iid on, stopping where the reference stops loading -- after
+ * max_hash_strings IDs, once max_hash_data_len bases (+1 per read) are in, or once the
+ * distinct k-mers reach max_hash_load * 2^hash_mask_bits * 21 table entries -- and return
+ * the last ID loaded in *last_iid.  Reads outside [min_lib_hash, max_lib_hash] or shorter
+ * than min_olap_len are not hashed (they still count as strings).  Fails with
+ * OVL_ERR_BAD_PARAM where the reference asserts (:523: more than max_hash_data_len +
+ * AS_MAX_READLEN bases in bgn..end). */
+int         ovl_build_hash_batch(ovl_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid,
+                                 const ovl_hash_limits *lim, uint32_t *last_iid);
+
+/* OverlapDriver() (overlapInCore.C:190-300): the whole job.  Hash batches over the -h range
+ * (ovl_build_hash_batch; a batch starts only while its first ID is below the range end,
+ * :222), each searched by the -r reads (Process_Overlaps, both orientations) as the
+ * reference's -t threads would take them in blocks (:249-269, Process_Overlaps.C:86: a
+ * block that starts at the range end is not searched).  -h / -r ends are clipped to
+ * store_num_reads (0 = the last loaded ID).  Records and counters of all batches
+ * accumulate: ovl_fetch_overlaps / ovl_get_stats / ovl_ctx_write_* then see the job. */
+typedef struct {
+  uint32_t bgn_hash_iid, end_hash_iid;   /* -h  (1, UINT32_MAX)                         */
+  uint32_t bgn_ref_iid, end_ref_iid;     /* -r  (1, UINT32_MAX)                         */
+  uint32_t min_lib_ref, max_lib_ref;     /* -R  (0, UINT32_MAX)                         */
+  uint32_t num_threads;                  /* -t  (1): only the ref block schedule uses it */
+  uint32_t store_num_reads;              /* gkStore_getNumReads(), 0 = last loaded ID   */
+  ovl_hash_limits limits;
+} ovl_driver_params;
+
+void        ovl_driver_params_init(ovl_driver_params *d);
+int         ovl_overlap_driver(ovl_ctx *ctx, const ovl_driver_params *d, uint64_t *n_out);
 
 /* Search ref reads bgn_iid..end_iid (inclusive, like -r) against the index, both
  * orientations, and keep the resulting records on the device. Returns the number of
@@ -151,6 +201,8 @@ typedef struct {
   uint32_t extend_launches;        /* k_extend launches (staged + generic)             */
   uint64_t bad_short_window;       /* -w rejections, Bad_Short_Window_Ct               */
   uint64_t bad_long_window;        /* -w rejections, Bad_Long_Window_Ct                */
+  uint64_t hash_batches;           /* hash batches of the last driver run (1 otherwise) */
+  uint64_t ref_reads;              /* query reads searched (both orientations each)    */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

@@ -148,6 +148,21 @@ def read_ovb_reference(path: str) -> np.ndarray:
         return np.fromfile(out, dtype=RECORD_DTYPE)
 
 
+def build_gkpstore(rs, workdir: str) -> str:
+    """A real gkpStore of rs, written by the reference's own gkStore code
+    (oic_ref --gkp-only, ref_harness.cpp); returns its path (<workdir>/ref.gkpStore)."""
+    from canu_amd.synth import write_reads_file  # input writer only
+    if not reference_available():
+        raise FileNotFoundError(REF_BIN)
+    reads = os.path.join(workdir, "reads.bin")
+    write_reads_file(reads, rs)
+    cp = subprocess.run([REF_BIN, reads, os.path.join(workdir, "w"), "-", "--gkp-only"],
+                        capture_output=True, text=True)
+    if cp.returncode != 0:
+        raise RuntimeError(f"oic_ref --gkp-only failed: {cp.stderr[-2000:]}")
+    return os.path.join(workdir, "w", "ref.gkpStore")
+
+
 MHAPCONVERT_BIN = os.path.join(HERE, "_ref", "mhapConvert")
 
 
@@ -197,13 +212,114 @@ def params_to_ref_args(params: dict) -> list[str]:
     return a
 
 
+UINT32_MAX = 0xFFFFFFFF
+ENTRIES_PER_BUCKET = 21                       # overlapInCore.H:102
+
+
+def first_read_kmers(rs, bgn: int, end: int, k: int, loadable) -> np.ndarray:
+    """Per read bgn..end: how many distinct k-mers of the batch first occur in it -- the
+    Hash_Entries growth of Hash_Insert (Build_Hash_Index.C:336-341).  Windows holding a
+    non-ACGT base are not hashed (key_is_bad, :392-425)."""
+    lut = np.full(256, 255, dtype=np.uint8)
+    for i, ch in enumerate(b"acgt"):
+        lut[ch] = i
+        lut[ord(chr(ch).upper())] = i
+    codes, owner = [], []
+    for iid in range(bgn, end + 1):
+        r = iid - rs.first_iid
+        if not loadable(r):
+            continue
+        b = lut[np.frombuffer(rs.read(r), dtype=np.uint8)]
+        L = b.shape[0]
+        if L < k:
+            continue
+        win = np.lib.stride_tricks.sliding_window_view(b, k)
+        ok = (win != 255).all(axis=1)
+        w = win[ok].astype(np.uint64)
+        c = (w << (2 * np.arange(k, dtype=np.uint64))).sum(axis=1, dtype=np.uint64)
+        codes.append(c)
+        owner.append(np.full(c.shape[0], iid - bgn, dtype=np.int64))
+    hist = np.zeros(end - bgn + 1, dtype=np.int64)
+    if codes:
+        allc = np.concatenate(codes)
+        allo = np.concatenate(owner)
+        _, first = np.unique(allc, return_index=True)
+        hist += np.bincount(allo[first], minlength=hist.shape[0])
+    return hist
+
+
+def hash_batch_end(rs, params: dict, bgn: int, end: int, hashstrings: int, hashdatalen: int,
+                   hashbits: int, hashload: float) -> int:
+    """Build_Hash_Index's loading loop (overlapInCore-Build_Hash_Index.C:495-541): the last
+    ID it loads from bgn on.  Raises where the reference asserts (:523)."""
+    AS_MAX_READLEN = (1 << 21) - 1
+    lens = rs.lengths
+    minlen = params["min_olap_len"]
+    loadable = lambda r: int(lens[r]) >= minlen
+    max_alloc = sum(int(lens[i - rs.first_iid]) + 1 for i in range(bgn, end + 1)
+                    if loadable(i - rs.first_iid))
+    if max_alloc >= hashdatalen + AS_MAX_READLEN:
+        raise ValueError("Build_Hash_Index.C:523 assert")
+    limit = int(hashload * (1 << hashbits) * ENTRIES_PER_BUCKET)
+    hist = first_read_kmers(rs, bgn, end, params["kmer_len"], loadable)
+    strings = total = entries = 0
+    cur = bgn
+    while strings < hashstrings and total < hashdatalen and entries < limit and cur <= end:
+        r = cur - rs.first_iid
+        if loadable(r):
+            total += int(lens[r]) + 1
+            entries += int(hist[cur - bgn])
+        cur += 1
+        strings += 1
+    return cur - 1
+
+
+def run_oracle_driver(rs, params: dict, hash_range=(1, UINT32_MAX), ref_range=(1, UINT32_MAX),
+                      threads: int = 1, hashstrings: int = 10000, hashdatalen: int = 100000000,
+                      hashbits: int = 22, hashload: float = 0.6, skip_kmers=None,
+                      with_stats=False):
+    """OverlapDriver (overlapInCore.C:190-300) restated over the oracle: hash batches with
+    Build_Hash_Index's loading rules, the `while (bgnHashID < endHashID)` loop (:222), and
+    the ref reads Process_Overlaps' thread blocks actually search (:249-269,
+    Process_Overlaps.C:86: a block starting at endRefID is skipped).  Counters add up over
+    the batches."""
+    nr = rs.first_iid + rs.nreads - 1
+    gbh, geh = max(hash_range[0], 1), min(hash_range[1], nr)
+    gbr, ger = max(ref_range[0], 1), min(ref_range[1], nr)
+    ref_last = None
+    if gbr < ger:
+        per = 1 + (ger - gbr) // max(threads, 1) // 8
+        ref_last = ger - 1 if (ger - gbr) % per == 0 else ger
+    recs, tot, batches = [], None, []
+    bgn, end = gbh, gbh + hashstrings - 1
+    while bgn < geh:
+        end = min(end, geh)
+        end = hash_batch_end(rs, params, bgn, end, hashstrings, hashdatalen, hashbits, hashload)
+        batches.append((bgn, end))
+        if ref_last is not None:
+            rec, st = run_oracle(rs, params, hash_range=(bgn, end), ref_range=(gbr, ref_last),
+                                 skip_kmers=skip_kmers, with_stats=True)
+            recs.append(rec)
+            tot = st if tot is None else {f: tot[f] + st[f] for f in st}
+        bgn, end = end + 1, end + hashstrings
+    rec = sort_records(np.concatenate(recs)) if recs else np.zeros(0, dtype=RECORD_DTYPE)
+    if tot is None:
+        tot = {f: 0 for f, _ in OracleStats._fields_}
+    tot["hash_batches"] = len(batches)
+    if with_stats:
+        return rec, tot, batches
+    return rec
+
+
 def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
                   skip_kmers=None, minkmers: bool = False, extra=None, workdir=None,
-                  with_time=False):
+                  with_time=False, batching: dict | None = None, with_stats=False):
     """Run the reference overlapInCore (built from its sources) on `rs`.
 
-    The whole read set is one hash batch and one ref range, so every pair (a<b) is
-    searched once, as the reference's full -h/-r ranges do."""
+    By default the whole read set is one hash batch and one ref range, so every pair (a<b)
+    is searched once, as the reference's full -h/-r ranges do.  `batching` instead passes
+    the hash-batch options as given ({"hashstrings": .., "hashdatalen": .., "hashload": ..},
+    missing ones at the reference defaults, overlapInCore.H:447-450)."""
     from canu_amd.synth import write_reads_file  # input writer only
     if not reference_available():
         raise FileNotFoundError(REF_BIN)
@@ -214,8 +330,14 @@ def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
         write_reads_file(reads, rs)
         out = os.path.join(wd, "records.bin")
         args = [REF_BIN, reads, os.path.join(wd, "w"), out, "-t", str(threads),
-                "--hashbits", str(hash_bits), "--hashstrings", str(max(rs.nreads + 10, 1000)),
-                "--hashdatalen", str(rs.total_bases() + rs.nreads + 1024), "--time"]
+                "--hashbits", str(hash_bits), "--time"]
+        if batching is None:
+            args += ["--hashstrings", str(max(rs.nreads + 10, 1000)),
+                     "--hashdatalen", str(rs.total_bases() + rs.nreads + 1024)]
+        else:
+            for opt in ("hashstrings", "hashdatalen", "hashload"):
+                if opt in batching:
+                    args += ["--" + opt, str(batching[opt])]
         args += params_to_ref_args(params)
         if minkmers:
             args.append("--minkmers")
@@ -233,13 +355,18 @@ def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
         if cp.returncode != 0:
             raise RuntimeError(f"oic_ref failed ({cp.returncode}): {cp.stderr[-2000:]}")
         secs = None
+        stats = {}
         for line in cp.stdout.splitlines():
             if line.startswith("OVERLAPDRIVER_SECONDS"):
                 secs = float(line.split()[1])
+            if line.startswith("STATS"):
+                stats = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in line.split()[1:]}
         rec = np.fromfile(out, dtype=RECORD_DTYPE)
         rec = sort_records(rec)
         if with_time:
             return rec, secs, wall
+        if with_stats:
+            return rec, stats
         return rec
     finally:
         if own:

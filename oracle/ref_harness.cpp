@@ -28,6 +28,7 @@
  *   -k N  --maxerate F  --minlength N  -G  -m|-u  -w  -z  -l N  --minkmers
  *   --hashbits N  --hashload F  --hashstrings N  --hashdatalen N  -t N
  *   -h a-b  -r a-b  --skip <kmers.fasta>  --time (print wall seconds of OverlapDriver)
+ *   -s <file> (the statistics text main() prints)
  */
 
 #include "overlapInCore.H"
@@ -88,6 +89,7 @@ int main(int argc, char **argv) {
   bool        timeIt   = false;
   bool        gkpOnly  = false;   //  build <workdir>/ref.gkpStore and stop (mhapConvert's -G)
   const char *skipPath = NULL;
+  const char *statPath = NULL;    //  -s: main()'s statistics text (overlapInCore.C:569-591)
 
   for (int arg = 4; arg < argc; arg++) {
     const char *a = argv[arg];
@@ -114,6 +116,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "--skip"))        skipPath = argv[++arg];
     else if (!strcmp(a, "--time"))        timeIt = true;
     else if (!strcmp(a, "--gkp-only"))    gkpOnly = true;
+    else if (!strcmp(a, "-s"))            statPath = argv[++arg];
     else { fprintf(stderr, "unknown option '%s'\n", a); exit(1); }
   }
 
@@ -227,6 +230,21 @@ int main(int argc, char **argv) {
           (unsigned long)Kmer_Hits_Without_Olap_Ct, (unsigned long)Kmer_Hits_With_Olap_Ct,
           (unsigned long)Multi_Overlap_Ct, (unsigned long)Total_Overlaps,
           (unsigned long)Contained_Overlap_Ct, (unsigned long)Dovetail_Overlap_Ct);
+
+  //  the -s file, in the reference's own format (overlapInCore.C:580-588)
+  if (statPath) {
+    FILE *S = fopen(statPath, "w");
+    if (!S) die("can't open -s file");
+    fprintf(S, " Kmer hits without olaps = " F_S64 "\n", Kmer_Hits_Without_Olap_Ct);
+    fprintf(S, "    Kmer hits with olaps = " F_S64 "\n", Kmer_Hits_With_Olap_Ct);
+    fprintf(S, "  Multiple overlaps/pair = " F_S64 "\n", Multi_Overlap_Ct);
+    fprintf(S, " Total overlaps produced = " F_S64 "\n", Total_Overlaps);
+    fprintf(S, "      Contained overlaps = " F_S64 "\n", Contained_Overlap_Ct);
+    fprintf(S, "       Dovetail overlaps = " F_S64 "\n", Dovetail_Overlap_Ct);
+    fprintf(S, "Rejected by short window = " F_S64 "\n", Bad_Short_Window_Ct);
+    fprintf(S, " Rejected by long window = " F_S64 "\n", Bad_Long_Window_Ct);
+    fclose(S);
+  }
 
   //  ---- 4. read the .ovb back with the reference reader ---------------------------------
   gkStore *store = gkStore::gkStore_open(gkp.c_str());

@@ -30,7 +30,42 @@ def test_library_exports_every_declared_symbol(built):
 
 
 def test_abi_version(built):
-    assert oic.load_library().ovl_abi_version() == 1
+    assert oic.load_library().ovl_abi_version() == 2
+
+
+def test_driver_defaults_match_reference(built):
+    """ovl_driver_params_init / ovl_hash_limits_init = oicParameters::initialize()
+    (overlapInCore.H:429-450): -h / -r 1-UINT32_MAX, 10000 strings, 1e8 bases, 22 bits,
+    load 0.6, all libraries, one thread."""
+    lib = oic.load_library()
+    d = oic._DriverParams()
+    lib.ovl_driver_params_init(ctypes.byref(d))
+    assert (d.bgn_hash_iid, d.end_hash_iid, d.bgn_ref_iid, d.end_ref_iid) == \
+        (1, 0xFFFFFFFF, 1, 0xFFFFFFFF)
+    assert (d.min_lib_ref, d.max_lib_ref, d.num_threads, d.store_num_reads) == (0, 0xFFFFFFFF, 1, 0)
+    L = d.limits
+    assert (L.max_hash_strings, L.max_hash_data_len, L.hash_mask_bits) == (10000, 100000000, 22)
+    assert abs(L.max_hash_load - 0.6) < 1e-15
+    assert (L.min_lib_hash, L.max_lib_hash) == (0, 0xFFFFFFFF)
+    assert ctypes.sizeof(oic._HashLimits) == 40 and ctypes.sizeof(oic._DriverParams) == 72
+
+
+@pytest.mark.gpu
+def test_failed_load_leaves_no_reads(built):
+    """A load the GPU path rejects leaves the context without reads: a later build is a
+    call-order error, not a kernel over stale buffers."""
+    o = oic.OverlapInCore(oic.OicParameters(Kmer_Len=22), device=0)
+    lib = o.lib
+    bases = np.frombuffer(b"ACGTXACGT" * 100, dtype=np.uint8).copy()
+    offs = np.array([0], dtype=np.uint64)
+    lens = np.array([bases.shape[0]], dtype=np.uint32)
+    rc = lib.ovl_load_reads(o.ctx, 1, 1, bases.ctypes.data, offs.ctypes.data,
+                            lens.ctypes.data, None)
+    assert rc == -4
+    assert lib.ovl_build_hash_index(o.ctx, 1, 1) == -7
+    n = ctypes.c_uint64()
+    assert lib.ovl_find_overlaps(o.ctx, 1, 1, ctypes.byref(n)) == -7
+    o.close()
 
 
 def test_params_init_matches_reference_defaults(built):

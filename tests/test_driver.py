@@ -1,0 +1,152 @@
+"""OverlapDriver semantics: hash batches and the ref-read block schedule.
+
+canu's jobs run overlapInCore with hash-batch limits (--hashstrings / --hashdatalen /
+--hashbits + --hashload; defaults overlapInCore.H:447-450), so one -h range can become
+several hash tables (overlapInCore.C:217-287).  Batching changes results in two places:
+a final one-read batch is never searched (`while (bgnHashID < endHashID)`, :222) and the
+table-load limit moves batch ends (Build_Hash_Index.C:538-541); the ref reads a job
+searches depend on -t through Process_Overlaps' blocks (a block that starts at endRefID
+is skipped, Process_Overlaps.C:86).
+
+CPU tests pin the oracle's restatement of the driver (oracle.run_oracle_driver) to the
+reference overlapInCore (oracle/_ref/oic_ref, built from its sources) -- records AND the
+-s counters.  GPU tests run the library's ovl_overlap_driver against both.
+"""
+import numpy as np
+import pytest
+
+from canu_amd.synth import synth_reads
+
+import oracle
+
+STAT_KEYS = [("total", "total_overlaps"), ("kmer_hits_with_olap", "kmer_hits_with_olap"),
+             ("kmer_hits_without_olap", "kmer_hits_without_olap"), ("multi", "multi_overlaps"),
+             ("contained", "contained_overlaps"), ("dovetail", "dovetail_overlaps")]
+
+# (read set, batch options, threads, -r range)
+CASES = {
+    # 301 reads, 100 strings per batch: 1-100, 101-200, 201-300, then read 301 alone is
+    # never hashed (the reference's `<` at overlapInCore.C:222)
+    "strings_one_read_tail": (dict(n_reads=301, read_len=2500, genome_len=80_000, error_rate=0.02,
+                                   seed=21, len_jitter=0.4),
+                              dict(hashstrings=100), 1, None),
+    # bases per batch (--hashdatalen) cut batches by length; 16 threads over -r 17-250:
+    # blocks of perThread = 1 reads, the one starting at 250 is skipped
+    "datalen_threads": (dict(n_reads=260, read_len=2500, genome_len=70_000, error_rate=0.02,
+                             seed=22, len_jitter=0.5),
+                        dict(hashstrings=150, hashdatalen=150_000), 16, (17, 250)),
+    # a 2^12-bucket table at load 0.5 holds ~43k k-mers: ~17 reads per batch
+    "table_load": (dict(n_reads=200, read_len=2500, genome_len=60_000, error_rate=0.02, seed=23),
+                   dict(hashbits=12, hashload=0.5), 4, (3, 180)),
+}
+
+
+def _params():
+    return oracle.default_params(kmer_len=22, max_erate=0.06, min_olap_len=500)
+
+
+def _driver_kw(batch):
+    return dict(hashstrings=batch.get("hashstrings", 10000),
+                hashdatalen=batch.get("hashdatalen", 100_000_000),
+                hashbits=batch.get("hashbits", 22), hashload=batch.get("hashload", 0.6))
+
+
+def _reference(rs, P, batch, threads, rr):
+    extra = ["-r", f"{rr[0]}-{rr[1]}"] if rr else []
+    return oracle.run_reference(rs, P, threads=threads, hash_bits=batch.get("hashbits", 22),
+                                batching={k: v for k, v in batch.items() if k != "hashbits"},
+                                extra=extra, with_stats=True)
+
+
+@pytest.mark.skipif(not oracle.reference_available(), reason="oracle/_ref/oic_ref not built")
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_oracle_driver_vs_reference(case):
+    kw, batch, threads, rr = CASES[case]
+    rs = synth_reads(**kw)
+    P = _params()
+    want, wst, batches = oracle.run_oracle_driver(
+        rs, P, ref_range=rr or (1, oracle.UINT32_MAX), threads=threads, with_stats=True,
+        **_driver_kw(batch))
+    assert len(batches) >= 3
+    ref, rst = _reference(rs, P, batch, threads, rr)
+    assert want.shape == ref.shape and np.array_equal(want, ref)
+    for rk, ok in STAT_KEYS:
+        assert wst[ok] == rst[rk], (rk, wst[ok], rst[rk])
+    if case == "strings_one_read_tail":
+        # the last read is in no batch: nothing overlaps it as the hashed read
+        single = oracle.run_oracle(rs, P)
+        assert single.shape[0] > ref.shape[0]
+        assert not np.any((ref["a"] == 301) | (ref["b"] == 301))
+
+
+def test_oracle_batch_end_rules():
+    """Build_Hash_Index's stop rules on a read set small enough to count by hand."""
+    rs = synth_reads(n_reads=40, read_len=1000, genome_len=20_000, error_rate=0.0, seed=24)
+    P = _params()
+    # strings: 10 IDs per batch
+    assert oracle.hash_batch_end(rs, P, 1, 40, 10, 10**8, 22, 0.6) == 10
+    # bases: each read adds len + 1 = 1001; the read that reaches 3,500 ends the batch
+    assert oracle.hash_batch_end(rs, P, 1, 40, 1000, 3500, 22, 0.6) == 4
+    # table load: a 2^7-bucket table at load 1.0 holds 2688 entries; error-free reads of a
+    # 20 kb genome bring ~979 new k-mers each until the genome is covered
+    end = oracle.hash_batch_end(rs, P, 1, 40, 1000, 10**8, 7, 1.0)
+    hist = oracle.first_read_kmers(rs, 1, 40, 22, lambda r: True)
+    assert np.cumsum(hist)[end - 1] >= 2688 > np.cumsum(hist)[end - 2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_gpu_driver_vs_oracle_and_reference(built, case):
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    kw, batch, threads, rr = CASES[case]
+    rs = synth_reads(**kw)
+    P = _params()
+    want, wst, batches = oracle.run_oracle_driver(
+        rs, P, ref_range=rr or (1, oracle.UINT32_MAX), threads=threads, with_stats=True,
+        **_driver_kw(batch))
+    d = _driver_kw(batch)
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=d["hashstrings"], Max_Hash_Data_Len=d["hashdatalen"],
+                      Hash_Mask_Bits=d["hashbits"], Max_Hash_Load=d["hashload"],
+                      Num_PThreads=threads).finalize()
+    if rr:
+        O.bgnRefID, O.endRefID = rr
+    oic = OverlapInCore(O, device=0)
+    got = oic.run_driver(rs)
+    st = oic.stats()
+    oic.close()
+    assert st["hash_batches"] == len(batches)
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for _, ok in STAT_KEYS:
+        assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
+    if oracle.reference_available():
+        ref, rst = _reference(rs, P, batch, threads, rr)
+        assert np.array_equal(got, ref)
+        assert st["total_overlaps"] == rst["total"]
+
+
+@pytest.mark.gpu
+def test_gpu_driver_10kb_production_batches(built):
+    """Reads at the benchmark's 10 kb length under byte-limited batches (canu's
+    partitionLength hands each job --hashdatalen; here ~1 Mbp per batch): 4 batches, the
+    last a single read that is never hashed.  Bit-exact against the reference itself."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    rs = synth_reads(n_reads=301, read_len=10_000, genome_len=400_000, error_rate=0.015, seed=25)
+    P = _params()
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Data_Len=1_000_000, Num_PThreads=8).finalize()
+    oic = OverlapInCore(O, device=0)
+    got = oic.run_driver(rs)
+    st = oic.stats()
+    oic.close()
+    assert st["hash_batches"] == 3
+    want, wst, batches = oracle.run_oracle_driver(rs, P, threads=8, hashdatalen=1_000_000,
+                                                  with_stats=True)
+    assert batches[-1][1] == 300
+    assert np.array_equal(got, want)
+    if oracle.reference_available():
+        ref, rst = oracle.run_reference(rs, P, threads=8, hash_bits=22,
+                                        batching={"hashdatalen": 1_000_000}, with_stats=True)
+        assert np.array_equal(got, ref)
+        for rk, ok in STAT_KEYS:
+            assert st[ok] == rst[rk], (rk, st[ok], rst[rk])

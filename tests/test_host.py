@@ -22,7 +22,16 @@ def test_parse_defaults_and_options():
     # maxErate > 0.06 turns off the window filter and the hopeless check (main() fix-up)
     assert not P.Use_Window_Filter and not P.Use_Hopeless_Check
     assert extra == {"skip_file": None, "store": "seq.gkpStore", "output": "out.ovb",
-                     "threads": 8}
+                     "threads": 8, "stats": None}
+    # hash-batch options reach the driver (oicParameters, overlapInCore.H:505-509)
+    assert P.Hash_Mask_Bits == 24 and P.Num_PThreads == 8
+    assert (P.Max_Hash_Strings, P.Max_Hash_Data_Len, P.Max_Hash_Load) == (10000, 100000000, 0.6)
+    P, extra = parse_overlapInCore_args(["-k", "22", "--hashstrings", "300", "--hashdatalen",
+                                         "123456", "--hashload", "0.75", "-H", "2-3", "-R", "4",
+                                         "-s", "job.stats", "st"])
+    assert (P.Max_Hash_Strings, P.Max_Hash_Data_Len, P.Max_Hash_Load) == (300, 123456, 0.75)
+    assert (P.minLibToHash, P.maxLibToHash, P.minLibToRef, P.maxLibToRef) == (2, 3, 4, 4)
+    assert extra["stats"] == "job.stats"
 
 
 def test_parse_k_file_and_minkmers_order():
