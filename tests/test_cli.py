@@ -139,5 +139,16 @@ def test_gpu_cli_canu_job(cli, job):
         assert got.shape == ref.shape and np.array_equal(got, ref)
         assert open(os.path.join(jobdir, "000001.counts"), "rb").read() == \
             open(os.path.join(refwd, "w", "ref.counts"), "rb").read()
-        assert open(os.path.join(jobdir, "000001.stats")).read() == \
-            open(os.path.join(wd, "ref.stats")).read()
+        mine = open(os.path.join(jobdir, "000001.stats")).read().splitlines()
+        theirs = open(os.path.join(wd, "ref.stats")).read().splitlines()
+        if job == "utg":
+            assert mine == theirs
+        else:
+            # -G: Output_Partial_Overlap counts with `Total_Overlaps++` on the GLOBAL
+            # (overlapInCore-Output.C:253) from every thread without a lock, so with -t > 1
+            # the reference's total can lose increments.  Every other line is exact; ours is
+            # the number of records written.
+            assert [l for l in mine if "Total overlaps" not in l] == \
+                [l for l in theirs if "Total overlaps" not in l]
+            tot = lambda lines: int([l for l in lines if "Total overlaps" in l][0].split("=")[1])
+            assert tot(mine) == got.shape[0] and tot(theirs) <= tot(mine)
