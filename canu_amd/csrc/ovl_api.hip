@@ -167,7 +167,8 @@ struct ovl_ctx {
     DBuf<Unit> units;
     DBuf<uint64_t> rbase;
     DBuf<Probe> probe;
-    DBuf<uint32_t> uhits, uflags, ctr, done, defer, okey, oidx, okey2, oidx2;
+    DBuf<uint32_t> uhits, uflags, ctr, done, dset, big, defer, okey, oidx, okey2, oidx2;
+    DBuf<unsigned long long> chits;
     DBuf<uint8_t> otmp;
     DBuf<Node> pool, pnodes;
     DBuf<PairRec> pairs;
@@ -856,7 +857,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   auto &d_uhits = c->fb.uhits;
   auto &d_uflags = c->fb.uflags;
   auto &d_ctr = c->fb.ctr;
-  auto &d_done = c->fb.done;
   auto &d_defer = c->fb.defer;
   auto &d_pool = c->fb.pool;
   auto &d_pnodes = c->fb.pnodes;
@@ -934,14 +934,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       ext_waves = std::min<uint32_t>(ext_waves, (uint32_t)bpc * stg_wpb * c->n_cu);
   }
   uint32_t chain_waves = 24u * c->n_cu;      // 6 blocks of 4 waves per CU (80 VGPRs, 21 KB LDS)
-  const uint32_t DONE_CAP = 4096;
-  if (d_done.alloc((size_t)chain_waves * DONE_CAP)) return fail(OVL_ERR_OOM, "done");
 
   size_t out_cap = std::max<size_t>(1u << 20, units.size() * 8);
   if (c->d_out.alloc(out_cap)) return fail(OVL_ERR_OOM, "output");
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
-  uint64_t npairs_tot = 0, probe_bytes = 0;
+  uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0;
+  uint32_t chain_retries = 0;
   uint32_t n_probe_launch = 0, n_ext_launch = 0;
   uint32_t nu = (uint32_t)units.size();
   uint32_t u0 = 0;
@@ -994,47 +993,113 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       WIN_BUDGET = (uint64_t)std::min(std::max(wb, 64.0 * (1 << 20)), 1536.0 * (1 << 20));
     }
 
+    // Chaining.  The first launch chains every unit whose targets fit one pass of the
+    // 128-target table and lists the others; the second chains the listed units over
+    // several passes with a done set sized for their targets.  Capacities come from the
+    // probe's hit counts; a batch that still overflows one (the counters say by how much)
+    // is chained again with bigger buffers -- never dropped.
     uint64_t pool_cap = hsum + (hsum / 4000 + chain_waves + 2) * (uint64_t)OVL_NODE_BLOCK + 8;
-    uint64_t pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * 256 + 1024);
-    if (pool_cap >= 0xFFFFFFF0ull) return fail(OVL_ERR_UNSUPPORTED, "node pool too large");
-    if (d_pool.alloc(pool_cap) || d_pnodes.alloc(hsum + 1) || d_pairs.alloc(pairs_cap))
-      return fail(OVL_ERR_OOM, "chain buffers (%llu hits)", (unsigned long long)hsum);
-    uint32_t ctr_init[16] = {0};
-    ctr_init[1] = 1;                                 // pool_next: node 0 is null
-    HIPC(hipMemcpyAsync(d_ctr.p, ctr_init, 64, hipMemcpyHostToDevice, s));
-    ChainArgs CA;
-    CA.R = c->reads();
-    CA.occ = c->d_occ.p;
-    CA.units = d_units.p;
-    CA.rbase = d_rbase.p;
-    CA.probes = d_probe.p;
-    CA.unit_flags = d_uflags.p;
-    CA.nunits = nc;
-    CA.k = k;
-    CA.unit_next = d_ctr.p + 0;
-    CA.pool = d_pool.p;
-    CA.pool_next = d_ctr.p + 1;
-    CA.pool_cap = (uint32_t)pool_cap;
-    CA.pnodes = d_pnodes.p;
-    CA.pnodes_next = d_ctr.p + 2;
-    CA.pnodes_cap = (uint32_t)(hsum + 1);
-    CA.pairs = d_pairs.p;
-    CA.npairs = d_ctr.p + 3;
-    CA.pairs_cap = (uint32_t)pairs_cap;
-    CA.overflow = d_ctr.p + 4;
-    CA.done_scratch = d_done.p;
-    CA.done_cap = DONE_CAP;
-    CA.seed_hits = (unsigned long long *)(d_stats.p + 7);
-    HIPC(hipEventRecord(c->ev[4], s));
-    hipLaunchKernelGGL(k_chain, dim3(chain_waves / 4), dim3(256), 0, s, CA);
-    HIPC(hipGetLastError());
-    HIPC(hipEventRecord(c->ev[5], s));
+    uint64_t per_unit = 256;                           // test knob: force the regrow path
+    if (const char *e = getenv("OVL_TEST_PAIRS_PER_UNIT")) per_unit = std::max(1, atoi(e));
+    uint64_t pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * per_unit + 1024);
+    uint64_t pnodes_cap = hsum + 1;
+    const uint32_t hash_reads = c->hash_end_iid - c->hash_bgn_iid + 1;
     uint32_t hc[16];
-    HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    unsigned long long chain_hits = 0;
+    for (int attempt = 0;; attempt++) {
+      if (pool_cap >= 0xFFFFFFF0ull || pairs_cap >= 0xFFFFFFF0ull || pnodes_cap >= 0xFFFFFFF0ull)
+        return fail(OVL_ERR_UNSUPPORTED, "chain buffers past 2^32 entries (%llu hits)",
+                    (unsigned long long)hsum);
+      if (d_pool.alloc(pool_cap) || d_pnodes.alloc(pnodes_cap) || d_pairs.alloc(pairs_cap) ||
+          c->fb.big.alloc(nc) || c->fb.chits.alloc(1))
+        return fail(OVL_ERR_OOM, "chain buffers (%llu hits)", (unsigned long long)hsum);
+      uint32_t ctr_init[16] = {0};
+      ctr_init[1] = 1;                                 // pool_next: node 0 is null
+      HIPC(hipMemcpyAsync(d_ctr.p, ctr_init, 64, hipMemcpyHostToDevice, s));
+      HIPC(hipMemsetAsync(c->fb.chits.p, 0, 8, s));
+      ChainArgs CA;
+      CA.R = c->reads();
+      CA.occ = c->d_occ.p;
+      CA.units = d_units.p;
+      CA.rbase = d_rbase.p;
+      CA.probes = d_probe.p;
+      CA.unit_flags = d_uflags.p;
+      CA.nunits = nc;
+      CA.k = k;
+      CA.unit_next = d_ctr.p + 0;
+      CA.pool = d_pool.p;
+      CA.pool_next = d_ctr.p + 1;
+      CA.pool_cap = (uint32_t)pool_cap;
+      CA.pnodes = d_pnodes.p;
+      CA.pnodes_next = d_ctr.p + 2;
+      CA.pnodes_cap = (uint32_t)pnodes_cap;
+      CA.pairs = d_pairs.p;
+      CA.npairs = d_ctr.p + 3;
+      CA.pairs_cap = (uint32_t)pairs_cap;
+      CA.overflow = d_ctr.p + 4;
+      CA.unit_list = nullptr;
+      CA.big_units = c->fb.big.p;
+      CA.n_big = d_ctr.p + 10;
+      CA.done_slots = nullptr;
+      CA.done_set = nullptr;
+      CA.done_cap = 0;
+      CA.set_mask = 0;
+      CA.seed_hits = c->fb.chits.p;
+      HIPC(hipEventRecord(c->ev[4], s));
+      hipLaunchKernelGGL(k_chain, dim3(chain_waves / 4), dim3(256), 0, s, CA);
+      HIPC(hipGetLastError());
+      HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+      const uint32_t n_big = hc[10];
+      if (n_big && !hc[4]) {
+        std::vector<uint32_t> big(n_big);
+        HIPC(hipMemcpy(big.data(), c->fb.big.p, 4ull * n_big, hipMemcpyDeviceToHost));
+        uint32_t cap = 1;                              // distinct targets of any listed unit
+        for (uint32_t b : big) cap = std::max<uint32_t>(cap, std::min<uint32_t>(uh[b], hash_reads));
+        uint32_t smask = 1;
+        while (smask + 1 < 2ull * cap) smask = 2 * smask + 1;
+        uint32_t w2 = std::min<uint32_t>(chain_waves, (n_big + 3) & ~3u);
+        while (w2 > 4 && (uint64_t)w2 * (cap + smask + 1) * 4 > (4ull << 30)) w2 = (w2 / 2 + 3) & ~3u;
+        if (c->fb.done.alloc((size_t)w2 * cap) || c->fb.dset.alloc((size_t)w2 * (smask + 1)))
+          return fail(OVL_ERR_OOM, "done sets (%u targets x %u waves)", cap, w2);
+        HIPC(hipMemsetAsync(c->fb.dset.p, 0, 4ull * w2 * (smask + 1), s));
+        HIPC(hipMemsetAsync(d_ctr.p, 0, 4, s));      // unit_next
+        CA.unit_list = c->fb.big.p;
+        CA.nunits = n_big;
+        CA.big_units = nullptr;
+        CA.n_big = nullptr;
+        CA.done_slots = c->fb.done.p;
+        CA.done_set = c->fb.dset.p;
+        CA.done_cap = cap;
+        CA.set_mask = smask;
+        hipLaunchKernelGGL(k_chain, dim3(w2 / 4), dim3(256), 0, s, CA);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        n_big_units += n_big;
+      }
+      HIPC(hipEventRecord(c->ev[5], s));
+      HIPC(hipStreamSynchronize(s));
+      if (!hc[4]) break;
+      if ((hc[4] & 4u) || attempt >= 3)
+        return fail(OVL_ERR_HIP, "chain capacity still exceeded after %d attempts (flags %u)",
+                    attempt + 1, hc[4]);
+      // grow what overflowed from what the counters asked for, then chain the batch again
+      if (hc[4] & 1u) pool_cap = (uint64_t)hc[1] + (uint64_t)(chain_waves + 2) * OVL_NODE_BLOCK;
+      if (hc[4] & 2u) {
+        pairs_cap = std::max<uint64_t>(pairs_cap, (uint64_t)hc[3] + 1024);
+        pnodes_cap = std::max<uint64_t>(pnodes_cap, (uint64_t)hc[2] + 1024);
+      }
+      chain_retries++;
+    }
     (void)hipEventElapsedTime(&t, c->ev[4], c->ev[5]);
     ms_chain += t;
-    if (hc[4]) return fail(OVL_ERR_OOM, "chain capacity exceeded (flags %u)", hc[4]);
+    {
+      unsigned long long h = 0;
+      HIPC(hipMemcpy(&h, c->fb.chits.p, 8, hipMemcpyDeviceToHost));
+      chain_hits += h;
+      seed_hits_tot += chain_hits;
+    }
     uint32_t npairs = hc[3];
     npairs_tot += npairs;
 
@@ -1184,7 +1249,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   c->stats.total_overlaps += hs[4];
   c->stats.contained_overlaps += hs[5];
   c->stats.dovetail_overlaps += hs[6];
-  c->stats.seed_hits += hs[7];
+  c->stats.seed_hits += seed_hits_tot;
+  c->stats.multi_pass_units += n_big_units;
+  c->stats.chain_retries += chain_retries;
   c->stats.bad_short_window += hs[8];
   c->stats.bad_long_window += hs[9];
   c->stats.pairs += npairs_tot;

@@ -170,11 +170,38 @@ struct ChainArgs {
   PairRec *pairs;
   uint32_t *npairs;
   uint32_t pairs_cap;
-  uint32_t *overflow;           // set when a capacity is exceeded (host retries smaller)
-  uint32_t *done_scratch;       // per wave: targets finished in earlier passes
-  uint32_t done_cap;
+  uint32_t *overflow;           // set when a capacity is exceeded (the host grows the
+                                // buffers from the counters and runs the batch again)
+  const uint32_t *unit_list;    // units to chain (indices into units), null = 0..nunits-1
+  // Units with more than OVL_MAXT targets need several passes.  The first launch
+  // (big_units != null) chains every unit whose first pass holds all its targets and only
+  // lists the others; a second launch chains the listed units with a done set:
+  uint32_t *big_units, *n_big;
+  uint32_t *done_slots;         // per wave: set slots of the targets finished so far
+  uint32_t *done_set;           // per wave: open-addressing set of those targets (0 = empty)
+  uint32_t done_cap;            // targets per wave (>= any listed unit's distinct targets)
+  uint32_t set_mask;            // set size - 1 (power of two >= 2 done_cap)
   unsigned long long *seed_hits; // qualifying occurrences (Add_Ref calls)
 };
+
+__device__ __forceinline__ uint32_t done_hash(uint32_t t, uint32_t mask) {
+  return (t * 0x85EBCA6Bu) & mask;
+}
+
+__device__ __forceinline__ bool done_has(const uint32_t *set, uint32_t mask, uint32_t t) {
+  for (uint32_t h = done_hash(t, mask);; h = (h + 1) & mask) {
+    const uint32_t v = set[h];
+    if (v == t) return true;
+    if (v == 0) return false;
+  }
+}
+
+__device__ __forceinline__ uint32_t done_insert(uint32_t *set, uint32_t mask, uint32_t t) {
+  for (uint32_t h = done_hash(t, mask);; h = (h + 1) & mask) {
+    const uint32_t old = atomicCAS(&set[h], 0u, t);
+    if (old == 0u || old == t) return h;
+  }
+}
 
 struct SlotState {
   uint32_t t;          // target iid (0 = none)
@@ -389,14 +416,17 @@ __global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
   if (lane == 0) { *W.cur = 0; *W.end = 0; }
   const int32_t k = (int32_t)A.k;
   uint32_t gw = blockIdx.x * 4 + wave;
-  uint32_t *done_list = A.done_scratch + (size_t)gw * A.done_cap;
+  const bool first_launch = A.big_units != nullptr;
+  uint32_t *done_list = first_launch ? nullptr : A.done_slots + (size_t)gw * A.done_cap;
+  uint32_t *done_set = first_launch ? nullptr : A.done_set + (size_t)gw * (A.set_mask + 1);
   unsigned long long nhits = 0;
 
   for (;;) {
-    uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(A.unit_next, 1u);
-    u = __shfl(u, 0);
-    if (u >= A.nunits) break;
+    uint32_t ui = 0;
+    if (lane == 0) ui = atomicAdd(A.unit_next, 1u);
+    ui = __shfl(ui, 0);
+    if (ui >= A.nunits) break;
+    const uint32_t u = A.unit_list ? A.unit_list[ui] : ui;
     Unit un = A.units[u];
     uint32_t nw = unit_windows(A.R, un, A.k);
     const Probe *pr = A.probes + A.rbase[u];
@@ -454,10 +484,8 @@ __global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
             uint32_t t = (uint32_t)(hb[idx - p0] >> 32);
             uint8_t slot = 0xFF;
             if (t > a_iid) {                     // Find_Overlaps.C:328
-              if (pass == 0) nhits++;
-              bool skip = false;
-              for (uint32_t q = 0; q < ndone; q++)
-                if (done_list[q] == t) { skip = true; break; }
+              if (pass == 0 && first_launch) nhits++;
+              const bool skip = ndone && done_has(done_set, A.set_mask, t);
               if (!skip) {
                 uint32_t h = thash(t);
                 bool placed = false;
@@ -547,21 +575,34 @@ __global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
         }
       }
 
+      bool over = s_over[wave] != 0;
+      if (over && first_launch) {
+        // more targets than one pass holds: chained by the second launch (its nodes here
+        // are abandoned; the pool is sized for that)
+        if (lane == 0) A.big_units[atomicAdd(A.n_big, 1u)] = u;
+        break;
+      }
       emit_slot(s0, u, uflags, A, lane);
       emit_slot(s1, u, uflags, A, lane);
-
-      bool over = s_over[wave] != 0;
       if (!over) break;
-      // targets the 128-slot table could not hold: another pass over the unit
+      // targets the 128-slot table could not hold: another pass over the unit, skipping
+      // the targets emitted so far (done set)
       uint64_t m0 = __ballot(s0.t != 0), m1 = __ballot(s1.t != 0);
       uint32_t c0 = __builtin_popcountll(m0), c1 = __builtin_popcountll(m1);
-      if (ndone + c0 + c1 > A.done_cap) {
+      if (ndone + c0 + c1 > A.done_cap) {                // the host's bound was wrong
         if (lane == 0) atomicOr(A.overflow, 4u);
         break;
       }
-      if (s0.t) done_list[ndone + __builtin_popcountll(m0 & ((1ull << lane) - 1))] = s0.t;
-      if (s1.t) done_list[ndone + c0 + __builtin_popcountll(m1 & ((1ull << lane) - 1))] = s1.t;
+      if (s0.t) done_list[ndone + __builtin_popcountll(m0 & ((1ull << lane) - 1))] =
+          done_insert(done_set, A.set_mask, s0.t);
+      if (s1.t) done_list[ndone + c0 + __builtin_popcountll(m1 & ((1ull << lane) - 1))] =
+          done_insert(done_set, A.set_mask, s1.t);
       ndone += c0 + c1;
+      __threadfence_block();
+      WAVE_SYNC();
+    }
+    if (ndone) {                                          // empty the set for the next unit
+      for (uint32_t q = lane; q < ndone; q += 64) done_set[done_list[q]] = 0u;
       __threadfence_block();
       WAVE_SYNC();
     }

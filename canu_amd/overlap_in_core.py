@@ -55,7 +55,8 @@ class _Stats(ctypes.Structure):
          ("probe_bytes", ctypes.c_uint64), ("probe_launches", ctypes.c_uint32),
          ("extend_launches", ctypes.c_uint32), ("bad_short_window", ctypes.c_uint64),
          ("bad_long_window", ctypes.c_uint64), ("hash_batches", ctypes.c_uint64),
-         ("ref_reads", ctypes.c_uint64)]
+         ("ref_reads", ctypes.c_uint64), ("multi_pass_units", ctypes.c_uint64),
+         ("chain_retries", ctypes.c_uint64)]
 
 
 class _HashLimits(ctypes.Structure):

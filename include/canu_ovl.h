@@ -203,6 +203,8 @@ typedef struct {
   uint64_t bad_long_window;        /* -w rejections, Bad_Long_Window_Ct                */
   uint64_t hash_batches;           /* hash batches of the last driver run (1 otherwise) */
   uint64_t ref_reads;              /* query reads searched (both orientations each)    */
+  uint64_t multi_pass_units;       /* (query, orientation) units with > 128 targets     */
+  uint64_t chain_retries;          /* chain launches repeated with grown buffers        */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

@@ -138,3 +138,29 @@ def test_long_reads(built, L):
     rs = synth_reads(16, L, int(16 * L / 6), 0.015, seed=61, len_jitter=0.3)
     got = _check(rs, _params(minlen=500))
     assert got.shape[0] > 10
+
+
+@pytest.mark.parametrize("force_regrow", [False, True])
+def test_repeat_many_targets(built, force_regrow, monkeypatch):
+    """A 300-bp repeat in 150 copies over a 70 kb genome: queries seed against ~160 target
+    reads on average and several hundred at most, so most (query, orientation) units take
+    several passes of the chain's 128-target table (the second, done-set launch).  With
+    force_regrow the pair buffer starts at 4 pairs per unit and the batch is chained again
+    with the capacity the counters report -- the result must not change."""
+    if force_regrow:
+        monkeypatch.setenv("OVL_TEST_PAIRS_PER_UNIT", "4")
+    rs = synth_reads(700, 1000, 70_000, 0.02, seed=41, n_repeats=150, repeat_len=300)
+    P = _params(minlen=200)
+    oic = OverlapInCore(P, device=0)
+    oic.load_reads(rs)
+    oic.build_hash_index()
+    got = oic.fetch(oic.find_overlaps())
+    st = oic.stats()
+    oic.close()
+    want, wst = oracle.run_oracle(rs, P.as_dict(), with_stats=True)
+    assert st["multi_pass_units"] > 100
+    assert (st["chain_retries"] > 0) == force_regrow
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for f in ("seed_hits", "pairs", "kmer_hits_with_olap", "kmer_hits_without_olap",
+              "total_overlaps"):
+        assert st[f] == wst[f], (f, st[f], wst[f])
