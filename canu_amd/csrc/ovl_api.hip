@@ -1265,6 +1265,119 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   return OVL_OK;
 }
 
+int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uint64_t max_hits,
+                  uint64_t *n_hits) {
+  if (!c || !n_hits) return fail(OVL_ERR_STATE, "null argument");
+  if (!c->have_index) return fail(OVL_ERR_STATE, "ovl_build_hash_index() first");
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const uint32_t k = c->P.kmer_len;
+  if (bgn < 1) bgn = 1;
+  if (bgn < c->first_iid) bgn = c->first_iid;
+  uint32_t last = c->first_iid + c->nreads - 1;
+  if (end > last) end = last;
+  std::vector<Unit> units;
+  std::vector<uint64_t> uwin;
+  for (uint32_t a = bgn; a <= end && a >= bgn; a++) {
+    uint32_t r = a - c->first_iid;
+    int32_t L = (int32_t)c->h_len[r];
+    if (L < c->P.min_olap_len || L < (int32_t)k) continue;
+    units.push_back(Unit{r, 0});
+    units.push_back(Unit{r, 1});
+    uwin.push_back((uint64_t)(L - (int32_t)k + 1));
+    uwin.push_back((uint64_t)(L - (int32_t)k + 1));
+  }
+  // units in batches of <= 512 M probe slots; each batch's hits are written to a device
+  // buffer of at most 256 M hits (4 GB), in pieces of whole units
+  const uint64_t WIN_BUDGET = 512ull << 20, HIT_BUF = 256ull << 20;
+  auto &fb = c->fb;
+  DBuf<uint64_t> ucnt, ubase;
+  DBuf<uint4> hbuf;
+  uint64_t total = 0, copied = 0;
+  float ms_tot = 0;
+  const uint32_t nu = (uint32_t)units.size();
+  for (uint32_t u0 = 0; u0 < nu;) {
+    uint32_t u1 = u0;
+    uint64_t acc = 0;
+    while (u1 < nu && (acc + uwin[u1] <= WIN_BUDGET || u1 == u0)) acc += uwin[u1++];
+    const uint32_t nb = u1 - u0;
+    std::vector<uint64_t> rbase(nb + 1);
+    acc = 0;
+    for (uint32_t i = 0; i < nb; i++) { rbase[i] = acc; acc += uwin[u0 + i]; }
+    rbase[nb] = acc;
+    if (fb.units.alloc(nb) || fb.rbase.alloc(nb + 1) || fb.probe.alloc(acc) ||
+        fb.uhits.alloc(nb) || fb.uflags.alloc(nb) || ucnt.alloc(nb) || ubase.alloc(nb))
+      return fail(OVL_ERR_OOM, "seed-hit buffers");
+    HIPC(hipMemcpyAsync(fb.units.p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(fb.rbase.p, rbase.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
+    HIPC(hipEventRecord(c->ev[2], s));
+    ProbeArgs PA;
+    PA.R = c->reads();
+    PA.X = index_dev(c);
+    PA.units = fb.units.p;
+    PA.rbase = fb.rbase.p;
+    PA.nunits = nb;
+    PA.out = fb.probe.p;
+    PA.unit_hits = fb.uhits.p;
+    PA.unit_flags = fb.uflags.p;
+    PA.k = k;
+    hipLaunchKernelGGL(k_probe, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
+    HitArgs HA;
+    HA.R = c->reads();
+    HA.occ = c->d_occ.p;
+    HA.units = fb.units.p;
+    HA.rbase = fb.rbase.p;
+    HA.probes = fb.probe.p;
+    HA.nunits = nb;
+    HA.k = k;
+    HA.unit_hits = ucnt.p;
+    HA.unit_base = nullptr;
+    HA.out = nullptr;
+    hipLaunchKernelGGL(k_hitlist, dim3((nb + 3) / 4), dim3(256), 0, s, HA);
+    HIPC(hipGetLastError());
+    std::vector<uint64_t> cnt(nb);
+    HIPC(hipMemcpyAsync(cnt.data(), ucnt.p, 8ull * nb, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    // write pass, in pieces of whole units that fit the hit buffer
+    for (uint32_t p0 = 0; p0 < nb;) {
+      uint32_t p1 = p0;
+      uint64_t h = 0;
+      while (p1 < nb && (h + cnt[p1] <= HIT_BUF || p1 == p0)) h += cnt[p1++];
+      std::vector<uint64_t> base(nb, 0);
+      uint64_t a2 = 0;
+      for (uint32_t i = p0; i < p1; i++) { base[i] = a2; a2 += cnt[i]; }
+      if (hbuf.alloc(std::max<uint64_t>(a2, 1)))
+        return fail(OVL_ERR_OOM, "seed-hit list (%llu hits)", (unsigned long long)a2);
+      HIPC(hipMemcpyAsync(ubase.p, base.data(), 8ull * nb, hipMemcpyHostToDevice, s));
+      HA.unit_base = ubase.p;
+      HA.out = hbuf.p;
+      HA.units = fb.units.p + p0;
+      HA.rbase = fb.rbase.p + p0;
+      HA.unit_base = ubase.p + p0;
+      HA.nunits = p1 - p0;
+      hipLaunchKernelGGL(k_hitlist, dim3((p1 - p0 + 3) / 4), dim3(256), 0, s, HA);
+      HIPC(hipGetLastError());
+      if (out && copied < max_hits && a2) {
+        uint64_t n = std::min<uint64_t>(a2, max_hits - copied);
+        HIPC(hipMemcpyAsync(out + copied, hbuf.p, 16ull * n, hipMemcpyDeviceToHost, s));
+        copied += n;
+      }
+      HIPC(hipStreamSynchronize(s));
+      total += a2;
+      p0 = p1;
+    }
+    HIPC(hipEventRecord(c->ev[3], s));
+    HIPC(hipStreamSynchronize(s));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+    ms_tot += t;
+    u0 = u1;
+  }
+  c->stats.ms_seed_hits = ms_tot;
+  *n_hits = total;
+  return OVL_OK;
+}
+
 int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
   return find_impl(c, bgn, end, 0, UINT32_MAX, false, n_out);
 }

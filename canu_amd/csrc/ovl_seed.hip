@@ -146,6 +146,57 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------
+// The seed-hit list (ovl_seed_hits): every Add_Ref call of Find_Overlaps (:328-370) as
+// {query, target, window | dir << 31, target offset}, in the reference's order -- window
+// ascending, then the k-mer's chain order (target iid, offset descending).  One wave per
+// unit; count pass (out == null) -> per-unit totals, write pass -> hits at unit_base[u].
+
+struct HitArgs {
+  ReadsDev R;
+  const uint64_t *occ;
+  const Unit *units;
+  const uint64_t *rbase;
+  const Probe *probes;
+  uint32_t nunits;
+  uint32_t k;
+  uint64_t *unit_hits;          // count pass: qualifying hits per unit
+  const uint64_t *unit_base;    // write pass: first output slot per unit
+  uint4 *out;
+};
+
+__global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t u = blockIdx.x * 4 + wave;
+  if (u >= A.nunits) return;
+  const Unit un = A.units[u];
+  const uint32_t nw = unit_windows(A.R, un, A.k);
+  const Probe *pr = A.probes + A.rbase[u];
+  const uint32_t a_iid = A.R.first_iid + un.r;
+  uint64_t run = A.out ? A.unit_base[u] : 0;
+  for (uint32_t base = 0; base < nw; base += 64) {
+    const uint32_t o = base + lane;
+    uint32_t q = 0, off = 0;
+    if (o < nw) {
+      const Probe p = pr[o];
+      off = p.off;
+      q = p.cnt ? qualifying(A.occ, p.off, p.cnt, a_iid) : 0;
+    }
+    uint32_t incl = q;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if ((int)lane >= d) incl += v;
+    }
+    if (A.out) {
+      uint4 *dst = A.out + run + (incl - q);
+      for (uint32_t i = 0; i < q; i++) {
+        const uint64_t e = A.occ[off + i];
+        dst[i] = make_uint4(a_iid, (uint32_t)(e >> 32), o | (un.dir << 31), (uint32_t)e);
+      }
+    }
+    run += __shfl(incl, 63);
+  }
+  if (!A.out && lane == 0) A.unit_hits[u] = run;
+}
 
 #define OVL_HCAP   256           // staged occurrences per wave
 #define OVL_MAXT   128           // targets per pass (2 per lane)

@@ -19,6 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libcanu_ovl.so")
 
 RECORD_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("w0", "<u8"), ("w1", "<u8")])
+# ovl_seed_hit: query, target, query window | orientation << 31, target offset
+SEED_HIT_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("a_pos_dir", "<u4"), ("b_pos", "<u4")])
 
 OVL_STATUS = {0: "OVL_OK", -1: "OVL_ERR_NO_DEVICE", -2: "OVL_ERR_BAD_PARAM",
               -3: "OVL_ERR_UNSUPPORTED", -4: "OVL_ERR_BAD_INPUT", -5: "OVL_ERR_HIP",
@@ -56,7 +58,7 @@ class _Stats(ctypes.Structure):
          ("extend_launches", ctypes.c_uint32), ("bad_short_window", ctypes.c_uint64),
          ("bad_long_window", ctypes.c_uint64), ("hash_batches", ctypes.c_uint64),
          ("ref_reads", ctypes.c_uint64), ("multi_pass_units", ctypes.c_uint64),
-         ("chain_retries", ctypes.c_uint64)]
+         ("chain_retries", ctypes.c_uint64), ("ms_seed_hits", ctypes.c_double)]
 
 
 class _HashLimits(ctypes.Structure):
@@ -80,7 +82,7 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
            "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream", "ovl_write_ovb",
            "ovl_ctx_write_ovb", "ovl_ctx_write_stats", "ovl_set_read_libraries",
            "ovl_hash_limits_init", "ovl_build_hash_batch", "ovl_driver_params_init",
-           "ovl_overlap_driver"]
+           "ovl_overlap_driver", "ovl_seed_hits"]
 
 _lib = None
 
@@ -123,6 +125,8 @@ def load_library(path: str | None = None):
                                          P(_HashLimits), P(ctypes.c_uint32)]
     lib.ovl_driver_params_init.argtypes = [P(_DriverParams)]
     lib.ovl_overlap_driver.argtypes = [ctypes.c_void_p, P(_DriverParams), P(ctypes.c_uint64)]
+    lib.ovl_seed_hits.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_void_p, ctypes.c_uint64, P(ctypes.c_uint64)]
     _lib = lib
     return lib
 
@@ -400,6 +404,21 @@ class OverlapInCore:
         if skip_kmers:
             self.set_skip_kmers(skip_kmers)
         return self.fetch(self.overlap_driver())
+
+    def seed_hits(self, bgn: int | None = None, end: int | None = None,
+                  fetch: bool = True) -> np.ndarray | int:
+        """The Add_Ref hit list of the ref reads against the current index (SEED_HIT_DTYPE,
+        reference order); fetch=False only counts (the lookup still runs in full)."""
+        bgn = self.params.bgnRefID if bgn is None else bgn
+        end = min(self.params.endRefID if end is None else end, 0xFFFFFFFF)
+        n = ctypes.c_uint64()
+        self._check(self.lib.ovl_seed_hits(self.ctx, bgn, end, None, 0, ctypes.byref(n)))
+        if not fetch:
+            return n.value
+        h = np.zeros(max(n.value, 1), dtype=SEED_HIT_DTYPE)
+        self._check(self.lib.ovl_seed_hits(self.ctx, bgn, end, h.ctypes.data, n.value,
+                                           ctypes.byref(n)))
+        return h[:n.value]
 
     def run(self, rs, skip_kmers=None) -> np.ndarray:
         """OverlapDriver() for one hash batch: load, index, search, fetch (sorted)."""

@@ -176,6 +176,25 @@ int         ovl_overlap_driver(ovl_ctx *ctx, const ovl_driver_params *d, uint64_
 int         ovl_find_overlaps(ovl_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid,
                               uint64_t *n_out);
 
+/* One seed hit: an Add_Ref call of Find_Overlaps (overlapInCore-Find_Overlaps.C:328-370)
+ * -- query read, target (hash) read, the query window's offset in the searched
+ * orientation with the orientation in bit 31 (1 = REVERSE), the k-mer's offset in the
+ * target. */
+typedef struct {
+  uint32_t a_iid;
+  uint32_t b_iid;
+  uint32_t a_pos_dir;
+  uint32_t b_pos;
+} ovl_seed_hit;
+
+/* The seed-hit list of ref reads bgn_iid..end_iid against the current index (the k-mer
+ * lookup alone: no chaining, no extension), in the reference's order: query ascending,
+ * FORWARD then REVERSE, window ascending, then the k-mer's chain order (target, offset
+ * descending).  *n_hits = the total; min(max_hits, total) hits are copied to out (host
+ * memory).  out == NULL counts only (the lookup still runs in full on the device). */
+int         ovl_seed_hits(ovl_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid,
+                          ovl_seed_hit *out, uint64_t max_hits, uint64_t *n_hits);
+
 /* Copy the records of the last ovl_find_overlaps() to host memory, sorted by
  * ovOverlap::operator< (a_iid, b_iid, dat[0], dat[1]).  max_records bounds the copy. */
 int         ovl_fetch_overlaps(ovl_ctx *ctx, ovl_record *out, uint64_t max_records,
@@ -205,6 +224,7 @@ typedef struct {
   uint64_t ref_reads;              /* query reads searched (both orientations each)    */
   uint64_t multi_pass_units;       /* (query, orientation) units with > 128 targets     */
   uint64_t chain_retries;          /* chain launches repeated with grown buffers        */
+  double   ms_seed_hits;           /* device time of the last ovl_seed_hits (probe + list) */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

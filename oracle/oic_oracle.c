@@ -644,7 +644,25 @@ typedef struct {
   oracle_record       *out;  uint64_t n_out, cap_out;
   oracle_stats         st;
   double               minkmer_exp;            /* exp(-k * maxErate), computeExpected */
+  /* seed-hit export (oic_oracle_seed_hits): every Add_Ref call in order, no extension */
+  int                  hits_only;
+  uint32_t            *hits;  uint64_t n_hits, cap_hits;
+  uint32_t             cur_a, cur_dir;
 } work_area;
+
+/* One Add_Ref call: {query iid, target iid, query window offset | dir << 31, target
+ * offset}, the layout of ovl_seed_hit (include/canu_ovl.h). */
+static void record_hit(work_area *W, uint32_t t_iid, uint32_t t_off, int32_t q_off) {
+  if (W->n_hits == W->cap_hits) {
+    W->cap_hits = W->cap_hits ? 2 * W->cap_hits : 1 << 16;
+    W->hits = (uint32_t *)realloc(W->hits, 16 * W->cap_hits);
+  }
+  uint32_t *h = W->hits + 4 * W->n_hits++;
+  h[0] = W->cur_a;
+  h[1] = t_iid;
+  h[2] = (uint32_t)q_off | (W->cur_dir << 31);
+  h[3] = t_off;
+}
 
 /* Find_Overlaps.C:79 Add_Match */
 static void add_match(work_area *W, uint32_t ref_off, int32_t *start, int32_t offset,
@@ -1187,22 +1205,25 @@ static void find_overlaps(work_area *W, const char *Frag, int32_t Frag_Len,
     for (uint64_t i = lo; i < hi; i++) {
       const kmer_occ *o = &ix->occ[i];
       if (Frag_Num < o->str + ix->hash_bgn) {
+        if (W->hits_only) { record_hit(W, o->str + ix->hash_bgn, o->off, off); continue; }
         add_ref(W, o->str, o->off, off);
         W->st.seed_hits++;
       }
     }
   }
-  process_string_olaps(W, Frag, Frag_Len, quality, Frag_Num, Dir);
+  if (!W->hits_only)
+    process_string_olaps(W, Frag, Frag_Len, quality, Frag_Num, Dir);
 }
 
 /* ------------------------------------------------------------------------------------ */
 /* Entry point                                                                           */
 
-int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
-                   const uint8_t *bases, const uint64_t *offsets, const uint32_t *lengths,
-                   const uint8_t *quals, const char *skip_kmers, uint64_t n_skip,
-                   uint32_t hash_bgn, uint32_t hash_end, uint32_t ref_bgn, uint32_t ref_end,
-                   oracle_record **out, uint64_t *n_out, oracle_stats *stats) {
+static int run_impl(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
+                    const uint8_t *bases, const uint64_t *offsets, const uint32_t *lengths,
+                    const uint8_t *quals, const char *skip_kmers, uint64_t n_skip,
+                    uint32_t hash_bgn, uint32_t hash_end, uint32_t ref_bgn, uint32_t ref_end,
+                    oracle_record **out, uint64_t *n_out, oracle_stats *stats,
+                    uint32_t **hits, uint64_t *n_hits) {
   if (P->kmer_len == 0 || P->kmer_len > 31) return -2;
   read_set rs;
   rs.first_iid = first_iid;
@@ -1246,6 +1267,7 @@ int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
     W.distinct[i].delta = (int32_t *)malloc(sizeof(int32_t) * W.delta_cap);
   W.q_diff = (char *)malloc(2 * (size_t)max_len + 16);
   W.minkmer_exp = exp(-1.0 * (double)P->kmer_len * P->max_erate);
+  W.hits_only = hits != NULL;
 
   char *fbuf = (char *)malloc(max_len + 1), *qbuf = (char *)malloc(max_len + 1);
   if (ref_bgn < 1) ref_bgn = 1;
@@ -1258,7 +1280,10 @@ int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
     if (len < (int32_t)P->kmer_len) continue;            /* reference would assert */
     memcpy(fbuf, rs.seq[r], len + 1);
     memcpy(qbuf, rs.qlt[r], len + 1);
+    W.cur_a = a;
+    W.cur_dir = 0;
     find_overlaps(&W, fbuf, len, qbuf, a, 0);
+    W.cur_dir = 1;
     /* AS_UTL_reverseComplement.C reverseComplement(seq, qlt, len) */
     for (int32_t i = 0, j = len - 1; i <= j; i++, j--) {
       char c = fbuf[i], q = qbuf[i];
@@ -1268,9 +1293,10 @@ int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
     find_overlaps(&W, fbuf, len, qbuf, a, 1);
   }
 
-  *out = W.out;
-  *n_out = W.n_out;
+  if (out) *out = W.out; else free(W.out);
+  if (n_out) *n_out = W.n_out;
   if (stats) *stats = W.st;
+  if (hits) { *hits = W.hits; *n_hits = W.n_hits; }
 
   free(fbuf); free(qbuf);
   free(W.so); free(W.mn); free(W.q_diff);
@@ -1281,6 +1307,29 @@ int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
   for (uint32_t i = 0; i < nreads; i++) { free(rs.seq[i]); free(rs.qlt[i]); }
   free(rs.seq); free(rs.qlt); free(rs.len);
   return 0;
+}
+
+int oic_oracle_run(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
+                   const uint8_t *bases, const uint64_t *offsets, const uint32_t *lengths,
+                   const uint8_t *quals, const char *skip_kmers, uint64_t n_skip,
+                   uint32_t hash_bgn, uint32_t hash_end, uint32_t ref_bgn, uint32_t ref_end,
+                   oracle_record **out, uint64_t *n_out, oracle_stats *stats) {
+  return run_impl(P, first_iid, nreads, bases, offsets, lengths, quals, skip_kmers, n_skip,
+                  hash_bgn, hash_end, ref_bgn, ref_end, out, n_out, stats, NULL, NULL);
+}
+
+/* The seed-hit list of Find_Overlaps (every Add_Ref call, Find_Overlaps.C:328-370) for the
+ * ref reads against the hash reads, in the reference's order: query ascending, FORWARD then
+ * REVERSE, window ascending, then the k-mer's chain order. */
+int oic_oracle_seed_hits(const oracle_params *P, uint32_t first_iid, uint32_t nreads,
+                         const uint8_t *bases, const uint64_t *offsets, const uint32_t *lengths,
+                         const char *skip_kmers, uint64_t n_skip,
+                         uint32_t hash_bgn, uint32_t hash_end, uint32_t ref_bgn, uint32_t ref_end,
+                         uint32_t **hits, uint64_t *n_hits) {
+  *hits = NULL;
+  *n_hits = 0;
+  return run_impl(P, first_iid, nreads, bases, offsets, lengths, NULL, skip_kmers, n_skip,
+                  hash_bgn, hash_end, ref_bgn, ref_end, NULL, NULL, NULL, hits, n_hits);
 }
 
 void oic_oracle_free(void *p) { free(p); }

@@ -60,6 +60,12 @@ def _load():
             ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64),
             ctypes.POINTER(OracleStats)]
         lib.oic_oracle_free.argtypes = [ctypes.c_void_p]
+        lib.oic_oracle_seed_hits.restype = ctypes.c_int
+        lib.oic_oracle_seed_hits.argtypes = [
+            ctypes.POINTER(OracleParams), ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64,
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
         lib.oic_oracle_match_limit.restype = ctypes.c_int
         lib.oic_oracle_match_limit.argtypes = [ctypes.c_double, ctypes.c_void_p, ctypes.c_int32]
         _lib = lib
@@ -122,6 +128,38 @@ def run_oracle(rs, params: dict, hash_range=None, ref_range=None, skip_kmers=Non
     if with_stats:
         return rec, {f: getattr(st, f) for f, _ in OracleStats._fields_}
     return rec
+
+
+SEED_HIT_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("a_pos_dir", "<u4"), ("b_pos", "<u4")])
+
+
+def seed_hits(rs, params: dict, hash_range=None, ref_range=None, skip_kmers=None) -> np.ndarray:
+    """Every Add_Ref call of Find_Overlaps in the reference's order (query asc, FORWARD
+    then REVERSE, window asc, chain order): {query, target, window | dir << 31, target pos}."""
+    lib = _load()
+    P = OracleParams(**params)
+    first = rs.first_iid
+    last = first + rs.nreads - 1
+    hb, he = hash_range if hash_range else (first, last)
+    rb, re_ = ref_range if ref_range else (first, last)
+    skip = b"".join(k.encode() if isinstance(k, str) else k for k in (skip_kmers or []))
+    out = ctypes.c_void_p()
+    n = ctypes.c_uint64()
+    bases = np.ascontiguousarray(rs.bases)
+    offs = np.ascontiguousarray(rs.offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(rs.lengths, dtype=np.uint32)
+    rc = lib.oic_oracle_seed_hits(ctypes.byref(P), first, rs.nreads, bases.ctypes.data,
+                                  offs.ctypes.data, lens.ctypes.data, skip,
+                                  len(skip_kmers or []), hb, he, rb, re_, ctypes.byref(out),
+                                  ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"oic_oracle_seed_hits failed: {rc}")
+    h = np.zeros(n.value, dtype=SEED_HIT_DTYPE)
+    if n.value:
+        ctypes.memmove(h.ctypes.data, out.value, n.value * SEED_HIT_DTYPE.itemsize)
+    if out.value:
+        lib.oic_oracle_free(out)
+    return h
 
 
 def match_limit(erate: float, n: int) -> tuple[int, np.ndarray]:

@@ -1,0 +1,55 @@
+"""BASELINE configs[1]: the hash-index + seed-hit kernels alone, the hit list bit-exact.
+
+ovl_seed_hits exports every Add_Ref call of Find_Overlaps (overlapInCore-Find_Overlaps.C:
+328-370) -- query, target, window (| orientation), target offset -- in the reference's
+order; the oracle records the same calls from its restatement of Find_Overlaps.
+"""
+import numpy as np
+import pytest
+
+from canu_amd.synth import synth_reads
+from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(rs, P, skip=None, hash_range=None, ref_range=None):
+    oic = OverlapInCore(P, device=0)
+    oic.load_reads(rs)
+    if skip:
+        oic.set_skip_kmers(skip)
+    hb, he = hash_range or (1, 0xFFFFFFFF)
+    rb, re_ = ref_range or (1, 0xFFFFFFFF)
+    oic.build_hash_index(hb, he)
+    got = oic.seed_hits(rb, re_)
+    n = oic.seed_hits(rb, re_, fetch=False)
+    oic.close()
+    want = oracle.seed_hits(rs, P.as_dict(), hash_range=hash_range, ref_range=ref_range,
+                            skip_kmers=skip)
+    assert n == want.shape[0]
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32).reshape(-1, 4), want.view(np.uint32).reshape(-1, 4))
+    return got
+
+
+def test_seed_hits_10kb(built):
+    """10 kb ONT-like reads (the benchmark's length): ~10 M hits, both orientations."""
+    rs = synth_reads(200, 10_000, 1_000_000, 0.015, seed=71, len_jitter=0.2)
+    P = OicParameters(Kmer_Len=22, maxErate=float(np.float32(0.06)), Min_Olap_Len=500).finalize()
+    got = _run(rs, P)
+    assert got.shape[0] > 1_000_000
+    assert np.any(got["a_pos_dir"] >> 31) and np.any((got["a_pos_dir"] >> 31) == 0)
+
+
+def test_seed_hits_ns_skip_ranges(built):
+    """'n' bases (forward wildcards, reverse-complement NULs that end the window scan),
+    skip k-mers, repeats (long chains), ragged lengths and -h / -r sub-ranges."""
+    rs = synth_reads(150, 3000, 40_000, 0.02, seed=72, n_rate=0.002, n_repeats=30,
+                     repeat_len=300, len_jitter=0.5)
+    skip = [rs.read(3)[i:i + 22].decode().upper() for i in range(0, 2500, 23)]
+    skip = [x for x in skip if set(x) <= set("ACGT")]
+    P = OicParameters(Kmer_Len=22, maxErate=float(np.float32(0.06)), Min_Olap_Len=300).finalize()
+    _run(rs, P, skip=skip)
+    _run(rs, P, skip=skip, hash_range=(40, 140), ref_range=(20, 100))

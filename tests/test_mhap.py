@@ -171,6 +171,8 @@ CASES = {
                        mhap.MhapParameters.sensitivity("high", min_olap=300)),
     "low_k14": (dict(n=70, L=5000, err=0.03, seed=6),
                 mhap.MhapParameters.sensitivity("low", min_olap=500)),
+    # BASELINE configs[3]'s read length: 15 kb reads at 25x, 5 % error, the 'normal' preset
+    "configs3_15kb": (dict(n=300, L=15000, cov=25, err=0.05, seed=9), mhap.MhapParameters()),
     "utg_small_k": (dict(n=60, L=2500, err=0.02, seed=7),
                     mhap.MhapParameters(k=12, num_hashes=128, num_min_matches=5,
                                         ordered_kmer_size=18, ordered_sketch_size=700,
