@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import dataclasses
 import os
+import warnings
 
 import numpy as np
 
@@ -146,9 +147,15 @@ def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
             p.ordered_kmer_size = int(val); i += 1
         elif a == "--min-olap-length":
             p.min_olap_length = int(val); i += 1
-        elif a in ("-f", "-p", "-q", "-s", "--num-threads", "--filter-threshold",
-                   "--repeat-weight", "--repeat-idf-scale"):
+        elif a in ("-f", "-p", "-q", "-s", "--num-threads"):
             io[a] = val; i += 1
+        elif a in ("--filter-threshold", "--repeat-weight", "--repeat-idf-scale"):
+            # canu always passes these (OverlapMhap.pm:382, :390).  The jar's tf-idf
+            # repeat weighting is not implemented here (its algorithm ships only as
+            # bytecode, no fixture pins it): the sketch stays unweighted and -f k-mers are
+            # dropped outright.  Say so rather than accept the options silently.
+            io[a] = val; i += 1
+            io.setdefault("ignored", []).append(a)
         elif a in ("--no-self",):
             io[a] = True
         elif a in ("--supress-noise", "--no-tf"):
@@ -156,7 +163,15 @@ def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
         else:
             raise MhapError(-2, f"unknown MHAP option '{a}'")
         i += 1
+    if io.get("ignored"):
+        warnings.warn("MHAP options " + ", ".join(io["ignored"]) + " are ignored: the sketch is "
+                      "unweighted (no tf-idf repeat weighting); see DESIGN.md", MhapWeightingWarning,
+                      stacklevel=2)
     return p, io
+
+
+class MhapWeightingWarning(UserWarning):
+    """The jar's repeat-weighting options were given; this build sketches unweighted."""
 
 
 class Mhap:

@@ -80,7 +80,9 @@ def test_parse_canu_command_line():
             "--num-min-matches 2 --threshold 0.73 --filter-threshold 0.000005 "
             "--ordered-sketch-size 1536 --ordered-kmer-size 12 --min-olap-length 500 "
             "--num-threads 8 -s ./blocks/000001.dat -q queries/000001").split()
-    p, io = mhap.parse_mhap_args(argv)
+    with pytest.warns(mhap.MhapWeightingWarning, match="repeat-weight"):
+        p, io = mhap.parse_mhap_args(argv)
+    assert io["ignored"] == ["--repeat-weight", "--repeat-idf-scale", "--filter-threshold"]
     assert (p.k, p.num_hashes, p.num_min_matches, p.ordered_sketch_size) == (16, 768, 2, 1536)
     assert abs(p.threshold - 0.73) < 1e-12 and p.min_olap_length == 500
     assert io["-s"] == "./blocks/000001.dat" and io["--num-threads"] == "8"
