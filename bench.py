@@ -44,6 +44,8 @@ def main() -> None:
     ap.add_argument("--cpu-sample-reads", type=int, default=1000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-shard-timing", action="store_true",
+                    help="skip the per-shard timing (1 GPU: each of the 8 query shards in turn)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -178,6 +180,33 @@ def main() -> None:
             probe_roof["traffic_gbs"] = round(tb / (avg_ms * 1e-3) / 1e9, 1)
             probe_roof["traffic_frac"] = round(probe_roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
 
+    # BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone (the
+    # Add_Ref hit list of every query, both orientations, written to HBM, not copied out)
+    oic.build_hash_index(1, n)
+    n_hits = oic.seed_hits(q_lo, q_hi, fetch=False)
+    st1 = oic.stats()
+    seed_only = {"workload": "configs[1]: hash index + seed-hit list, same reads",
+                 "seed_hits": n_hits, "ms_index": round(st1["ms_index"], 2),
+                 "ms_seed_hits": round(st1["ms_seed_hits"], 2),
+                 "seed_hits_per_s": round(n_hits / ((st1["ms_index"] + st1["ms_seed_hits"]) * 1e-3), 1)}
+
+    # Multi-GPU evidence from one GPU: the 8-way query shards (dist.query_shards) one after
+    # another, each with its own index build, as each rank of an 8-GPU job runs them
+    shard = None
+    if world == 1 and not args.no_shard_timing:
+        shard_ms = []
+        for lo8, hi8 in query_shards(n, 8):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            oic.build_hash_index(1, n)
+            oic.find_overlaps(lo8, hi8)
+            torch.cuda.synchronize()
+            shard_ms.append(round(1000.0 * (time.perf_counter() - t1), 1))
+        shard = {"shards": 8, "shard_ms": shard_ms,
+                 "projected_speedup_8": round(sum(shard_ms) / max(shard_ms), 2),
+                 "note": "sum / max of the 8 ranks' jobs (index build included), timed in turn "
+                         "on one GPU; the driver's 8-GPU run measures the real curve"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -202,6 +231,8 @@ def main() -> None:
             "setup_s": round(setup_s, 1),
             "roofline": roof,
             "probe_roofline": probe_roof,
+            "seed_only": seed_only,
+            "shard_timing": shard,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -231,7 +262,12 @@ def load_traffic() -> dict:
 
 def cpu_baseline(args) -> dict | None:
     """The reference overlapInCore (oracle/_ref/oic_ref, built from its sources) on a
-    bounded sample of the same workload: fewer reads, same read length / error / coverage."""
+    bounded sample of the same workload: fewer reads, same read length / error / coverage,
+    with canu's production hash settings -- utgOvlHashBits 23, utgOvlHashLoad 0.75
+    (Defaults.pm:687-688) and a --hashdatalen that splits the sample into three hash
+    batches, as partitionLength hands a job its block (overlapInCorePartition.C:343).
+    Threads: the GPU box's CPU share (16 per GPU), not os.cpu_count(), which there reports
+    the whole host; a per-core figure is given for scaling to other hosts."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import oracle
@@ -246,12 +282,18 @@ def cpu_baseline(args) -> dict | None:
     p = oracle.default_params(kmer_len=args.k, max_erate=args.maxerate,
                               min_olap_len=args.minlength)
     threads = min(args.cpu_threads, os.cpu_count() or 1)
-    rec, secs, wall = oracle.run_reference(rs, p, threads=threads, hash_bits=22, with_time=True)
-    return {"value": round(len(rec) / secs, 1), "unit": "overlaps/s", "cores": threads,
-            "kind": "reference",
+    datalen = (rs.total_bases() + rs.nreads) // 3 + 1
+    rec, secs, wall = oracle.run_reference(
+        rs, p, threads=threads, hash_bits=23, with_time=True,
+        batching={"hashstrings": rs.nreads, "hashdatalen": datalen, "hashload": 0.75})
+    v = len(rec) / secs
+    return {"value": round(v, 1), "unit": "overlaps/s", "cores": threads,
+            "kind": "reference", "per_core": round(v / threads, 1),
+            "host_cpus": os.cpu_count(),
             "sample": f"{ns} reads x {args.read_len} bp at {args.coverage:.0f}x "
-                      f"(genome {gl} bp), reference OverlapDriver() wall {secs:.2f}s, "
-                      f"{len(rec)} overlaps"}
+                      f"(genome {gl} bp), --hashbits 23 --hashload 0.75 --hashdatalen {datalen} "
+                      f"(3 hash batches), reference OverlapDriver() wall {secs:.2f}s incl. its "
+                      f".ovb writing, {len(rec)} overlaps"}
 
 
 if __name__ == "__main__":
