@@ -250,8 +250,9 @@ def _traffic(t: dict, k: str):
 
 def load_traffic() -> dict:
     """Per-kernel HBM traffic of one default bench step from the committed rocprofv3 PMC
-    passes (profiles/traffic.json, tools/pmc_traffic.py): (2 x FETCH_SIZE + WRITE_SIZE) KiB,
-    the x2 being the gfx950 FETCH_SIZE correction.  Empty when absent."""
+    passes (profiles/traffic.json, tools/pmc_traffic.py): (r x FETCH_SIZE + WRITE_SIZE) KiB
+    with r the read correction calibrated per access pattern (profiles/calib_traffic.json:
+    2 for coalesced streams, 1 for k_probe's random 16-B table loads).  Empty when absent."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:

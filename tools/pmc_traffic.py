@@ -4,8 +4,13 @@
   profiles/<tag>_traffic.csv        per kernel: launches, avg ns, HBM bytes per launch
   profiles/traffic.json             {kernel: {hbm_bytes_per_step, launches_per_step}} for
                                     bench.py (the profiled run is one step, no warmup)
-HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE/WRITE_SIZE are in KiB and on
-gfx950 FETCH_SIZE reports half the bytes of a coalesced read (MI355X_MICROARCH.md, HBM).
+HBM bytes = (r * FETCH_SIZE + WRITE_SIZE) * 1024 (counters in KiB).  r is the read
+correction of the kernel's dominant read pattern, measured on known byte counts by
+tools/calib_traffic.hip (profiles/calib_traffic.json): coalesced streaming reads are
+reported at half their bytes (r = 2, as MI355X_MICROARCH.md documents), random 16-B loads
+(k_probe's table probes) at 64 B each -- one 64-B request, r = 1.  WRITE_SIZE reads the
+bytes of streaming stores exactly (calibrated 1.00) and counts a scattered 16-B store as
+the 32 B it writes (2.00), so it is taken as is.
 
     python tools/pmc_traffic.py <tag>
 """
@@ -44,6 +49,10 @@ def counters(tag, what, name=None):
                 calls[k].add(row["Dispatch_Id"])
     return tot, {k: len(v) for k, v in calls.items()}
 
+
+# read correction per kernel (see the docstring): k_probe's reads are random 16-B table
+# entries; the others read mostly coalesced streams
+READ_CORR = {"k_probe": 1.0}
 
 N_SIMD = 1024          # 256 CUs x 4 SIMDs
 VALU_ISSUE_CYC = 2     # MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles
@@ -89,12 +98,16 @@ def main():
         for k in sorted(set(fetch) | set(write)):
             n = max(nf.get(k, 0), nw.get(k, 0), 1)
             fk, wk = fetch.get(k, 0.0) / n, write.get(k, 0.0) / n
-            b = (2.0 * fk + wk) * 1024.0
+            b = (READ_CORR.get(k, 2.0) * fk + wk) * 1024.0
             traffic[k] = {"hbm_bytes_per_step": int(b * n), "launches_per_step": n,
                           "hbm_bytes_per_launch": int(b)}
             if k in iss:
                 traffic[k]["issue"] = iss[k]
             f.write(f"{k},{n},{avg_ns.get(k, 0):.0f},{fk:.1f},{wk:.1f},{b:.0f}\n")
+    traffic["_method"] = {"hbm_bytes": "(r * FETCH_SIZE + WRITE_SIZE) KiB",
+                          "read_correction": {"default": 2.0, **READ_CORR},
+                          "calibration": "profiles/calib_traffic.json (tools/calib_traffic.hip)",
+                          "tag": tag}
     with open(os.path.join(PROF, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
     print(json.dumps(traffic, indent=1))
