@@ -44,6 +44,8 @@ def main() -> None:
     ap.add_argument("--cpu-sample-reads", type=int, default=1000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-seed-only", action="store_true",
+                    help="skip the configs[1] seed-hit figure (profiling passes)")
     ap.add_argument("--no-shard-timing", action="store_true",
                     help="skip the per-shard timing (1 GPU: each of the 8 query shards in turn)")
     args = ap.parse_args()
@@ -182,13 +184,16 @@ def main() -> None:
 
     # BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone (the
     # Add_Ref hit list of every query, both orientations, written to HBM, not copied out)
-    oic.build_hash_index(1, n)
-    n_hits = oic.seed_hits(q_lo, q_hi, fetch=False)
-    st1 = oic.stats()
-    seed_only = {"workload": "configs[1]: hash index + seed-hit list, same reads",
-                 "seed_hits": n_hits, "ms_index": round(st1["ms_index"], 2),
-                 "ms_seed_hits": round(st1["ms_seed_hits"], 2),
-                 "seed_hits_per_s": round(n_hits / ((st1["ms_index"] + st1["ms_seed_hits"]) * 1e-3), 1)}
+    seed_only = None
+    if not args.no_seed_only:
+        oic.build_hash_index(1, n)
+        n_hits = oic.seed_hits(q_lo, q_hi, fetch=False)
+        st1 = oic.stats()
+        seed_only = {"workload": "configs[1]: hash index + seed-hit list, same reads",
+                     "seed_hits": n_hits, "ms_index": round(st1["ms_index"], 2),
+                     "ms_seed_hits": round(st1["ms_seed_hits"], 2),
+                     "seed_hits_per_s": round(n_hits / ((st1["ms_index"] + st1["ms_seed_hits"])
+                                                        * 1e-3), 1)}
 
     # Multi-GPU evidence from one GPU: the 8-way query shards (dist.query_shards) one after
     # another, each with its own index build, as each rank of an 8-GPU job runs them
@@ -265,8 +270,7 @@ def cpu_baseline(args) -> dict | None:
     """The reference overlapInCore (oracle/_ref/oic_ref, built from its sources) on a
     bounded sample of the same workload: fewer reads, same read length / error / coverage,
     with canu's production hash settings -- utgOvlHashBits 23, utgOvlHashLoad 0.75
-    (Defaults.pm:687-688) and a --hashdatalen that splits the sample into three hash
-    batches, as partitionLength hands a job its block (overlapInCorePartition.C:343).
+    (Defaults.pm:687-688) -- and the sample split into three hash batches (--hashstrings).
     Threads: the GPU box's CPU share (16 per GPU), not os.cpu_count(), which there reports
     the whole host; a per-core figure is given for scaling to other hosts."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -283,16 +287,19 @@ def cpu_baseline(args) -> dict | None:
     p = oracle.default_params(kmer_len=args.k, max_erate=args.maxerate,
                               min_olap_len=args.minlength)
     threads = min(args.cpu_threads, os.cpu_count() or 1)
-    datalen = (rs.total_bases() + rs.nreads) // 3 + 1
+    # three hash batches by --hashstrings (a --hashdatalen below the range's bases trips
+    # the reference's assert at Build_Hash_Index.C:523)
+    strings = (rs.nreads + 2) // 3
+    datalen = rs.total_bases() + rs.nreads + 1
     rec, secs, wall = oracle.run_reference(
         rs, p, threads=threads, hash_bits=23, with_time=True,
-        batching={"hashstrings": rs.nreads, "hashdatalen": datalen, "hashload": 0.75})
+        batching={"hashstrings": strings, "hashdatalen": datalen, "hashload": 0.75})
     v = len(rec) / secs
     return {"value": round(v, 1), "unit": "overlaps/s", "cores": threads,
             "kind": "reference", "per_core": round(v / threads, 1),
             "host_cpus": os.cpu_count(),
             "sample": f"{ns} reads x {args.read_len} bp at {args.coverage:.0f}x "
-                      f"(genome {gl} bp), --hashbits 23 --hashload 0.75 --hashdatalen {datalen} "
+                      f"(genome {gl} bp), --hashbits 23 --hashload 0.75 --hashstrings {strings} "
                       f"(3 hash batches), reference OverlapDriver() wall {secs:.2f}s incl. its "
                       f".ovb writing, {len(rec)} overlaps"}
 
