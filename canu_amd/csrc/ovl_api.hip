@@ -167,7 +167,7 @@ struct ovl_ctx {
     DBuf<Unit> units;
     DBuf<uint64_t> rbase;
     DBuf<Probe> probe;
-    DBuf<uint32_t> uhits, uflags, ctr, done, dset, big, defer, okey, oidx, okey2, oidx2;
+    DBuf<uint32_t> uhits, uflags, ctr, done, dset, big, defer, defer2, okey, oidx, okey2, oidx2;
     DBuf<unsigned long long> chits;
     DBuf<uint8_t> otmp;
     DBuf<Node> pool, pnodes;
@@ -180,6 +180,8 @@ struct ovl_ctx {
   std::vector<uint32_t> h_lib;
   bool nohash_set = false;       // some read carries OVL_RFLAG_NOHASH
   uint32_t stats_hash_lib_lo = 0, stats_hash_lib_hi = UINT32_MAX;   // -H of the index
+  std::vector<uint32_t> ext_classes;       // read-length cap of each staged launch
+  uint32_t stats_ext_waves = 0, stats_gen_waves = 0;
   uint64_t index_records = 0;    // records of the current index (windows + skip markers)
 
   // results
@@ -868,71 +870,138 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   if (d_ctr.alloc(16) || d_stats.alloc(16)) return fail(OVL_ERR_OOM, "counters");
   HIPC(hipMemsetAsync(d_stats.p, 0, 128, s));
 
-  // extension scratch per wave
-  int32_t e_cap = c->h_error_bound[std::min<uint32_t>(c->max_len, AS_MAX_READLEN)] + 2;
-  // generic kernel: band-compact rows, <= (e_cap+2)^2; staged kernel: 64*OVL_RJ cells per row
-  // (the window filter reuses a wave's row scratch: 3 segment arrays + column prefix sums)
-  uint64_t rows_cap = std::max<uint64_t>(std::max<uint64_t>(
-                                             (uint64_t)(e_cap + 2) * (e_cap + 2) + 4ull * (e_cap + 2) + 64,
-                                             window ? 3ull * (e_cap + 9) + 2ull * c->max_len + 64 : 0),
-                                         (uint64_t)(e_cap + 2) * 64 * OVL_RJ);
-  uint64_t per_wave = rows_cap * 4 + 16ull * (e_cap + 2) + 16ull * (e_cap + 8);
-  uint32_t ext_waves = 24u * c->n_cu;
-  uint64_t budget = 24ull << 30;
-  while (ext_waves > 256 && (uint64_t)ext_waves * per_wave > budget) ext_waves /= 2;
+  // ---- extension configuration --------------------------------------------------------
+  // Pairs go through up to three launches: the staged kernel at full occupancy (8 waves per
+  // <= 64 KB block) for pairs whose reads are both <= len1, the staged kernel with more LDS
+  // per wave for reads <= len2, and the generic kernel for the rest (reads with an 'n',
+  // bands wider than the register window, longer reads).  Each launch's scratch and LDS are
+  // sized for its own length class, so one long read in a job does not shrink the others.
+  auto ecap_of = [&](uint64_t L) {
+    return c->h_error_bound[std::min<uint64_t>(L, AS_MAX_READLEN)] + 2;
+  };
+  auto sw_of = [](uint64_t L) { return (int32_t)(((L + 31) / 32 + 2) & ~1ull); };
+  auto stg_lds_of = [&](uint64_t L) { return 4ull * (4ull * (uint64_t)sw_of(L) + OVL_SCR); };
+  auto ml_of = [](int32_t ec) { return 4ull * (((uint64_t)(ec + 2) + 3) & ~3ull); };
+  auto fits = [&](uint64_t L, uint32_t wpb, size_t cap) {
+    return stg_lds_of(L) * wpb + ml_of(ecap_of(L)) <= cap;
+  };
+  auto longest_fitting = [&](uint32_t wpb, size_t cap) -> uint32_t {
+    uint64_t lo = 0, hi = c->max_len;
+    if (fits(hi, wpb, cap)) return (uint32_t)hi;
+    while (lo + 1 < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (fits(mid, wpb, cap)) lo = mid; else hi = mid;
+    }
+    return (uint32_t)lo;
+  };
+  struct ExtClass {
+    uint32_t len = 0, wpb = 1, waves = 0;
+    int32_t ecap = 0, sw = 0;
+    size_t lds = 0;
+    bool l16 = false;
+    uint64_t stride = 0;
+  };
+  const uint64_t SCRATCH_BUDGET = 24ull << 30;
+  std::vector<ExtClass> ext_stage;
+  auto per_wave_bytes = [](const ExtClass &g) {
+    return g.stride * 4 + 16ull * (g.ecap + 2) + 28ull * (g.ecap + 8);
+  };
+  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob) -> int {
+    ExtClass g;
+    g.len = L;
+    g.ecap = ecap_of(L);
+    g.sw = sw_of(L);
+    g.l16 = L < 16384;
+    g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, ml_of(g.ecap))) / stg_lds_of(L));
+    if (g.wpb < 1) return -1;
+    g.lds = stg_lds_of(L) * g.wpb + ml_of(g.ecap);
+    // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the LDS so that at most that many blocks
+    // fit on a CU (occupancy studies); unset = natural occupancy
+    if (allow_knob)
+      if (const char *bp = getenv("OVL_EXT_BLOCKS_PER_CU")) {
+        int nb = atoi(bp);
+        if (nb > 0) g.lds = std::max<size_t>(g.lds, (160 * 1024) / nb - 256);
+      }
+    uint64_t st = (uint64_t)(g.ecap + 2) * 64 * OVL_RJ / (g.l16 ? 2 : 1);   // the row log
+    if (window) st = std::max<uint64_t>(st, 3ull * (g.ecap + 9) + 2ull * L + 64);
+    g.stride = (st + 63) & ~63ull;
+    const void *kfn = g.l16 ? reinterpret_cast<const void *>(k_extend<true, true>)
+                            : reinterpret_cast<const void *>(k_extend<true, false>);
+    if (g.lds > 64 * 1024)
+      if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess)
+        return -1;
+    // persistent grid: as many blocks as are resident at once (registers and LDS), so no
+    // block starts only after the work queue has drained; within the scratch budget
+    uint32_t waves = 24u * c->n_cu;
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kfn, 64 * g.wpb, g.lds) == hipSuccess &&
+        bpc > 0)
+      waves = std::min<uint32_t>(waves, (uint32_t)bpc * g.wpb * c->n_cu);
+    while (waves > g.wpb && (uint64_t)waves * per_wave_bytes(g) > SCRATCH_BUDGET) waves /= 2;
+    g.waves = std::max<uint32_t>(g.wpb, (waves / g.wpb) * g.wpb);
+    c->ext_classes.push_back(g.len);
+    ext_stage.push_back(g);
+    return 0;
+  };
+  c->ext_classes.clear();
+  // occupancy tiers of the staged kernel: 3 blocks of 8 waves per CU (the register limit),
+  // 2 blocks of 8, then one block with as many waves as fit 160 KB.  A class's length is the
+  // longest loaded read inside its tier, so its scratch (and a short-read job's launch) is
+  // exactly what a job without the longer reads would get.
+  {
+    const size_t tier_cap[3] = {52 * 1024, 80 * 1024, 160 * 1024};
+    const uint32_t tier_wpb[3] = {8, 8, 1};
+    uint32_t prev = 0;
+    for (int t = 0; t < 3; t++) {
+      const uint32_t T = longest_fitting(tier_wpb[t], tier_cap[t]);
+      uint32_t L = 0;
+      for (uint32_t x : c->h_len)
+        if (x <= T && x > L) L = x;
+      if (L < 64 || L <= prev) continue;
+      if (make_stage(L, tier_cap[t], t == 0)) return fail(OVL_ERR_HIP, "staged kernel setup");
+      prev = L;
+    }
+  }
+  // the generic kernel: every read length; rows in LDS while two row buffers and the
+  // Edit_Match_Limit table fit a CU, else in global memory (GR)
+  ExtClass gen;
+  gen.len = c->max_len;
+  gen.ecap = ecap_of(c->max_len);
+  {
+    const size_t ml = ml_of(gen.ecap);
+    size_t w = 4ull * ((2ull * (2 * gen.ecap + 8) + TB_ROWS * TB_W + OVL_LDCAP + 3) & ~3ull);
+    gen.l16 = w + ml > 160 * 1024;                       // GR
+    if (gen.l16) w = 4ull * ((TB_ROWS * TB_W + OVL_LDCAP + 3) & ~3ull);
+    gen.wpb = (4 * w <= 80 * 1024) ? 4 : (2 * w <= 80 * 1024) ? 2 : 1;
+    gen.lds = w * gen.wpb + (gen.l16 ? 0 : ml);
+    uint64_t st = (uint64_t)(gen.ecap + 2) * (gen.ecap + 2) + 4ull * (gen.ecap + 2) + 64;
+    if (window) st = std::max<uint64_t>(st, 3ull * (gen.ecap + 9) + 2ull * c->max_len + 64);
+    // a wave's band-compact row log holds every row of one extension (quadratic in the
+    // error limit); past 2^28 ints the GR kernel checks its cursor and fails loudly
+    if (gen.l16) st = std::min<uint64_t>(st, 1ull << 28);
+    gen.stride = (st + 63) & ~63ull;
+    uint32_t waves = 24u * c->n_cu;
+    while (waves > gen.wpb && (uint64_t)waves * per_wave_bytes(gen) > (16ull << 30)) waves /= 2;
+    gen.waves = std::max<uint32_t>(gen.wpb, (waves / gen.wpb) * gen.wpb);
+    const void *kfn = gen.l16 ? reinterpret_cast<const void *>(k_extend<false, true>)
+                              : reinterpret_cast<const void *>(k_extend<false, false>);
+    if (gen.lds > 64 * 1024)
+      HIPC(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen.lds));
+  }
+  uint64_t rows_n = gen.stride * gen.waves, rowdir_n = 4ull * (gen.ecap + 2) * gen.waves,
+           deltas_n = 7ull * (gen.ecap + 8) * gen.waves;
+  for (const ExtClass &g : ext_stage) {
+    rows_n = std::max<uint64_t>(rows_n, g.stride * g.waves);
+    rowdir_n = std::max<uint64_t>(rowdir_n, 4ull * (g.ecap + 2) * g.waves);
+    deltas_n = std::max<uint64_t>(deltas_n, 7ull * (g.ecap + 8) * g.waves);
+  }
   auto &d_rows = c->fb.rows;
   auto &d_rowdir = c->fb.rowdir;
   auto &d_deltas = c->fb.deltas;
-  if (d_rows.alloc(rows_cap * ext_waves) ||
-      d_rowdir.alloc((size_t)4 * (e_cap + 2) * ext_waves) ||
-      d_deltas.alloc((size_t)7 * (e_cap + 8) * ext_waves))
+  if (d_rows.alloc(rows_n) || d_rowdir.alloc(rowdir_n) || d_deltas.alloc(deltas_n))
     return fail(OVL_ERR_OOM, "extension scratch");
-  // LDS per extension wave (ovl_extend.hip k_extend).  Generic kernel: two row buffers, the
-  // traceback window and the delta cache.  Staged kernel: both strands and a scratch.
-  const size_t ml_lds = 4ull * (((e_cap + 2) + 3) & ~3);
-  size_t gen_lds_wave = 4ull * ((2ull * (2 * e_cap + 8) + TB_ROWS * TB_W + OVL_LDCAP + 3) & ~3ull);
-  uint32_t gen_wpb = (4 * gen_lds_wave <= 80 * 1024) ? 4 : (2 * gen_lds_wave <= 80 * 1024) ? 2 : 1;
-  if (gen_lds_wave + ml_lds > 160 * 1024)
-    return fail(OVL_ERR_UNSUPPORTED, "error limit %d needs more LDS than a CU has", e_cap);
-  int32_t sw_words = (int32_t)((((uint64_t)c->max_len + 31) / 32 + 2) & ~1ull);
-  size_t stg_lds_wave = 4ull * (4ull * sw_words + OVL_SCR);
-  // 512-thread blocks (one ML table per 8 waves) while they fit in 64 KB of LDS; longer
-  // reads take fewer waves per block and up to a CU's 160 KB (opt-in attribute below)
-  uint32_t stg_wpb = 8;
-  size_t stg_cap = 64 * 1024;
-  if (stg_lds_wave * 8 + ml_lds > stg_cap) {
-    stg_cap = 160 * 1024;
-    stg_wpb = (uint32_t)std::min<size_t>(8, (stg_cap - std::min(stg_cap, ml_lds)) / stg_lds_wave);
-  }
-  bool staged = stg_wpb >= 1 && stg_lds_wave * stg_wpb + ml_lds <= stg_cap;
-  if (!staged) stg_wpb = 1;
-  // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the staged kernel's LDS so that at most that
-  // many 512-thread blocks fit on a CU (occupancy studies); unset = natural occupancy
-  size_t stg_lds = stg_lds_wave * stg_wpb + ml_lds;
-  if (const char *bp = getenv("OVL_EXT_BLOCKS_PER_CU")) {
-    int nb = atoi(bp);
-    if (nb > 0) stg_lds = std::max<size_t>(stg_lds, (160 * 1024) / nb - 256);
-  }
-  ext_waves = (ext_waves / 8) * 8;
-  if (staged) {
-    ext_waves = (ext_waves / stg_wpb) * stg_wpb;
-    if (stg_lds > 64 * 1024) {
-      HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_extend<true, true>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)stg_lds));
-      HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_extend<true, false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)stg_lds));
-    }
-    // persistent grid: as many 512-thread blocks as are resident at once (registers and
-    // LDS), so no block starts only after the work queue has drained
-    int bpc = 0;
-    const bool l16 = c->max_len < 16384;
-    hipError_t oe = l16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                              &bpc, reinterpret_cast<const void *>(k_extend<true, true>), 64 * stg_wpb, stg_lds)
-                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                              &bpc, reinterpret_cast<const void *>(k_extend<true, false>), 64 * stg_wpb, stg_lds);
-    if (oe == hipSuccess && bpc > 0)
-      ext_waves = std::min<uint32_t>(ext_waves, (uint32_t)bpc * stg_wpb * c->n_cu);
-  }
+  c->stats_ext_waves = ext_stage.empty() ? 0 : ext_stage[0].waves;
+  c->stats_gen_waves = gen.waves;
   uint32_t chain_waves = 24u * c->n_cu;      // 6 blocks of 4 waves per CU (80 VGPRs, 21 KB LDS)
 
   size_t out_cap = std::max<size_t>(1u << 20, units.size() * 8);
@@ -940,6 +1009,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
   uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0;
+  uint64_t staged_pairs = 0, long_pairs = 0, generic_pairs = 0;
   uint32_t chain_retries = 0;
   uint32_t n_probe_launch = 0, n_ext_launch = 0;
   uint32_t nu = (uint32_t)units.size();
@@ -1124,11 +1194,8 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     EA.filter_by_kmer_count = c->P.filter_by_kmer_count;
     EA.minkmer_exp = exp(-1.0 * (double)k * c->P.max_erate);
     EA.rows = d_rows.p;
-    EA.rows_cap = rows_cap;
     EA.rowdir = d_rowdir.p;
     EA.deltas = d_deltas.p;
-    EA.e_cap = e_cap;
-    EA.sw_words = sw_words;
     // output capacity: grow if this batch could exceed it (<= 3 records per pair)
     uint64_t need = c->nout + 3ull * npairs;
     if (need > c->d_out.n) {
@@ -1177,44 +1244,58 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
                                                         32, s));
       EA.list = fb.oidx2.p;
     }
-    EA.ndefer = d_ctr.p + 8;
     HIPC(hipEventRecord(c->ev[6], s));
     if (npairs) {
-      size_t lds = gen_lds_wave * gen_wpb + ml_lds;
-      const uint32_t ext_wpb = gen_wpb;
-      if (lds > 64 * 1024)
-        HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_extend<false, false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      if (staged) {
-        // staged kernel for exception-free pairs; pairs touching an 'n' are deferred to
-        // the generic kernel below
-        if (d_defer.alloc(npairs)) return fail(OVL_ERR_OOM, "defer list");
-        EA.defer = d_defer.p;
-        // 16-bit traceback cells hold (r << 2 | code) when every r < 2^14
+      // the staged classes in turn, each deferring what it cannot take to the next list;
+      // the generic kernel takes the last list (or every pair when no class exists)
+      if (d_defer.alloc(npairs) || c->fb.defer2.alloc(npairs)) return fail(OVL_ERR_OOM, "defer lists");
+      uint32_t *defer_buf[2] = {d_defer.p, c->fb.defer2.p};
+      uint32_t left = npairs;
+      const uint32_t ctr_next[3] = {5, 11, 13}, ctr_defer[3] = {8, 12, 14};
+      for (size_t ci = 0; ci < ext_stage.size() && left; ci++) {
+        const ExtClass &g = ext_stage[ci];
+        EA.e_cap = g.ecap;
+        EA.rows_cap = g.stride;
+        EA.sw_words = g.sw;
+        EA.stage_len = (int32_t)g.len;
+        EA.npairs = left;
+        EA.pair_next = d_ctr.p + ctr_next[ci];
+        EA.defer = defer_buf[ci & 1];
+        EA.ndefer = d_ctr.p + ctr_defer[ci];
         n_ext_launch++;
-        if (c->max_len < 16384)
-          hipLaunchKernelGGL((k_extend<true, true>), dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
-                             stg_lds, s, EA);
+        if (g.l16)
+          hipLaunchKernelGGL((k_extend<true, true>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, s, EA);
         else
-          hipLaunchKernelGGL((k_extend<true, false>), dim3(ext_waves / stg_wpb), dim3(64 * stg_wpb),
-                             stg_lds, s, EA);
+          hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, s, EA);
         HIPC(hipGetLastError());
         uint32_t nd = 0;
-        HIPC(hipMemcpyAsync(&nd, d_ctr.p + 8, 4, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(&nd, d_ctr.p + ctr_defer[ci], 4, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
-        if (getenv("OVL_DEBUG")) fprintf(stderr, "OVL_DEBUG deferred %u of %u pairs\n", nd, npairs);
-        if (nd) {
-          EA.list = d_defer.p;
-          EA.npairs = nd;
-          EA.pair_next = d_ctr.p + 9;
-          n_ext_launch++;
-          hipLaunchKernelGGL((k_extend<false, false>), dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
-                             lds, s, EA);
-        }
-      } else {
+        if (getenv("OVL_DEBUG"))
+          fprintf(stderr, "OVL_DEBUG class %zu (reads <= %u): deferred %u of %u pairs\n", ci, g.len,
+                  nd, left);
+        if (ci == 0) staged_pairs += left - nd;
+        else long_pairs += left - nd;
+        left = nd;
+        EA.list = defer_buf[ci & 1];
+      }
+      if (left) {
+        EA.e_cap = gen.ecap;
+        EA.rows_cap = gen.stride;
+        EA.sw_words = 0;
+        EA.stage_len = 0;
+        EA.npairs = left;
+        EA.pair_next = d_ctr.p + 9;
+        EA.defer = nullptr;
+        EA.ndefer = nullptr;
+        generic_pairs += left;
         n_ext_launch++;
-        hipLaunchKernelGGL((k_extend<false, false>), dim3(ext_waves / ext_wpb), dim3(64 * ext_wpb),
-                           lds, s, EA);
+        if (gen.l16)
+          hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                             gen.lds, s, EA);
+        else
+          hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                             gen.lds, s, EA);
       }
     }
     HIPC(hipGetLastError());
@@ -1223,7 +1304,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     HIPC(hipStreamSynchronize(s));
     (void)hipEventElapsedTime(&t, c->ev[6], c->ev[7]);
     ms_ext += t;
-    if (hc[7]) return fail(OVL_ERR_OOM, "extension capacity exceeded (flags %u)", hc[7]);
+    if (hc[7] & 32u)
+      return fail(OVL_ERR_UNSUPPORTED, "an extension needs more than 2^28 row cells (error limit "
+                  "%d of a %u-base read): past the generic kernel's per-wave row log", gen.ecap,
+                  c->max_len);
+    if (hc[7]) return fail(OVL_ERR_HIP, "extension capacity exceeded (flags %u)", hc[7]);
     c->nout = hc[6];
     u0 += nc;
   }
@@ -1252,6 +1337,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   c->stats.seed_hits += seed_hits_tot;
   c->stats.multi_pass_units += n_big_units;
   c->stats.chain_retries += chain_retries;
+  c->stats.staged_pairs += staged_pairs;
+  c->stats.long_pairs += long_pairs;
+  c->stats.generic_pairs += generic_pairs;
+  c->stats.ext_waves = c->stats_ext_waves;
+  c->stats.generic_waves = c->stats_gen_waves;
+  c->stats.stage_len = c->ext_classes.empty() ? 0 : c->ext_classes[0];
+  c->stats.long_stage_len = c->ext_classes.size() > 1 ? c->ext_classes.back() : 0;
   c->stats.bad_short_window += hs[8];
   c->stats.bad_long_window += hs[9];
   c->stats.pairs += npairs_tot;

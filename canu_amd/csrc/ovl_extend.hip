@@ -45,6 +45,7 @@ struct ExtendArgs {
   int32_t *rowdir;              // per wave: (offset, lo) per error level
   int32_t *deltas;              // per wave: stack | right | left
   int32_t e_cap;                // error levels the scratch holds
+  int32_t stage_len;            // staged kernel: pairs with a longer read are deferred
   int32_t sw_words;             // staged kernel: LDS words per strand (even)
   Rec *out;
   uint32_t *nout;
@@ -203,11 +204,15 @@ __device__ __forceinline__ void ped_traceback(const WaveMem &WM, int32_t tb_e, i
   nd_out = nd;
 }
 
-template <int DIR, typename SS>
+// GR (global rows): the error limit is too large for the two LDS row buffers and the LDS
+// Edit_Match_Limit table, so row e-1 is read back from the global row log itself (which
+// holds the same values and sentinels) and the table from global memory.
+template <int DIR, typename SS, bool GR>
 __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const SS &A, int32_t a0, int32_t m,
                            const SS &T, int32_t t0, int32_t n, int32_t limit,
                            const WaveMem &WM, int32_t *dst, uint32_t lane) {
   int32_t *rows = WM.rows, *rowdir = WM.rowdir;
+  typedef typename std::conditional<GR, int32_t, lds_i32>::type row_t;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;
@@ -225,9 +230,14 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 
   int32_t row0 = (m > 0) ? ped_slide<DIR>(A, a0, m, T, t0, n, 0, 0) : 0;
   row0 = __builtin_amdgcn_readfirstlane(row0);
-  lds_i32 *lbuf0 = WM.lrow, *lbuf1 = WM.lrow + WM.wcap;
-  if (lane == 0) { rowdir[0] = 0; rowdir[1] = -2; rows[2] = row0; lbuf0[2] = row0; }
-  lds_sync();
+  row_t *lbuf0, *lbuf1;
+  if constexpr (GR) { lbuf0 = nullptr; lbuf1 = nullptr; }
+  else              { lbuf0 = WM.lrow; lbuf1 = WM.lrow + WM.wcap; }
+  if (lane == 0) {
+    rowdir[0] = 0; rowdir[1] = -2; rows[2] = row0;
+    if constexpr (!GR) lbuf0[2] = row0;
+  }
+  if constexpr (GR) vm_sync(); else lds_sync();
   if (row0 == m) {
     out.err = 0; out.a_len = m; out.t_len = m; out.mte = 1;
     out.leftover = m;          // reverse(): Leftover = m on an exact match
@@ -242,30 +252,47 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
   int32_t prev_off = 0, prev_lo = -2;
   int32_t tb_e = -1, tb_d = 0;
   bool finished = false;
-  lds_i32 *lprev = lbuf0;
+  row_t *lprev = lbuf0;
   const double bmv = X.branch_match_value;
   const bool partial = X.partial != 0;
   const int32_t mbed = X.min_branch_end_dist;
   const double mbts = X.min_branch_tail_slope;
 
   for (int32_t e = 1; e <= limit; e++) {
-    const int32_t ML = WM.mlim[e];             // LDS: no global load in the row loop
+    int32_t ML;
+    if constexpr (GR) ML = __builtin_amdgcn_readfirstlane(X.match_limit[e]);
+    else              ML = WM.mlim[e];         // LDS: no global load in the row loop
     left = (left - 1 > -e) ? left - 1 : -e;
     right = (right + 1 < e) ? right + 1 : e;
     const int32_t lo = left - 2, width = right - left + 5, off = cursor;
     cursor += width;
+    if (GR && (uint64_t)cursor > X.rows_cap) {   // past the wave's row log: refuse loudly
+      if (lane == 0) atomicOr(X.overflow, 32u);
+      out.err = 0; out.a_len = 0; out.t_len = 0; out.mte = 0; out.nd = -1;
+      return out;
+    }
     // sentinels around the new band in row e-1 (LDS copy and the traceback log)
     if (lane < 4) {
       int32_t d = (lane == 0) ? left : (lane == 1) ? left - 1 : (lane == 2) ? right : right + 1;
-      lprev[d - prev_lo] = -2;
+      if constexpr (!GR) lprev[d - prev_lo] = -2;
       rows[prev_off + d - prev_lo] = -2;
     }
     if (lane == 0) { rowdir[2 * e] = off; rowdir[2 * e + 1] = lo; }
-    lds_i32 *lcur = (e & 1) ? lbuf1 : lbuf0;
-    const lds_i32 *prev = lprev - prev_lo;      // index by diagonal
-    lds_i32 *cur = lcur - lo;
     int32_t *glog = rows + off - lo;
-    lds_sync();
+    row_t *lcur;
+    const row_t *prev;                          // index by diagonal
+    row_t *cur;
+    if constexpr (GR) {
+      lcur = nullptr;
+      prev = rows + prev_off - prev_lo;
+      cur = glog;
+      vm_sync();
+    } else {
+      lcur = (e & 1) ? lbuf1 : lbuf0;
+      prev = lprev - prev_lo;
+      cur = lcur - lo;
+      lds_sync();
+    }
 
     // ---- the row: 64 diagonals per step ------------------------------------------
     int32_t end_d = NONE, end_row = 0, nl = NONE, nr = NEG;
@@ -281,7 +308,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
       j = 1 + prev[dd + 1];
       r = j > r ? j : r;
       if (act && r < m && r + d < n) r += ped_slide<DIR>(A, a0, m, T, t0, n, r, d);
-      if (act) { cur[d] = r; glog[d] = r; }
+      if (act) {
+        if constexpr (!GR) cur[d] = r;
+        glog[d] = r;
+      }
       if (nch == 0) rv0 = act ? r : NEG;
       if (nch == 1) rv1 = act ? r : NEG;
       nch++;
@@ -301,7 +331,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
     }
     dbg_rows++;
     dbg_chunks += nch;
-    lds_sync();
+    if constexpr (GR) vm_sync(); else lds_sync();
 
     if (end_d != NONE) {
       double  score = end_row * bmv - e;
@@ -321,7 +351,10 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
         // forward.C:212 -- force the last error to be a mismatch rather than an insertion
         if (DIR > 0 && end_row == m && 1 + prev[d + 1] == end_row && d < right) {
           d++;
-          if (lane == 0) { cur[d] = end_row; glog[d] = end_row; }
+          if (lane == 0) {
+            if constexpr (!GR) cur[d] = end_row;
+            glog[d] = end_row;
+          }
         }
         out.err = e;
         out.a_len = end_row;
@@ -362,7 +395,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
     }
     prev_off = off;
     prev_lo = lo;
-    lprev = lcur;
+    if constexpr (!GR) lprev = lcur;
   }
   if (!finished) {
     out.err = max_score_best_e;
@@ -590,9 +623,8 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
   out.leftover = 0;
   out.nd = 0;
   out.ovf = 0;
-  if (limit > X.e_cap - 2) {
-    if (lane == 0) atomicOr(X.overflow, 8u);
-    out.err = 0; out.a_len = 0; out.t_len = 0; out.mte = 0; out.nd = -1;
+  if (limit > X.e_cap - 2) {                   // not this kernel's class: defer the pair
+    out.ovf = 1;
     return out;
   }
   int32_t row0 = 0;
@@ -973,7 +1005,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     PedOut po;
     PROF_T(pc0);
     if constexpr (FAST) po = wave_ped_reg<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
-    else                po = wave_ped<1, SS>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    else                po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
 #ifdef OVL_PROFILE
     PROF_T(pc1);
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc1 - pc0);
@@ -1013,7 +1045,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     PedOut po;
     PROF_T(pc2);
     if constexpr (FAST) po = wave_ped_reg<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
-    else                po = wave_ped<-1, SS>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    else                po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
 #ifdef OVL_PROFILE
     PROF_T(pc3);
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc3 - pc2);
@@ -1403,10 +1435,12 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     // drop the longest match and every match on this alignment (:517-531)
     int32_t removed = 0;
     const bool on_aln = (kind == K_DOVETAIL || X.partial);
-    // thresholds and diagonals as int16 when every read is < 16384 (L16), else int32
-    typedef typename std::conditional<L16, __attribute__((address_space(3))) int16_t,
+    // thresholds and diagonals as int16 when every read is < 16384 (the staged kernel's
+    // L16; for the generic kernel L16 means global rows, GR), else int32
+    constexpr bool T16 = FAST && L16;
+    typedef typename std::conditional<T16, __attribute__((address_space(3))) int16_t,
                                       lds_i32>::type lds_t;
-    constexpr int32_t per = L16 ? 1 : 2;               // ints per (thr, diag) pair
+    constexpr int32_t per = T16 ? 1 : 2;               // ints per (thr, diag) pair
     if (on_aln && per * (ld_len + 1) <= WM.ldcap) {
       // Lies_On_Alignment (:307) by binary search: walking the deltas, delta i is reached
       // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
@@ -1428,7 +1462,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
         cs += __builtin_amdgcn_readlane(ss, 63);
         cd += __builtin_amdgcn_readlane(sd, 63);
       }
-      if (lane == 0) { thr[ld_len] = L16 ? 32767 : 0x7fffffff; dgl[ld_len] = cd; }
+      if (lane == 0) { thr[ld_len] = T16 ? 32767 : 0x7fffffff; dgl[ld_len] = cd; }
       lds_sync();
       for (int32_t i = lane; i < nn; i += 64) {
         Node nd = nodes[i];
@@ -1564,15 +1598,20 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
 // STAGE = true: exception-free pairs, strands staged in LDS, rows in registers; pairs with
 // 'n' bases or a band wider than the register window are deferred to the generic kernel.
 // STAGE = false: the generic kernel (global strands with exception masks, rows in LDS).
-// L16: every read < 16384 bases, so the traceback code log holds 16-bit cells
+// L16, staged kernel: every read < 16384 bases, so the traceback log holds 16-bit cells.
+// L16, generic kernel: GR -- the rows and the Edit_Match_Limit table stay in global memory
+// (error limits past what a CU's LDS holds; see wave_ped).
 template <bool STAGE, bool L16>
 __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-  int32_t mlsz = ((X.e_cap + 2) + 3) & ~3;
-  for (int32_t i = threadIdx.x; i < X.e_cap + 2; i += blockDim.x)
-    s_ext0[i] = (i <= X.max_errors) ? X.match_limit[i] : 0x7fffffff;
+  constexpr bool GR = !STAGE && L16;
+  int32_t mlsz = GR ? 0 : ((X.e_cap + 2) + 3) & ~3;
+  if constexpr (!GR) {
+    for (int32_t i = threadIdx.x; i < X.e_cap + 2; i += blockDim.x)
+      s_ext0[i] = (i <= X.max_errors) ? X.match_limit[i] : 0x7fffffff;
+  }
   __syncthreads();
   lds_i32 *l_ext0 = (lds_i32 *)s_ext0;
   lds_i32 *s_ext = l_ext0 + mlsz;
@@ -1593,8 +1632,8 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
     WM.ldc = WM.tbw;
     WM.ldcap = OVL_SCR;
   } else {
-    // per wave: row buffers, traceback window, delta cache
-    int32_t wcap = 2 * X.e_cap + 8;
+    // per wave: row buffers (not with GR), traceback window, delta cache
+    int32_t wcap = GR ? 0 : 2 * X.e_cap + 8;
     uint32_t wave_ints = (2 * wcap + TB_ROWS * TB_W + OVL_LDCAP + 3) & ~3u;
     lds_i32 *wlds = s_ext + wave * wave_ints;
     WM.lrow = wlds;
@@ -1621,7 +1660,7 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
     Strand T = strand_fwd(X.R, P.tgt);
     if constexpr (STAGE) {
       bool ok = false;
-      if (!(S.ex_wild || S.ex_nul || T.ex_wild)) {
+      if (!(S.ex_wild || S.ex_nul || T.ex_wild) && S.len <= X.stage_len && T.len <= X.stage_len) {
         StrandLP SL = stage_strand(S, sw, lane);
         StrandLP TL = stage_strand(T, tw, lane);
         lds_sync();
@@ -1641,7 +1680,7 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
           if (nodes[i].Len < 0) nodes[i].Len = ~nodes[i].Len;
         vm_sync();
       }
-      process_pair<false, false>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
+      process_pair<false, L16>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
     }
     lds_sync();
   }

@@ -58,7 +58,11 @@ class _Stats(ctypes.Structure):
          ("extend_launches", ctypes.c_uint32), ("bad_short_window", ctypes.c_uint64),
          ("bad_long_window", ctypes.c_uint64), ("hash_batches", ctypes.c_uint64),
          ("ref_reads", ctypes.c_uint64), ("multi_pass_units", ctypes.c_uint64),
-         ("chain_retries", ctypes.c_uint64), ("ms_seed_hits", ctypes.c_double)]
+         ("chain_retries", ctypes.c_uint64), ("ms_seed_hits", ctypes.c_double),
+         ("staged_pairs", ctypes.c_uint64), ("long_pairs", ctypes.c_uint64),
+         ("generic_pairs", ctypes.c_uint64), ("ext_waves", ctypes.c_uint32),
+         ("generic_waves", ctypes.c_uint32), ("stage_len", ctypes.c_uint32),
+         ("long_stage_len", ctypes.c_uint32)]
 
 
 class _HashLimits(ctypes.Structure):

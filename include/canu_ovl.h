@@ -225,6 +225,13 @@ typedef struct {
   uint64_t multi_pass_units;       /* (query, orientation) units with > 128 targets     */
   uint64_t chain_retries;          /* chain launches repeated with grown buffers        */
   double   ms_seed_hits;           /* device time of the last ovl_seed_hits (probe + list) */
+  uint64_t staged_pairs;           /* pairs the full-occupancy staged kernel extended    */
+  uint64_t long_pairs;             /* pairs of the long-read staged class               */
+  uint64_t generic_pairs;          /* pairs of the generic kernel ('n', wide bands, ...) */
+  uint32_t ext_waves;              /* waves of the full-occupancy staged launch          */
+  uint32_t generic_waves;          /* waves of the generic launch                        */
+  uint32_t stage_len;              /* longest read of the full-occupancy class           */
+  uint32_t long_stage_len;         /* longest read of the long-read class (0: none)      */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

@@ -164,3 +164,42 @@ def test_repeat_many_targets(built, force_regrow, monkeypatch):
     for f in ("seed_hits", "pairs", "kmer_hits_with_olap", "kmer_hits_without_olap",
               "total_overlaps"):
         assert st[f] == wst[f], (f, st[f], wst[f])
+
+
+def _concat(a, b):
+    from canu_amd.synth import ReadSet
+    off_b = b.offsets.astype(np.uint64) + np.uint64(a.bases.shape[0])
+    return ReadSet(bases=np.concatenate([a.bases, b.bases]),
+                   offsets=np.concatenate([a.offsets.astype(np.uint64), off_b]),
+                   lengths=np.concatenate([a.lengths, b.lengths]).astype(np.uint32))
+
+
+def test_long_read_among_short(built):
+    """One 60 kb read in a set of 3 kb reads at maxErate 0.144.  Before, its error limit
+    sized every extension wave (and past ~8,000 errors of LDS failed the job).  Now the
+    full-occupancy staged launch keeps its waves and read-length class; the long read's
+    pairs carry 'n' bases, so they take the generic kernel, whose row buffers at that error
+    limit live in global memory (GR).  Every record matches the oracle."""
+    from canu_amd.synth import random_genome
+    g = random_genome(np.random.default_rng(82), 60_000)
+    short = synth_reads(100, 3000, 60_000, 0.04, seed=81, genome=g)
+    long_ = synth_reads(1, 60_000, 60_000, 0.04, seed=83, genome=g, n_rate=0.0005)
+    P = _params(erate=0.144, minlen=500)
+
+    def run(rs):
+        oic = OverlapInCore(P, device=0)
+        oic.load_reads(rs)
+        oic.build_hash_index()
+        got = oic.fetch(oic.find_overlaps())
+        st = oic.stats()
+        oic.close()
+        return got, st
+
+    _, st_short = run(short)
+    both = _concat(short, long_)
+    got, st = run(both)
+    assert st["ext_waves"] == st_short["ext_waves"] and st["stage_len"] == st_short["stage_len"]
+    assert st["generic_pairs"] > 0
+    want = oracle.run_oracle(both, P.as_dict())
+    assert got.shape == want.shape and np.array_equal(got, want)
+    assert np.any((got["a"] == 101) | (got["b"] == 101))
