@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -49,13 +50,21 @@ static int fail(int code, const char *fmt, ...) {
                   hipGetErrorString(_e));                                               \
   } while (0)
 
+// wall time spent in device (re)allocation and frees (OVL_TIMING reports it)
+static double g_alloc_ms = 0;
+static uint64_t g_alloc_n = 0, g_alloc_bytes = 0;
+
 template <typename T>
 struct DBuf {
   T *p = nullptr;
   size_t n = 0;
   ~DBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      const auto t0 = std::chrono::steady_clock::now();
+      (void)hipFree(p);
+      g_alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     p = nullptr;
     n = 0;
   }
@@ -63,9 +72,26 @@ struct DBuf {
     if (count <= n && p) return hipSuccess;
     release();
     size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc((void **)&p, bytes);
+    g_alloc_n++;
+    g_alloc_bytes += bytes;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    g_alloc_ms += ms;
+    static const bool trace = getenv("OVL_TIMING") != nullptr;
+    if (trace && bytes >= (1ull << 30))
+      fprintf(stderr, "OVL_TIMING alloc %.2f GB (%zu x %zu B) %.1f ms%s\n", bytes / 1e9, count,
+              sizeof(T), ms, e == hipSuccess ? "" : " FAILED");
     if (e == hipSuccess) n = count;
+    else (void)hipGetLastError();                  // an OOM must not surface at a later check
     return e;
+  }
+  // search working buffers: sizes vary from batch to batch, so a regrow takes 1.5x (each
+  // hipMalloc / hipFree of tens of GB costs seconds), or exactly `count` when 1.5x does not fit
+  hipError_t grow(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p && alloc(std::max(count, n + n / 2)) == hipSuccess) return hipSuccess;
+    return alloc(count);
   }
 };
 
@@ -703,6 +729,39 @@ void ovl_driver_params_init(ovl_driver_params *d) {
 static const uint32_t ENTRIES_PER_BUCKET = 21;          // overlapInCore.H:102
 static const uint64_t MAX_STRING_NUM = (1ull << 31) - 1; // overlapInCore.C:57-63
 
+// The most windows one index build may take: its records are 32-bit indexed, and its build
+// needs ~112 B per window (two 16-B record arrays, keys and positions, a table of up to 4
+// slots per window) out of the HBM that is free now plus what the current index and the
+// previous search hold (released when a build needs it), less 64 GB kept for the seed and
+// extension buffers (whose budgets shrink to fit).  OVL_TEST_INDEX_WINDOW_CAP lowers
+// it (tests of the capped path).
+static void release_find_buffers(ovl_ctx *c) {
+  auto &f = c->fb;
+  f.units.release(); f.rbase.release(); f.probe.release(); f.uhits.release();
+  f.uflags.release(); f.done.release(); f.dset.release(); f.big.release();
+  f.defer.release(); f.defer2.release(); f.okey.release(); f.oidx.release();
+  f.okey2.release(); f.oidx2.release(); f.otmp.release(); f.pool.release();
+  f.pnodes.release(); f.pairs.release(); f.rows.release(); f.rowdir.release();
+  f.deltas.release();
+}
+
+static uint64_t index_window_cap(ovl_ctx *c) {
+  uint64_t cap = 0xFFFFFFF0ull - 64 - c->h_skip.size();
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+    const auto &f = c->fb;
+    const uint64_t held = 2ull * c->d_tmpR.n * sizeof(Rec2) + 2ull * c->d_occ.n * 8 +
+                          (uint64_t)c->d_tab.n * sizeof(TabEntry) + f.probe.n * sizeof(Probe) +
+                          (f.pool.n + f.pnodes.n) * sizeof(Node) + f.pairs.n * sizeof(PairRec) +
+                          4ull * (f.rows.n + f.rowdir.n + f.deltas.n);
+    const uint64_t avail = fr + held, reserve = 64ull << 30;
+    cap = std::min<uint64_t>(cap, avail > reserve ? (avail - reserve) / 112 : 0);
+  }
+  if (const char *e = getenv("OVL_TEST_INDEX_WINDOW_CAP"))
+    cap = std::min<uint64_t>(cap, strtoull(e, nullptr, 10));
+  return std::max<uint64_t>(cap, 1);
+}
+
 // Build_Hash_Index's loading loop (overlapInCore-Build_Hash_Index.C:495-541): before each
 // read it requires String_Ct < Max_Hash_Strings, total_len < Max_Hash_Data_Len and
 // Hash_Entries < hash_entry_limit.  String_Ct counts every ID (skipped reads too);
@@ -754,14 +813,48 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
   c->stats_hash_lib_lo = L->min_lib_hash;
   c->stats_hash_lib_hi = L->max_lib_hash;
   if ((rc = apply_hash_libs(c, L->min_lib_hash, L->max_lib_hash))) return rc;
-  if ((rc = build_index(c, bgn, e))) return rc;
   // table load: at most one entry per window, so only a batch with more windows than the
   // limit can be stopped by it
   const uint64_t entry_limit =
       (uint64_t)(L->max_hash_load * (double)(1ull << L->hash_mask_bits) * (double)ENTRIES_PER_BUCKET);
-  if (windows >= entry_limit && e > bgn) {
+  const bool load_may_cut = windows >= entry_limit && e > bgn;
+  // When the load may cut the batch, the first build covers only a prefix of about twice
+  // the limit's windows (a read's new k-mers are at most its windows, so the cut lies past
+  // the limit's windows; typical reads bring 0.3-0.7 new k-mers per window).  A prefix the
+  // load does not stop inside is doubled.  One index holds at most wcap windows (32-bit
+  // records; this GPU's free HBM): the previous batch's search buffers are released only
+  // when the build needs their memory, since every (re)allocation costs ~30 GB/s of
+  // clearing.
+  uint64_t target = load_may_cut ? std::min<uint64_t>(windows, std::max<uint64_t>(2 * entry_limit, 1u << 20))
+                                 : windows;
+  for (;;) {
+    const uint64_t wcap = index_window_cap(c);
+    if (!load_may_cut && windows > wcap)
+      return fail(OVL_ERR_UNSUPPORTED, "hash batch %u-%u holds %llu k-mers, more than one index "
+                  "on this GPU (%llu); lower --hashstrings", bgn, e,
+                  (unsigned long long)windows, (unsigned long long)wcap);
+    const uint64_t tw = std::min(target, wcap);
+    uint32_t eb = e;
+    if (tw < windows) {
+      uint64_t w = 0;
+      eb = bgn;
+      for (uint32_t id = bgn; id <= e; id++) {
+        uint32_t r = id - c->first_iid;
+        uint64_t add = (loadable(r) && c->h_len[r] >= k) ? c->h_len[r] - k + 1 : 0;
+        if (w + add > tw && id > bgn) break;
+        w += add;
+        eb = id;
+      }
+    }
+    if ((rc = build_index(c, bgn, eb)) == OVL_ERR_OOM) {
+      // the previous batch's search buffers make room (the next search grows them again)
+      release_find_buffers(c);
+      rc = build_index(c, bgn, eb);
+    }
+    if (rc) return rc;
+    if (!load_may_cut) break;
     hipStream_t s = c->stream;
-    uint32_t nr = e - bgn + 1;
+    uint32_t nr = eb - bgn + 1;
     DBuf<uint32_t> hist;
     if (hist.alloc(nr)) return fail(OVL_ERR_OOM, "first-read histogram");
     HIPC(hipMemsetAsync(hist.p, 0, 4ull * nr, s));
@@ -774,15 +867,25 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
     HIPC(hipMemcpyAsync(h.data(), hist.p, 4ull * nr, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     uint64_t entries = 0;
-    uint32_t el = e;
+    uint32_t el = eb;
+    bool reached = false;
     for (uint32_t i = 0; i < nr; i++) {
       entries += h[i];
-      if (entries >= entry_limit) { el = bgn + i; break; }
+      if (entries >= entry_limit) { el = bgn + i; reached = true; break; }
     }
-    if (el < e) {
+    if (reached) {
+      if (el < eb && (rc = build_index(c, bgn, el))) return rc;
       e = el;
-      if ((rc = build_index(c, bgn, e))) return rc;
+      break;
     }
+    if (eb == e) break;                           // the whole range, under the load limit
+    if (tw >= wcap)
+      return fail(OVL_ERR_UNSUPPORTED, "hash batch from %u: the table load limit (%llu entries, "
+                  "--hashbits %u --hashload %g) is not reached within %llu k-mers, the most one "
+                  "index holds on this GPU; lower --hashbits or --hashload", bgn,
+                  (unsigned long long)entry_limit, L->hash_mask_bits, L->max_hash_load,
+                  (unsigned long long)wcap);
+    target = std::min<uint64_t>(windows, 2 * tw);
   }
   *last_iid = e;
   return OVL_OK;
@@ -851,7 +954,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // A batch is sized by seed hits (node pool + list-ordered copy: 32 B per hit); the probe
   // window budget adapts to the hits-per-window ratio seen so far so that a batch's probe
   // results are all consumed (units beyond the hit budget would otherwise be re-probed).
-  const uint64_t HIT_BUDGET = 1792ull << 20;    // seed hits per batch (the node pool stays < 2^32)
+  // seed hits per batch (the node pool stays < 2^32); halved while the chain buffers do not
+  // fit the HBM the index leaves, as the probe-slot cap is for the probe records
+  uint64_t HIT_BUDGET = 1792ull << 20;
+  uint64_t win_cap = 1536ull << 20;
   uint64_t WIN_BUDGET = 512ull << 20;           // probe slots per batch (8 B each)
   auto &d_units = c->fb.units;
   auto &d_rbase = c->fb.rbase;
@@ -945,12 +1051,12 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   };
   c->ext_classes.clear();
   // occupancy tiers of the staged kernel: 3 blocks of 8 waves per CU (the register limit),
-  // 2 blocks of 8, then one block with as many waves as fit 160 KB.  A class's length is the
+  // 3 blocks of 6, then blocks of up to 8 waves within 160 KB (as many as fit a CU).  A class's length is the
   // longest loaded read inside its tier, so its scratch (and a short-read job's launch) is
   // exactly what a job without the longer reads would get.
   {
-    const size_t tier_cap[3] = {52 * 1024, 80 * 1024, 160 * 1024};
-    const uint32_t tier_wpb[3] = {8, 8, 1};
+    const size_t tier_cap[3] = {52 * 1024, 52 * 1024, 160 * 1024};
+    const uint32_t tier_wpb[3] = {8, 6, 1};
     uint32_t prev = 0;
     for (int t = 0; t < 3; t++) {
       const uint32_t T = longest_fitting(tier_wpb[t], tier_cap[t]);
@@ -1024,9 +1130,12 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     uint64_t acc = 0;
     for (uint32_t i = 0; i < nb; i++) { rbase[i] = acc; acc += uwin[u0 + i]; }
     rbase[nb] = acc;
-    if (d_units.alloc(nb) || d_rbase.alloc(nb + 1) || d_probe.alloc(acc) ||
-        d_uhits.alloc(nb) || d_uflags.alloc(nb))
-      return fail(OVL_ERR_OOM, "probe buffers");
+    if (d_units.grow(nb) || d_rbase.grow(nb + 1) || d_probe.grow(acc) ||
+        d_uhits.grow(nb) || d_uflags.grow(nb)) {
+      if (nb == 1 || WIN_BUDGET <= (16ull << 20)) return fail(OVL_ERR_OOM, "probe buffers");
+      win_cap = WIN_BUDGET = WIN_BUDGET / 2;
+      continue;
+    }
     HIPC(hipMemcpyAsync(d_units.p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(d_rbase.p, rbase.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
     ProbeArgs PA;
@@ -1056,23 +1165,35 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     // shrink the batch to the hit budget (probe results stay valid for the prefix)
     uint64_t hsum = 0;
     uint32_t nc = 0;
-    while (nc < nb && (hsum + uh[nc] <= HIT_BUDGET || nc == 0)) hsum += uh[nc++];
-    {
+    auto fit_hits = [&]() {
+      hsum = 0;
+      nc = 0;
+      while (nc < nb && (hsum + uh[nc] <= HIT_BUDGET || nc == 0)) hsum += uh[nc++];
       double ratio = (double)hsum / (double)std::max<uint64_t>(1, rbase[nc]);
       double wb = (double)HIT_BUDGET / std::max(ratio, 1e-3) * 1.05;
-      WIN_BUDGET = (uint64_t)std::min(std::max(wb, 64.0 * (1 << 20)), 1536.0 * (1 << 20));
-    }
+      WIN_BUDGET = (uint64_t)std::min(std::max(wb, 16.0 * (1 << 20)), (double)win_cap);
+    };
+    fit_hits();
 
     // Chaining.  The first launch chains every unit whose targets fit one pass of the
     // 128-target table and lists the others; the second chains the listed units over
     // several passes with a done set sized for their targets.  Capacities come from the
     // probe's hit counts; a batch that still overflows one (the counters say by how much)
     // is chained again with bigger buffers -- never dropped.
-    uint64_t pool_cap = hsum + (hsum / 4000 + chain_waves + 2) * (uint64_t)OVL_NODE_BLOCK + 8;
     uint64_t per_unit = 256;                           // test knob: force the regrow path
     if (const char *e = getenv("OVL_TEST_PAIRS_PER_UNIT")) per_unit = std::max(1, atoi(e));
-    uint64_t pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * per_unit + 1024);
-    uint64_t pnodes_cap = hsum + 1;
+    uint64_t pool_cap = 0, pairs_cap = 0, pnodes_cap = 0;
+    // nodes <= hits; a wave claims OVL_NODE_BLOCK nodes at a time for at most 64 lanes per
+    // claim, so a block wastes < 64 / 4096 of itself, and each wave ends holding one block
+    auto pool_for = [&](uint64_t h) {
+      return h + h / 32 + (uint64_t)(chain_waves + 2) * OVL_NODE_BLOCK + 8;
+    };
+    auto set_caps = [&]() {
+      pool_cap = pool_for(hsum);
+      pairs_cap = std::min<uint64_t>(hsum + 1, (uint64_t)nc * per_unit + 1024);
+      pnodes_cap = hsum + 1;
+    };
+    set_caps();
     const uint32_t hash_reads = c->hash_end_iid - c->hash_bgn_iid + 1;
     uint32_t hc[16];
     unsigned long long chain_hits = 0;
@@ -1080,9 +1201,18 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       if (pool_cap >= 0xFFFFFFF0ull || pairs_cap >= 0xFFFFFFF0ull || pnodes_cap >= 0xFFFFFFF0ull)
         return fail(OVL_ERR_UNSUPPORTED, "chain buffers past 2^32 entries (%llu hits)",
                     (unsigned long long)hsum);
-      if (d_pool.alloc(pool_cap) || d_pnodes.alloc(pnodes_cap) || d_pairs.alloc(pairs_cap) ||
-          c->fb.big.alloc(nc) || c->fb.chits.alloc(1))
-        return fail(OVL_ERR_OOM, "chain buffers (%llu hits)", (unsigned long long)hsum);
+      // sized for the hit budget, not this batch's hits: the next batch reuses them as they are
+      if (d_pool.grow(std::max(pool_cap, pool_for(HIT_BUDGET))) ||
+          d_pnodes.grow(std::max<uint64_t>(pnodes_cap, HIT_BUDGET + 1)) || d_pairs.grow(pairs_cap) ||
+          c->fb.big.grow(nc) || c->fb.chits.grow(1)) {
+        if (nc == 1 || hsum <= (16ull << 20))
+          return fail(OVL_ERR_OOM, "chain buffers (%llu hits)", (unsigned long long)hsum);
+        HIT_BUDGET = hsum / 2;                         // fewer units per chain launch
+        fit_hits();
+        set_caps();
+        attempt--;
+        continue;
+      }
       uint32_t ctr_init[16] = {0};
       ctr_init[1] = 1;                                 // pool_next: node 0 is null
       HIPC(hipMemcpyAsync(d_ctr.p, ctr_init, 64, hipMemcpyHostToDevice, s));
@@ -1130,7 +1260,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         while (smask + 1 < 2ull * cap) smask = 2 * smask + 1;
         uint32_t w2 = std::min<uint32_t>(chain_waves, (n_big + 3) & ~3u);
         while (w2 > 4 && (uint64_t)w2 * (cap + smask + 1) * 4 > (4ull << 30)) w2 = (w2 / 2 + 3) & ~3u;
-        if (c->fb.done.alloc((size_t)w2 * cap) || c->fb.dset.alloc((size_t)w2 * (smask + 1)))
+        if (c->fb.done.grow((size_t)w2 * cap) || c->fb.dset.grow((size_t)w2 * (smask + 1)))
           return fail(OVL_ERR_OOM, "done sets (%u targets x %u waves)", cap, w2);
         HIPC(hipMemsetAsync(c->fb.dset.p, 0, 4ull * w2 * (smask + 1), s));
         HIPC(hipMemsetAsync(d_ctr.p, 0, 4, s));      // unit_next
@@ -1228,8 +1358,8 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     if (npairs > 1) {
       // longest-first work order (node count descending; ties keep pair order)
       auto &fb = c->fb;
-      if (fb.okey.alloc(npairs) || fb.oidx.alloc(npairs) || fb.okey2.alloc(npairs) ||
-          fb.oidx2.alloc(npairs))
+      if (fb.okey.grow(npairs) || fb.oidx.grow(npairs) || fb.okey2.grow(npairs) ||
+          fb.oidx2.grow(npairs))
         return fail(OVL_ERR_OOM, "work order");
       hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
                          dim3(256), 0, s, d_pairs.p, npairs, fb.okey.p, fb.oidx.p);
@@ -1238,7 +1368,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       HIPC(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, fb.okey.p, fb.okey2.p,
                                                         fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
                                                         32, s));
-      if (fb.otmp.alloc(tmp)) return fail(OVL_ERR_OOM, "work order scratch");
+      if (fb.otmp.grow(tmp)) return fail(OVL_ERR_OOM, "work order scratch");
       HIPC(hipcub::DeviceRadixSort::SortPairsDescending(fb.otmp.p, tmp, fb.okey.p, fb.okey2.p,
                                                         fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
                                                         32, s));
@@ -1248,7 +1378,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     if (npairs) {
       // the staged classes in turn, each deferring what it cannot take to the next list;
       // the generic kernel takes the last list (or every pair when no class exists)
-      if (d_defer.alloc(npairs) || c->fb.defer2.alloc(npairs)) return fail(OVL_ERR_OOM, "defer lists");
+      if (d_defer.grow(npairs) || c->fb.defer2.grow(npairs)) return fail(OVL_ERR_OOM, "defer lists");
       uint32_t *defer_buf[2] = {d_defer.p, c->fb.defer2.p};
       uint32_t left = npairs;
       const uint32_t ctr_next[3] = {5, 11, 13}, ctr_defer[3] = {8, 12, 14};
@@ -1397,8 +1527,8 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
     acc = 0;
     for (uint32_t i = 0; i < nb; i++) { rbase[i] = acc; acc += uwin[u0 + i]; }
     rbase[nb] = acc;
-    if (fb.units.alloc(nb) || fb.rbase.alloc(nb + 1) || fb.probe.alloc(acc) ||
-        fb.uhits.alloc(nb) || fb.uflags.alloc(nb) || ucnt.alloc(nb) || ubase.alloc(nb))
+    if (fb.units.grow(nb) || fb.rbase.grow(nb + 1) || fb.probe.grow(acc) ||
+        fb.uhits.grow(nb) || fb.uflags.grow(nb) || ucnt.grow(nb) || ubase.grow(nb))
       return fail(OVL_ERR_OOM, "seed-hit buffers");
     HIPC(hipMemcpyAsync(fb.units.p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(fb.rbase.p, rbase.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
@@ -1515,14 +1645,26 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   while (bgn < g_end_hash) {                                             // :222
     if (end > g_end_hash) end = g_end_hash;
     uint32_t loaded = 0;
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = build_batch_impl(c, bgn, end, &L, &loaded);
     if (rc) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
     end = loaded;
     batches++;
     if (any_ref) {
       uint64_t n = 0;
       if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n)))
         return rc;
+    }
+    if (getenv("OVL_TIMING")) {
+      const auto t2 = std::chrono::steady_clock::now();
+      fprintf(stderr, "OVL_TIMING batch %llu: hash %u-%u, wall build %.1f ms, find %.1f ms; "
+              "device index %.1f seed %.1f extend %.1f ms, alloc/free %.1f ms (%llu allocs, %.1f GB) so far\n",
+              (unsigned long long)batches, bgn, end,
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(), c->stats.ms_index,
+              c->stats.ms_seed, c->stats.ms_extend, g_alloc_ms,
+              (unsigned long long)g_alloc_n, g_alloc_bytes / 1e9);
     }
     bgn = end + 1;
     end = bgn + L.max_hash_strings - 1;

@@ -150,3 +150,41 @@ def test_gpu_driver_10kb_production_batches(built):
         assert np.array_equal(got, ref)
         for rk, ok in STAT_KEYS:
             assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
+
+
+@pytest.mark.gpu
+def test_gpu_driver_load_cut_within_window_cap(built, monkeypatch):
+    """A batch the table load cuts, built from a prefix of the -h range: when the range
+    holds more windows than one index may take (OVL_TEST_INDEX_WINDOW_CAP stands in for the
+    HBM / 2^32 cap), the first build covers the longest prefix within the cap and the load
+    has to stop the batch inside it -- the same batches and records as without the cap.
+    A cap the load cannot be reached within fails loudly instead of changing the batches."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore, OvlError
+    kw, batch, threads, rr = CASES["table_load"]
+    rs = synth_reads(**kw)
+    P = _params()
+    want, wst, batches = oracle.run_oracle_driver(
+        rs, P, ref_range=rr, threads=threads, with_stats=True, **_driver_kw(batch))
+    d = _driver_kw(batch)
+
+    def run():
+        O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                          Hash_Mask_Bits=d["hashbits"], Max_Hash_Load=d["hashload"],
+                          Num_PThreads=threads).finalize()
+        O.bgnRefID, O.endRefID = rr
+        oic = OverlapInCore(O, device=0)
+        try:
+            got = oic.run_driver(rs)
+            return got, oic.stats()
+        finally:
+            oic.close()
+
+    monkeypatch.setenv("OVL_TEST_INDEX_WINDOW_CAP", "80000")
+    got, st = run()
+    assert st["hash_batches"] == len(batches)
+    assert np.array_equal(got, want)
+    for _, ok in STAT_KEYS:
+        assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
+    monkeypatch.setenv("OVL_TEST_INDEX_WINDOW_CAP", "20000")
+    with pytest.raises(OvlError, match="load limit"):
+        run()

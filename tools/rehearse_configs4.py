@@ -8,10 +8,12 @@ This script runs that loop -- ovl_overlap_driver, the reference's batch semantic
 --hashdatalen limits -- on a 1/8-size read set (default 500k x 12 kb at 15x), and reports
 per-phase times, the hash batches taken, and the device memory the library holds (free HBM
 before the load minus free HBM after the job: the library's buffers only grow, so this is
-its high-water mark).  DESIGN.md's configs[4] memory plan extrapolates from these numbers.
+its high-water mark).  The reference asserts when the whole -h range holds more bases than
+--hashdatalen (Build_Hash_Index.C:521-523), so batches are cut by the hash load
+(--hashbits / --hashload) and --hashstrings.  DESIGN.md's configs[4] memory plan extrapolates from these numbers.
 
     python tools/rehearse_configs4.py [--reads 500000] [--read-len 12000] [--coverage 15]
-                                      [--hashbits 27] [--hashdatalen 2000000000]
+                                      [--hashbits 26] [--hashdatalen 8000000000]
 """
 import argparse
 import json
@@ -60,10 +62,10 @@ def main() -> None:
     ap.add_argument("--read-len", type=int, default=12_000)
     ap.add_argument("--coverage", type=float, default=15.0)
     ap.add_argument("--read-error", type=float, default=0.015)
-    ap.add_argument("--hashbits", type=int, default=27)
+    ap.add_argument("--hashbits", type=int, default=26)
     ap.add_argument("--hashload", type=float, default=0.75)
     ap.add_argument("--hashstrings", type=int, default=1_000_000)
-    ap.add_argument("--hashdatalen", type=int, default=2_000_000_000)
+    ap.add_argument("--hashdatalen", type=int, default=8_000_000_000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--seed", type=int, default=5)
     args = ap.parse_args()
@@ -120,6 +122,9 @@ def main() -> None:
         "seed_hits": st["seed_hits"], "pairs": st["pairs"],
         "staged_pairs": st["staged_pairs"], "long_pairs": st["long_pairs"],
         "generic_pairs": st["generic_pairs"],
+        "extra": {k: st[k] for k in ("chain_retries", "multi_pass_units", "ms_probe_kernel",
+                                     "ext_waves", "generic_waves", "stage_len",
+                                     "long_stage_len", "extend_launches") if k in st},
         "hbm_gib": {"total": round(total / gib, 1),
                     "raw_bases_staged": round((free0 - free_staged) / gib, 2),
                     "library_store": round((free_staged - free_loaded) / gib, 2),
