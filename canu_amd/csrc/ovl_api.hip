@@ -1108,7 +1108,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     return fail(OVL_ERR_OOM, "extension scratch");
   c->stats_ext_waves = ext_stage.empty() ? 0 : ext_stage[0].waves;
   c->stats_gen_waves = gen.waves;
-  uint32_t chain_waves = 24u * c->n_cu;      // 6 blocks of 4 waves per CU (80 VGPRs, 21 KB LDS)
+  uint32_t chain_waves = 4u * OVL_CHAIN_OCC * c->n_cu;   // OVL_CHAIN_OCC blocks of 4 waves per CU
 
   size_t out_cap = std::max<size_t>(1u << 20, units.size() * 8);
   if (c->d_out.alloc(out_cap)) return fail(OVL_ERR_OOM, "output");

@@ -99,23 +99,23 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
       e[q].key = 0; e[q].off = 0; e[q].cnt = 0;
       if (ok[q]) e[q] = A.X.tab[slot0[q]];
     }
-#pragma unroll
-    for (int q = 0; q < PU; q++) {
-      const uint32_t o = o0 + 64 * q + lane;
-      if (o >= nw) continue;
+    // finish each window with its values passed in: a loop over q holding the unbounded
+    // probe loop is not unrolled, and its dynamically indexed arrays went to scratch (80 B
+    // per lane, ~3x the records' bytes of write traffic)
+    auto finish = [&](uint32_t o, bool okq, uint64_t Mq, uint64_t s0, TabEntry t) {
+      if (o >= nw) return;
       Probe pr;
       pr.off = 0;
       pr.cnt = 0;
-      if (ok[q]) {
+      if (okq) {
         // index_find's linear probe within the slice, from the entry already loaded
-        TabEntry t = e[q];
         bool found = false;
-        const uint64_t base = slot0[q] & ~smask;
+        const uint64_t base = s0 & ~smask;
         for (uint64_t i = 1;; i++) {
           if (t.cnt == 0) break;
-          if (t.key == M[q]) { found = true; break; }
+          if (t.key == Mq) { found = true; break; }
           if (i > smask) break;
-          t = A.X.tab[base | ((slot0[q] + i) & smask)];
+          t = A.X.tab[base | ((s0 + i) & smask)];
         }
         if (found) {
           const uint32_t c = t.cnt;
@@ -133,7 +133,12 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
         }
       }
       out[o] = pr;
-    }
+    };
+    static_assert(PU == 4, "finish() calls below");
+    finish(o0 + lane, ok[0], M[0], slot0[0], e[0]);
+    finish(o0 + 64 + lane, ok[1], M[1], slot0[1], e[1]);
+    finish(o0 + 128 + lane, ok[2], M[2], slot0[2], e[2]);
+    finish(o0 + 192 + lane, ok[3], M[3], slot0[3], e[3]);
   }
   for (int s = 32; s > 0; s >>= 1) {
     hits += __shfl_xor(hits, s);
@@ -201,6 +206,9 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 #define OVL_HCAP   256           // staged occurrences per wave
 #define OVL_MAXT   128           // targets per pass (2 per lane)
 #define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
+#ifndef OVL_CHAIN_OCC
+#define OVL_CHAIN_OCC 6          // k_chain waves per SIMD (80 VGPRs)
+#endif
 
 struct ChainArgs {
   ReadsDev R;
@@ -438,7 +446,7 @@ __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
   } while (0)
 
-__global__ void __launch_bounds__(256, 6) k_chain(ChainArgs A) {
+__global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   __shared__ uint64_t s_hb[4][OVL_HCAP];
   __shared__ uint8_t  s_hw[4][OVL_HCAP];      // window (0..63) of each staged occurrence
   __shared__ uint8_t  s_hs[4][OVL_HCAP];      // its target slot (0..127), 0xFF: none

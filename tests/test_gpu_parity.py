@@ -203,3 +203,31 @@ def test_long_read_among_short(built):
     want = oracle.run_oracle(both, P.as_dict())
     assert got.shape == want.shape and np.array_equal(got, want)
     assert np.any((got["a"] == 101) | (got["b"] == 101))
+
+
+def test_query_over_4096_targets(built):
+    """One 300-bp repeat written into every one of 5,200 reads: each of the first queries
+    seeds against > 4,096 target reads (round 1's DONE_CAP aborted such a job with
+    OVL_ERR_OOM).  The chain's multi-pass launch sizes its done set from the probe's
+    counts; records and counters equal the oracle's on a query sub-range."""
+    rs = synth_reads(5200, 2000, 500_000, 0.02, seed=91)
+    rep = np.frombuffer(b"ACGT", dtype=np.uint8)[np.random.default_rng(92).integers(0, 4, 300)]
+    for i in range(rs.nreads):
+        o = int(rs.offsets[i]) + 100
+        rs.bases[o:o + 300] = rep
+    P = _params(minlen=500)
+    oic = OverlapInCore(P, device=0)
+    oic.load_reads(rs)
+    oic.build_hash_index()
+    hits = oic.seed_hits(1, 1)
+    targets = np.unique(hits["b"][(hits["a_pos_dir"] >> 31) == 0])
+    assert targets.shape[0] > 4096
+    got = oic.fetch(oic.find_overlaps(1, 8))
+    st = oic.stats()
+    oic.close()
+    want, wst = oracle.run_oracle(rs, P.as_dict(), ref_range=(1, 8), with_stats=True)
+    assert st["multi_pass_units"] >= 8
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for f in ("seed_hits", "pairs", "kmer_hits_with_olap", "kmer_hits_without_olap",
+              "total_overlaps"):
+        assert st[f] == wst[f], (f, st[f], wst[f])
