@@ -158,6 +158,10 @@ struct ovl_ctx {
   int n_cu = 256;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8];
+  // find_overlaps runs the extension of hash-batch chunk i on xstream while the probe and
+  // chain of chunk i+1 run on stream; xev[slot] / xev[2 + slot] bracket chunk i's extension
+  hipStream_t xstream = nullptr;
+  hipEvent_t xev[4];
 
   // tables
   int32_t max_errors = 0;
@@ -189,15 +193,18 @@ struct ovl_ctx {
 
   // find_overlaps working buffers: kept across calls (grow-only), hipMalloc of tens of
   // GB per call would cost seconds
+  // [2]: one per pipeline slot (chunk i's extension reads slot i & 1 while the chain of
+  // chunk i + 1 writes the other)
   struct {
-    DBuf<Unit> units;
+    DBuf<Unit> units[2];
     DBuf<uint64_t> rbase;
     DBuf<Probe> probe;
     DBuf<uint32_t> uhits, uflags, ctr, done, dset, big, defer, defer2, okey, oidx, okey2, oidx2;
+    DBuf<uint32_t> xctr[2], xnout;
     DBuf<unsigned long long> chits;
     DBuf<uint8_t> otmp;
-    DBuf<Node> pool, pnodes;
-    DBuf<PairRec> pairs;
+    DBuf<Node> pool, pnodes[2];
+    DBuf<PairRec> pairs[2];
     DBuf<unsigned long long> stats;
     DBuf<int32_t> rows, rowdir, deltas;
   } fb;
@@ -284,11 +291,14 @@ int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
   c->device = device;
   c->n_cu = prop.multiProcessorCount;
   memset(&c->stats, 0, sizeof(c->stats));
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking) != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return fail(OVL_ERR_HIP, "stream create failed");
   }
   for (int i = 0; i < 8; i++) (void)hipEventCreate(&c->ev[i]);
+  for (int i = 0; i < 4; i++) (void)hipEventCreate(&c->xev[i]);
 
   double er = c->P.max_erate;
   c->max_errors = 1 + (int32_t)ceil(er * AS_MAX_READLEN);
@@ -315,9 +325,13 @@ void ovl_ctx_destroy(ovl_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->xstream) (void)hipStreamSynchronize(c->xstream);
   for (int i = 0; i < 8; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  for (int i = 0; i < 4; i++)
+    if (c->xev[i]) (void)hipEventDestroy(c->xev[i]);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->xstream) (void)hipStreamDestroy(c->xstream);
   delete c;
 }
 
@@ -737,12 +751,14 @@ static const uint64_t MAX_STRING_NUM = (1ull << 31) - 1; // overlapInCore.C:57-6
 // it (tests of the capped path).
 static void release_find_buffers(ovl_ctx *c) {
   auto &f = c->fb;
-  f.units.release(); f.rbase.release(); f.probe.release(); f.uhits.release();
+  for (int i = 0; i < 2; i++) {
+    f.units[i].release(); f.pnodes[i].release(); f.pairs[i].release();
+  }
+  f.rbase.release(); f.probe.release(); f.uhits.release();
   f.uflags.release(); f.done.release(); f.dset.release(); f.big.release();
   f.defer.release(); f.defer2.release(); f.okey.release(); f.oidx.release();
   f.okey2.release(); f.oidx2.release(); f.otmp.release(); f.pool.release();
-  f.pnodes.release(); f.pairs.release(); f.rows.release(); f.rowdir.release();
-  f.deltas.release();
+  f.rows.release(); f.rowdir.release(); f.deltas.release();
 }
 
 static uint64_t index_window_cap(ovl_ctx *c) {
@@ -752,7 +768,8 @@ static uint64_t index_window_cap(ovl_ctx *c) {
     const auto &f = c->fb;
     const uint64_t held = 2ull * c->d_tmpR.n * sizeof(Rec2) + 2ull * c->d_occ.n * 8 +
                           (uint64_t)c->d_tab.n * sizeof(TabEntry) + f.probe.n * sizeof(Probe) +
-                          (f.pool.n + f.pnodes.n) * sizeof(Node) + f.pairs.n * sizeof(PairRec) +
+                          (f.pool.n + f.pnodes[0].n + f.pnodes[1].n) * sizeof(Node) +
+                          (f.pairs[0].n + f.pairs[1].n) * sizeof(PairRec) +
                           4ull * (f.rows.n + f.rowdir.n + f.deltas.n);
     const uint64_t avail = fr + held, reserve = 64ull << 30;
     cap = std::min<uint64_t>(cap, avail > reserve ? (avail - reserve) / 112 : 0);
@@ -959,7 +976,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   uint64_t HIT_BUDGET = 1792ull << 20;
   uint64_t win_cap = 1536ull << 20;
   uint64_t WIN_BUDGET = 512ull << 20;           // probe slots per batch (8 B each)
-  auto &d_units = c->fb.units;
   auto &d_rbase = c->fb.rbase;
   auto &d_probe = c->fb.probe;
   auto &d_uhits = c->fb.uhits;
@@ -967,13 +983,19 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   auto &d_ctr = c->fb.ctr;
   auto &d_defer = c->fb.defer;
   auto &d_pool = c->fb.pool;
-  auto &d_pnodes = c->fb.pnodes;
-  auto &d_pairs = c->fb.pairs;
   auto &d_stats = c->fb.stats;
+  // OVL_PIPELINE=1 runs chunk i's extension on a second stream while chunk i+1 is probed and
+  // chained (two buffer slots).  Measured slower (50k x 10 kb: 1.37-1.41 s vs 1.31 s per
+  // job): the extension keeps every CU's issue slots busy, so the co-running probe and chain
+  // only take them from it.  Default: one stream, one slot.
+  const bool pipe = getenv("OVL_PIPELINE") != nullptr;
+  hipStream_t xs = pipe ? c->xstream : s;
   const bool window = c->P.use_window_filter && c->P.max_erate <= 0.06;
   if (window && !c->have_qual)
     return fail(OVL_ERR_BAD_PARAM, "-w (window filter) needs the reads' qualities");
-  if (d_ctr.alloc(16) || d_stats.alloc(16)) return fail(OVL_ERR_OOM, "counters");
+  if (d_ctr.alloc(16) || d_stats.alloc(16) || c->fb.xctr[0].alloc(16) ||
+      c->fb.xctr[1].alloc(16) || c->fb.xnout.alloc(1))
+    return fail(OVL_ERR_OOM, "counters");
   HIPC(hipMemsetAsync(d_stats.p, 0, 128, s));
 
   // ---- extension configuration --------------------------------------------------------
@@ -1110,8 +1132,34 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   c->stats_gen_waves = gen.waves;
   uint32_t chain_waves = 4u * OVL_CHAIN_OCC * c->n_cu;   // OVL_CHAIN_OCC blocks of 4 waves per CU
 
-  size_t out_cap = std::max<size_t>(1u << 20, units.size() * 8);
-  if (c->d_out.alloc(out_cap)) return fail(OVL_ERR_OOM, "output");
+  // With OVL_PIPELINE, chunk i's extension runs on xs while chunk i+1 is probed and chained
+  // on s.  Any return from here on first drains xs (its kernels use this context's buffers).
+  struct Drain {
+    hipStream_t x;
+    ~Drain() { (void)hipStreamSynchronize(x); }
+  } drain{xs};
+  // records: the device counter xnout continues from the records already held (the
+  // driver's earlier hash batches); the host tracks an upper bound (<= 3 per pair)
+  uint32_t nout32 = (uint32_t)c->nout;
+  HIPC(hipMemcpyAsync(c->fb.xnout.p, &nout32, 4, hipMemcpyHostToDevice, s));
+  HIPC(hipStreamSynchronize(s));
+  uint64_t nout_ub = c->nout;
+  auto ensure_out = [&](uint64_t need) -> int {
+    if (need <= c->d_out.n && c->d_out.p) return OVL_OK;
+    HIPC(hipStreamSynchronize(xs));
+    uint32_t cur = 0;
+    HIPC(hipMemcpy(&cur, c->fb.xnout.p, 4, hipMemcpyDeviceToHost));
+    DBuf<Rec> bigger;
+    if (bigger.alloc(need + (need >> 2))) return fail(OVL_ERR_OOM, "output grow");
+    if (cur)
+      HIPC(hipMemcpyAsync(bigger.p, c->d_out.p, sizeof(Rec) * cur, hipMemcpyDeviceToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    std::swap(bigger.p, c->d_out.p);
+    std::swap(bigger.n, c->d_out.n);
+    return OVL_OK;
+  };
+  if (int rc = ensure_out(std::max<uint64_t>(c->nout + (1u << 20), c->nout + units.size() * 8)))
+    return rc;
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
   uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0;
@@ -1120,7 +1168,46 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   uint32_t n_probe_launch = 0, n_ext_launch = 0;
   uint32_t nu = (uint32_t)units.size();
   uint32_t u0 = 0;
+  const uint32_t ctr_next[3] = {5, 11, 13}, ctr_defer[3] = {8, 12, 14};
+  bool pending[2] = {false, false};
+  uint32_t slot_pairs[2] = {0, 0};
+  // chunk i's extension has finished: its counters, class split and time
+  auto collect = [&](int sl) -> int {
+    if (!pending[sl]) return OVL_OK;
+    pending[sl] = false;
+    HIPC(hipEventSynchronize(c->xev[2 + sl]));
+    uint32_t hx[16];
+    HIPC(hipMemcpy(hx, c->fb.xctr[sl].p, 64, hipMemcpyDeviceToHost));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, c->xev[sl], c->xev[2 + sl]);
+    ms_ext += t;
+    if (hx[7] & 32u)
+      return fail(OVL_ERR_UNSUPPORTED, "an extension needs more than 2^28 row cells (error limit "
+                  "%d of a %u-base read): past the generic kernel's per-wave row log",
+                  ecap_of(c->max_len), c->max_len);
+    if (hx[7]) return fail(OVL_ERR_HIP, "extension capacity exceeded (flags %u)", hx[7]);
+    uint32_t left = slot_pairs[sl];
+    for (size_t ci = 0; ci < ext_stage.size(); ci++) {
+      const uint32_t nd = hx[ctr_defer[ci]];
+      if (getenv("OVL_DEBUG"))
+        fprintf(stderr, "OVL_DEBUG class %zu (reads <= %u): deferred %u of %u pairs\n", ci,
+                ext_stage[ci].len, nd, left);
+      if (ci == 0) staged_pairs += left - nd;
+      else long_pairs += left - nd;
+      left = nd;
+    }
+    generic_pairs += left;
+    return OVL_OK;
+  };
+  uint64_t chunk = 0;
   while (u0 < nu) {
+    const int slot = pipe ? (int)(chunk & 1) : 0;
+    // this slot's buffers are free once the extension of chunk i-2 has finished
+    if (int rc = collect(slot)) return rc;
+    auto &d_units = c->fb.units[slot];
+    auto &d_pnodes = c->fb.pnodes[slot];
+    auto &d_pairs = c->fb.pairs[slot];
+    auto &x_ctr = c->fb.xctr[slot];
     // batch by probe slots
     uint32_t u1 = u0;
     uint64_t wsum = 0;
@@ -1303,13 +1390,18 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     uint32_t npairs = hc[3];
     npairs_tot += npairs;
 
+    // ---- the extension of this chunk, queued on xs (the host does not wait for it) ----
+    nout_ub += 3ull * npairs;
+    if (int rc = ensure_out(nout_ub)) return rc;
     ExtendArgs EA;
     EA.R = c->reads();
     EA.units = d_units.p;
     EA.pairs = d_pairs.p;
     EA.npairs = npairs;
+    EA.npairs_dev = nullptr;
+    EA.restore = 0;
     EA.pnodes = d_pnodes.p;
-    EA.pair_next = d_ctr.p + 5;
+    EA.pair_next = x_ctr.p + 5;
     EA.error_bound = c->d_error_bound.p;
     EA.match_limit = c->d_match_limit.p;
     EA.max_errors = c->max_errors;
@@ -1326,121 +1418,104 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     EA.rows = d_rows.p;
     EA.rowdir = d_rowdir.p;
     EA.deltas = d_deltas.p;
-    // output capacity: grow if this batch could exceed it (<= 3 records per pair)
-    uint64_t need = c->nout + 3ull * npairs;
-    if (need > c->d_out.n) {
-      DBuf<Rec> bigger;
-      if (bigger.alloc(need + (need >> 2))) return fail(OVL_ERR_OOM, "output grow");
-      if (c->nout)
-        HIPC(hipMemcpyAsync(bigger.p, c->d_out.p, sizeof(Rec) * c->nout, hipMemcpyDeviceToDevice, s));
-      HIPC(hipStreamSynchronize(s));
-      std::swap(bigger.p, c->d_out.p);
-      std::swap(bigger.n, c->d_out.n);
-    }
-    uint32_t nout32 = (uint32_t)c->nout;
-    HIPC(hipMemcpyAsync(d_ctr.p + 6, &nout32, 4, hipMemcpyHostToDevice, s));
     EA.out = c->d_out.p;
-    EA.nout = d_ctr.p + 6;
+    EA.nout = c->fb.xnout.p;
     EA.out_cap = (uint32_t)std::min<uint64_t>(c->d_out.n, 0xFFFFFFF0ull);
     EA.stats = d_stats.p;
     EA.window = window ? 1 : 0;
-    EA.overflow = d_ctr.p + 7;
+    EA.overflow = x_ctr.p + 7;
     EA.dbg = nullptr;
     if (getenv("OVL_DEBUG")) {
       if (!c->dbg.p) {
+        HIPC(hipStreamSynchronize(xs));
         if (c->dbg.alloc(32)) return fail(OVL_ERR_OOM, "debug counters");
-        HIPC(hipMemsetAsync(c->dbg.p, 0, 256, s));
+        HIPC(hipMemsetAsync(c->dbg.p, 0, 256, xs));
       }
       EA.dbg = c->dbg.p;
     }
     EA.list = nullptr;
     EA.defer = nullptr;
-    if (npairs > 1) {
-      // longest-first work order (node count descending; ties keep pair order)
+    EA.ndefer = nullptr;
+    slot_pairs[slot] = npairs;
+    HIPC(hipMemsetAsync(x_ctr.p, 0, 64, xs));
+    if (npairs) {
+      // the extension-only buffers are shared by the slots: regrowing one waits for xs
       auto &fb = c->fb;
-      if (fb.okey.grow(npairs) || fb.oidx.grow(npairs) || fb.okey2.grow(npairs) ||
-          fb.oidx2.grow(npairs))
-        return fail(OVL_ERR_OOM, "work order");
-      hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
-                         dim3(256), 0, s, d_pairs.p, npairs, fb.okey.p, fb.oidx.p);
-      HIPC(hipGetLastError());
       size_t tmp = 0;
       HIPC(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, fb.okey.p, fb.okey2.p,
                                                         fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
-                                                        32, s));
-      if (fb.otmp.grow(tmp)) return fail(OVL_ERR_OOM, "work order scratch");
-      HIPC(hipcub::DeviceRadixSort::SortPairsDescending(fb.otmp.p, tmp, fb.okey.p, fb.okey2.p,
-                                                        fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
-                                                        32, s));
-      EA.list = fb.oidx2.p;
+                                                        32, xs));
+      if (fb.okey.n < npairs || fb.oidx.n < npairs || fb.okey2.n < npairs || fb.oidx2.n < npairs ||
+          d_defer.n < npairs || fb.defer2.n < npairs || fb.otmp.n < tmp || !fb.otmp.p) {
+        HIPC(hipStreamSynchronize(xs));
+        if (fb.okey.grow(npairs) || fb.oidx.grow(npairs) || fb.okey2.grow(npairs) ||
+            fb.oidx2.grow(npairs) || d_defer.grow(npairs) || fb.defer2.grow(npairs) ||
+            fb.otmp.grow(std::max<size_t>(tmp, 1)))
+          return fail(OVL_ERR_OOM, "work order");
+      }
+      if (npairs > 1) {
+        // longest-first work order (node count descending; ties keep pair order)
+        hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
+                           dim3(256), 0, xs, d_pairs.p, npairs, fb.okey.p, fb.oidx.p);
+        HIPC(hipGetLastError());
+        HIPC(hipcub::DeviceRadixSort::SortPairsDescending(fb.otmp.p, tmp, fb.okey.p, fb.okey2.p,
+                                                          fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
+                                                          32, xs));
+        EA.list = fb.oidx2.p;
+      }
     }
-    HIPC(hipEventRecord(c->ev[6], s));
+    HIPC(hipEventRecord(c->xev[slot], xs));
     if (npairs) {
-      // the staged classes in turn, each deferring what it cannot take to the next list;
-      // the generic kernel takes the last list (or every pair when no class exists)
-      if (d_defer.grow(npairs) || c->fb.defer2.grow(npairs)) return fail(OVL_ERR_OOM, "defer lists");
+      // the staged classes in turn, each deferring what it cannot take to the next list
+      // (whose length the next launch reads from the device counter); the generic kernel
+      // takes the last list, or every pair when no class exists
       uint32_t *defer_buf[2] = {d_defer.p, c->fb.defer2.p};
-      uint32_t left = npairs;
-      const uint32_t ctr_next[3] = {5, 11, 13}, ctr_defer[3] = {8, 12, 14};
-      for (size_t ci = 0; ci < ext_stage.size() && left; ci++) {
+      for (size_t ci = 0; ci < ext_stage.size(); ci++) {
         const ExtClass &g = ext_stage[ci];
         EA.e_cap = g.ecap;
         EA.rows_cap = g.stride;
         EA.sw_words = g.sw;
         EA.stage_len = (int32_t)g.len;
-        EA.npairs = left;
-        EA.pair_next = d_ctr.p + ctr_next[ci];
+        EA.pair_next = x_ctr.p + ctr_next[ci];
         EA.defer = defer_buf[ci & 1];
-        EA.ndefer = d_ctr.p + ctr_defer[ci];
+        EA.ndefer = x_ctr.p + ctr_defer[ci];
         n_ext_launch++;
         if (g.l16)
-          hipLaunchKernelGGL((k_extend<true, true>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, s, EA);
+          hipLaunchKernelGGL((k_extend<true, true>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
         else
-          hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, s, EA);
+          hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
         HIPC(hipGetLastError());
-        uint32_t nd = 0;
-        HIPC(hipMemcpyAsync(&nd, d_ctr.p + ctr_defer[ci], 4, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
-        if (getenv("OVL_DEBUG"))
-          fprintf(stderr, "OVL_DEBUG class %zu (reads <= %u): deferred %u of %u pairs\n", ci, g.len,
-                  nd, left);
-        if (ci == 0) staged_pairs += left - nd;
-        else long_pairs += left - nd;
-        left = nd;
         EA.list = defer_buf[ci & 1];
+        EA.npairs_dev = x_ctr.p + ctr_defer[ci];
+        EA.restore = 1;          // a deferred pair may have had nodes removed (~Len)
       }
-      if (left) {
-        EA.e_cap = gen.ecap;
-        EA.rows_cap = gen.stride;
-        EA.sw_words = 0;
-        EA.stage_len = 0;
-        EA.npairs = left;
-        EA.pair_next = d_ctr.p + 9;
-        EA.defer = nullptr;
-        EA.ndefer = nullptr;
-        generic_pairs += left;
-        n_ext_launch++;
-        if (gen.l16)
-          hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
-                             gen.lds, s, EA);
-        else
-          hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
-                             gen.lds, s, EA);
-      }
+      EA.e_cap = gen.ecap;
+      EA.rows_cap = gen.stride;
+      EA.sw_words = 0;
+      EA.stage_len = 0;
+      EA.pair_next = x_ctr.p + 9;
+      EA.defer = nullptr;
+      EA.ndefer = nullptr;
+      n_ext_launch++;
+      if (gen.l16)
+        hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                           gen.lds, xs, EA);
+      else
+        hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                           gen.lds, xs, EA);
+      HIPC(hipGetLastError());
     }
-    HIPC(hipGetLastError());
-    HIPC(hipEventRecord(c->ev[7], s));
-    HIPC(hipMemcpyAsync(hc, d_ctr.p, 64, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    (void)hipEventElapsedTime(&t, c->ev[6], c->ev[7]);
-    ms_ext += t;
-    if (hc[7] & 32u)
-      return fail(OVL_ERR_UNSUPPORTED, "an extension needs more than 2^28 row cells (error limit "
-                  "%d of a %u-base read): past the generic kernel's per-wave row log", gen.ecap,
-                  c->max_len);
-    if (hc[7]) return fail(OVL_ERR_HIP, "extension capacity exceeded (flags %u)", hc[7]);
-    c->nout = hc[6];
+    HIPC(hipEventRecord(c->xev[2 + slot], xs));
+    pending[slot] = true;
+    chunk++;
     u0 += nc;
+  }
+  for (int sl = 0; sl < 2; sl++)
+    if (int rc = collect(sl)) return rc;
+  {
+    uint32_t n = 0;
+    HIPC(hipMemcpy(&n, c->fb.xnout.p, 4, hipMemcpyDeviceToHost));
+    c->nout = n;
   }
   unsigned long long hs[16];
   HIPC(hipMemcpy(hs, d_stats.p, 128, hipMemcpyDeviceToHost));
@@ -1527,16 +1602,16 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
     acc = 0;
     for (uint32_t i = 0; i < nb; i++) { rbase[i] = acc; acc += uwin[u0 + i]; }
     rbase[nb] = acc;
-    if (fb.units.grow(nb) || fb.rbase.grow(nb + 1) || fb.probe.grow(acc) ||
+    if (fb.units[0].grow(nb) || fb.rbase.grow(nb + 1) || fb.probe.grow(acc) ||
         fb.uhits.grow(nb) || fb.uflags.grow(nb) || ucnt.grow(nb) || ubase.grow(nb))
       return fail(OVL_ERR_OOM, "seed-hit buffers");
-    HIPC(hipMemcpyAsync(fb.units.p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(fb.units[0].p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(fb.rbase.p, rbase.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
     HIPC(hipEventRecord(c->ev[2], s));
     ProbeArgs PA;
     PA.R = c->reads();
     PA.X = index_dev(c);
-    PA.units = fb.units.p;
+    PA.units = fb.units[0].p;
     PA.rbase = fb.rbase.p;
     PA.nunits = nb;
     PA.out = fb.probe.p;
@@ -1547,7 +1622,7 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
     HitArgs HA;
     HA.R = c->reads();
     HA.occ = c->d_occ.p;
-    HA.units = fb.units.p;
+    HA.units = fb.units[0].p;
     HA.rbase = fb.rbase.p;
     HA.probes = fb.probe.p;
     HA.nunits = nb;
@@ -1573,7 +1648,7 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
       HIPC(hipMemcpyAsync(ubase.p, base.data(), 8ull * nb, hipMemcpyHostToDevice, s));
       HA.unit_base = ubase.p;
       HA.out = hbuf.p;
-      HA.units = fb.units.p + p0;
+      HA.units = fb.units[0].p + p0;
       HA.rbase = fb.rbase.p + p0;
       HA.unit_base = ubase.p + p0;
       HA.nunits = p1 - p0;

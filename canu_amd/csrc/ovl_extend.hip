@@ -26,6 +26,8 @@ struct ExtendArgs {
   const Unit *units;
   const PairRec *pairs;
   uint32_t npairs;
+  const uint32_t *npairs_dev;   // non-null: the pair count is there (an earlier launch's defers)
+  int32_t restore;              // the list holds deferred pairs: undo their node removals
   Node *pnodes;                 // Len < 0 marks a node removed from its list
   uint32_t *pair_next;
   const uint32_t *list;   // non-null: process pairs[list[0 .. npairs)] instead of pairs[0 .. npairs)
@@ -1647,17 +1649,26 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
   int32_t *RD = stk + (X.e_cap + 8);
   int32_t *LD = RD + (X.e_cap + 8);
   unsigned long long st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t npairs = X.npairs_dev ? __builtin_amdgcn_readfirstlane(*X.npairs_dev) : X.npairs;
 
   for (;;) {
     uint32_t pi = 0;
     if (lane == 0) pi = atomicAdd(X.pair_next, 1u);
     pi = __shfl(pi, 0);
-    if (pi >= X.npairs) break;
+    if (pi >= npairs) break;
     if (X.list) pi = X.list[pi];
     PairRec P = X.pairs[pi];
     Unit un = X.units[P.unit];
     Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
     Strand T = strand_fwd(X.R, P.tgt);
+    if (X.restore) {
+      // a pair deferred by an earlier launch may have had nodes removed (~Len) before it
+      // stopped there
+      Node *nodes = X.pnodes + P.node_off;
+      for (uint32_t i = lane; i < P.node_cnt; i += 64)
+        if (nodes[i].Len < 0) nodes[i].Len = ~nodes[i].Len;
+      vm_sync();
+    }
     if constexpr (STAGE) {
       bool ok = false;
       if (!(S.ex_wild || S.ex_nul || T.ex_wild) && S.len <= X.stage_len && T.len <= X.stage_len) {
@@ -1673,13 +1684,6 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
       }
       if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
     } else {
-      if (X.list) {
-        // a deferred pair may have had nodes removed (~Len) before it overflowed
-        Node *nodes = X.pnodes + P.node_off;
-        for (uint32_t i = lane; i < P.node_cnt; i += 64)
-          if (nodes[i].Len < 0) nodes[i].Len = ~nodes[i].Len;
-        vm_sync();
-      }
       process_pair<false, L16>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
     }
     lds_sync();
