@@ -13,11 +13,21 @@ from __future__ import annotations
 import numpy as np
 
 
-def query_shards(n: int, world: int, first: int = 1) -> list[tuple[int, int]]:
-    """Split query IDs first..first+n-1 so every rank gets about the same number of (a, b>a)
-    pairs: read a is paired with the n-a reads after it.  Ranges are inclusive and may be
-    empty (lo > hi) when world > n."""
-    w = np.arange(n, 0, -1, dtype=np.float64) - 1.0
+# A query's cost in units of one (a, b > a) pair's: the extension work of read a grows with
+# the n - a reads after it, but its probe and chain scan every occurrence of its k-mers
+# whatever their IDs (Find_Overlaps.C:328 filters them afterwards).  Measured on 50k x 10 kb
+# (1 MI355X): seed 125 ms for 50k queries against extension 1,142 ms for n^2/2 pair
+# weights, i.e. ~0.055 n pairs' worth per query.  Without it the last shard, which holds the
+# most queries, ran 19 % longer than the others.
+QUERY_FIXED_COST = 0.055
+
+
+def query_shards(n: int, world: int, first: int = 1,
+                 fixed: float = QUERY_FIXED_COST) -> list[tuple[int, int]]:
+    """Split query IDs first..first+n-1 so every rank gets about the same work: read a costs
+    its n-a later reads (the pairs it searches) plus `fixed` * n for its own probe and chain.
+    Ranges are inclusive and may be empty (lo > hi) when world > n."""
+    w = np.arange(n, 0, -1, dtype=np.float64) - 1.0 + fixed * n
     c = np.cumsum(w)
     tot = c[-1] if n else 0.0
     out, lo = [], 1
