@@ -102,3 +102,68 @@ def all_gather_rows(local, n: int, dist):
     got = [torch.empty_like(pad) for _ in range(world)]
     _all_gather(dist, got, pad)
     return torch.cat([g[:hi - lo] for g, (lo, hi) in zip(got, sl)])
+
+
+# configs[4] (4M x 12 kb on 8 GPUs): per-unit costs measured by tools/rehearse_configs4.py on
+# one MI355X (500k x 12 kb, 15x, --hashbits 26 --hashload 0.75: 4 hash batches, 23.7 s):
+#   extension  19.7 s for 9.0 M pairs       -> ~2.2 us per (a < b) candidate pair
+#   seed        2.2 s for 48 G query windows probed (500k queries x 2 strands x ~12 k x 4)
+#   index       1.4 s for 6 G hashed windows
+REHEARSAL_COSTS = {"pair_s": 19.7 / 9.0e6, "probe_window_s": 2.2 / 48e9,
+                   "index_window_s": 1.4 / 6.0e9}
+
+
+def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
+                    batch_windows: float, costs: dict | None = None) -> list[dict]:
+    """canu's partitioning model with GPU-sized blocks: rank r runs ONE overlapInCore job
+    (`-h lo_r-hi_r -r 1-hi_r`, the reference's OverlapDriver batches inside it) over a
+    contiguous hash block; every (a < b) pair is found by the rank whose block holds b.
+    pairs_per_read: candidate partners of a read among all reads (both sides; 36 for the
+    rehearsal's 15x), of which read b has ~b / n before it.  Block r's work: its hashed
+    reads' pairs with earlier reads, its index batches (batch_windows k-mers each), and
+    every query a <= hi_r probing each batch.  Blocks
+    are cut so the ranks' modelled times agree (the triangular pair count makes the first
+    block the widest).  Returns per rank {"h": (lo, hi), "r": (1, hi), "est_s": seconds}."""
+    c = dict(REHEARSAL_COSTS if costs is None else costs)
+    w = max(read_len - 21.0, 1.0)                 # windows per read and strand (k = 22)
+
+    def cost(lo: int, hi: int) -> float:
+        if hi < lo:
+            return 0.0
+        m = hi - lo + 1
+        pairs = pairs_per_read * (lo + hi) / 2.0 * m / n    # sum over b of b * ppr / n
+        batches = max(1.0, m * w / batch_windows)
+        probe = hi * 2.0 * w * batches
+        return (pairs * c["pair_s"] + probe * c["probe_window_s"] +
+                m * w * c["index_window_s"])
+
+    def cut(target: float) -> list[int]:
+        ends, lo = [], 1
+        for _ in range(world - 1):
+            a, b = lo - 1, n
+            while a < b:                            # largest hi with cost(lo, hi) <= target
+                mid = (a + b + 1) // 2
+                if cost(lo, mid) <= target:
+                    a = mid
+                else:
+                    b = mid - 1
+            ends.append(a)
+            lo = a + 1
+        ends.append(n)
+        return ends
+
+    lo_t, hi_t = 0.0, cost(1, n)
+    for _ in range(60):                             # the smallest target the last rank meets
+        mid = (lo_t + hi_t) / 2.0
+        ends = cut(mid)
+        lo_last = (ends[-2] + 1) if world > 1 else 1
+        if cost(lo_last, n) <= mid:
+            hi_t = mid
+        else:
+            lo_t = mid
+    ends = cut(hi_t)
+    jobs, lo = [], 1
+    for hi in ends:
+        jobs.append({"h": (lo, hi), "r": (1, hi), "est_s": round(cost(lo, hi), 2)})
+        lo = hi + 1
+    return jobs

@@ -77,3 +77,20 @@ def test_synth_slices_match_whole():
     assert b.first_iid == 18
     assert np.array_equal(np.concatenate([a.bases, b.bases]), whole.bases)
     assert np.array_equal(np.concatenate([a.lengths, b.lengths]), whole.lengths)
+
+
+def test_hash_block_jobs_cover_and_balance():
+    """configs[4]'s per-rank overlapInCore jobs: contiguous hash blocks covering every read,
+    each searched by every earlier read (so each a < b pair is found once), equal modelled
+    time per rank, the first block the widest (triangular pair count)."""
+    from canu_amd.dist import hash_block_jobs
+    js = hash_block_jobs(4_000_000, 8, 12_000, 36.0, 1.6e9)
+    assert js[0]["h"][0] == 1 and js[-1]["h"][1] == 4_000_000
+    for a, b in zip(js, js[1:]):
+        assert b["h"][0] == a["h"][1] + 1
+    for j in js:
+        assert j["r"] == (1, j["h"][1])
+    est = [j["est_s"] for j in js]
+    assert max(est) / min(est) < 1.02
+    widths = [j["h"][1] - j["h"][0] for j in js]
+    assert widths == sorted(widths, reverse=True)
