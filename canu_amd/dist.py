@@ -13,31 +13,62 @@ from __future__ import annotations
 import numpy as np
 
 
-# A query's cost in units of one (a, b > a) pair's: the extension work of read a grows with
-# the n - a reads after it, but its probe and chain scan every occurrence of its k-mers
-# whatever their IDs (Find_Overlaps.C:328 filters them afterwards).  Measured on 50k x 10 kb
-# (1 MI355X): seed 125 ms for 50k queries against extension 1,142 ms for n^2/2 pair
-# weights, i.e. ~0.055 n pairs' worth per query.  Without it the last shard, which holds the
-# most queries, ran 19 % longer than the others.
-QUERY_FIXED_COST = 0.055
+# The cost model of one rank's job, from the 1-GPU step on 50k x 10 kb (1 MI355X): index
+# 37 ms over every hashed read, probe 37 ms and chain 87 ms over every query, extension
+# 1,146 ms over the n^2/2 (a, b > a) pairs.  A query shard [lo, hi] only ever pairs with reads
+# b > a >= lo (Find_Overlaps.C:328 keeps targets with a larger ID), so its rank indexes
+# reads lo..n only: the same records and counters, a smaller index, and occurrence lists
+# (chain work) shortened by (n - lo) / n.
+SHARD_COSTS = {"index_per_read": 37.0 / 50_000, "probe_per_query": 37.0 / 50_000,
+               "chain_per_query": 87.0 / 50_000, "pair": 1146.0 / (50_000 ** 2 / 2)}
+
+
+def shard_cost(n: int, lo: int, hi: int, costs: dict | None = None) -> float:
+    """Modelled time of the rank searching queries lo..hi (index over lo..n)."""
+    c = SHARD_COSTS if costs is None else costs
+    if hi < lo:
+        return 0.0
+    q = hi - lo + 1
+    hashed = n - lo + 1
+    pairs = q * (2 * n - lo - hi) / 2.0                # sum of n - a over the shard
+    return (c["index_per_read"] * hashed + c["probe_per_query"] * q +
+            c["chain_per_query"] * q * hashed / n + c["pair"] * pairs)
 
 
 def query_shards(n: int, world: int, first: int = 1,
-                 fixed: float = QUERY_FIXED_COST) -> list[tuple[int, int]]:
-    """Split query IDs first..first+n-1 so every rank gets about the same work: read a costs
-    its n-a later reads (the pairs it searches) plus `fixed` * n for its own probe and chain.
-    Ranges are inclusive and may be empty (lo > hi) when world > n."""
-    w = np.arange(n, 0, -1, dtype=np.float64) - 1.0 + fixed * n
-    c = np.cumsum(w)
-    tot = c[-1] if n else 0.0
-    out, lo = [], 1
-    for r in range(world):
-        if r == world - 1:
-            hi = n
+                 costs: dict | None = None) -> list[tuple[int, int]]:
+    """Split query IDs first..first+n-1 into `world` contiguous shards of equal modelled
+    time (shard_cost: each rank indexes its own lo..n).  Ranges are inclusive and may be
+    empty (lo > hi) when world > n."""
+    if n <= 0:
+        return [(first, first - 1)] * world
+
+    def cut(target: float) -> list[int]:
+        ends, lo = [], 1
+        for _ in range(world - 1):
+            a, b = lo - 1, n
+            while a < b:                               # largest hi with cost <= target
+                mid = (a + b + 1) // 2
+                if shard_cost(n, lo, mid, costs) <= target:
+                    a = mid
+                else:
+                    b = mid - 1
+            ends.append(a)
+            lo = a + 1
+        ends.append(n)
+        return ends
+
+    lo_t, hi_t = 0.0, shard_cost(n, 1, n, costs)
+    for _ in range(60):
+        mid = (lo_t + hi_t) / 2.0
+        ends = cut(mid)
+        last_lo = ends[-2] + 1 if world > 1 else 1
+        if shard_cost(n, last_lo, n, costs) <= mid:
+            hi_t = mid
         else:
-            hi = int(np.searchsorted(c, tot * (r + 1) / world)) + 1
-            hi = max(hi, lo - 1)
-            hi = min(hi, n)
+            lo_t = mid
+    out, lo = [], 1
+    for hi in cut(hi_t):
         out.append((first - 1 + lo, first - 1 + hi))
         lo = hi + 1
     return out

@@ -40,7 +40,8 @@ def _worker(rank, world, port, q):
     rs = ReadSet(bases=bases.numpy(), offsets=offsets, lengths=lengths)
     p = oracle.default_params(kmer_len=22, max_erate=0.06, min_olap_len=200)
     q_lo, q_hi = query_shards(n, world)[rank]
-    mine = oracle.run_oracle(rs, p, ref_range=(q_lo, q_hi))
+    # each rank indexes only reads q_lo..n: its queries' targets all have larger IDs
+    mine = oracle.run_oracle(rs, p, hash_range=(q_lo, n), ref_range=(q_lo, q_hi))
     counts = [None] * world
     dist.all_gather_object(counts, mine.tobytes())
     if rank == 0:

@@ -34,14 +34,15 @@ def test_golden_gpu(built, name):
     assert np.array_equal(got, want)
 
 
-def _run(rs, P, ref=None):
+def _run(rs, P, ref=None, hash_lo=1, with_stats=False):
     oic = OverlapInCore(P, device=0)
     oic.load_reads(rs)
-    oic.build_hash_index(1, rs.nreads)
+    oic.build_hash_index(hash_lo, rs.nreads)
     n = oic.find_overlaps(*(ref or (1, rs.nreads)))
     rec = oic.fetch(n)
+    st = oic.stats()
     oic.close()
-    return rec
+    return (rec, st) if with_stats else rec
 
 
 @pytest.fixture(scope="module")
@@ -67,6 +68,17 @@ def test_ont_shards_union_and_determinism(built, ont):
     from canu_amd.dist import query_shards
     parts = [_run(ont, P, ref=r) for r in query_shards(ont.nreads, 4)]
     assert np.array_equal(oracle.sort_records(np.concatenate(parts)), whole)
+    # a rank indexes only reads lo..n (its queries' targets all have larger IDs): the same
+    # records and counters as against the whole index (the multi-GPU bench does this)
+    for lo, hi in query_shards(ont.nreads, 4)[1:]:
+        full, sf = _run(ont, P, ref=(lo, hi), with_stats=True)
+        part, sp = _run(ont, P, ref=(lo, hi), hash_lo=lo, with_stats=True)
+        assert np.array_equal(part, full)
+        for f in ("kmer_hits_with_olap", "kmer_hits_without_olap", "kmer_hits_skipped",
+                  "multi_overlaps", "total_overlaps", "contained_overlaps", "dovetail_overlaps",
+                  "pairs"):
+            assert sp[f] == sf[f], (f, sp[f], sf[f])
+        assert sp["seed_hits"] <= sf["seed_hits"]
     # record invariants: hangs within the reads, span positive, evalue in range
     L = ont.lengths.astype(np.int64)
     a, b = whole["a"].astype(np.int64) - 1, whole["b"].astype(np.int64) - 1

@@ -3,7 +3,7 @@ the synthetic read generator."""
 import numpy as np
 import pytest
 
-from canu_amd.dist import QUERY_FIXED_COST, query_shards
+from canu_amd.dist import query_shards, shard_cost
 from canu_amd.overlap_in_core import (UINT64_MAX, OicParameters, parse_overlapInCore_args,
                                       read_skip_fasta)
 from canu_amd.synth import synth_reads
@@ -60,12 +60,10 @@ def test_query_shards_cover_and_balance(n, world):
     ids = [i for lo, hi in sh for i in range(lo, hi + 1)]
     assert ids == list(range(1, n + 1))
     if n >= 1000:
-        # the cost model: a query's later reads plus its own probe / chain (QUERY_FIXED_COST)
-        cost = [sum(n - a + QUERY_FIXED_COST * n for a in range(lo, hi + 1)) for lo, hi in sh]
+        # equal modelled time (index lo..n, probe and chain per query, pairs)
+        cost = [shard_cost(n, lo, hi) for lo, hi in sh]
         assert max(cost) / (sum(cost) / world) < 1.01
-        # pairs alone: the later shards hold fewer, as their queries' probes cost the same
-        pairs = [sum(n - a for a in range(lo, hi + 1)) for lo, hi in sh]
-        assert pairs[-1] < pairs[0]
+
 
 
 def test_synth_slices_match_whole():
