@@ -72,6 +72,30 @@ def build_cli(force: bool = False, verbose: bool = True) -> str:
     return CLI_OUT
 
 
+MHAP_CLI_OUT = os.path.join(BIN_DIR, "mhap")
+
+
+def build_mhap_cli(force: bool = False, verbose: bool = True) -> str:
+    """canu_amd/bin/mhap: the MHAP command line canu's mhap.sh / precompute.sh run (host
+    C++ over libcanu_mhap.so, found next to it through the rpath; zlib for -f .gz)."""
+    lib = build_mhap(verbose=verbose)
+    src = os.path.join(CSRC, "mhap_main.cpp")
+    deps = [src, lib, os.path.join(HERE, "..", "include", "canu_mhap.h")]
+    if not force and os.path.exists(MHAP_CLI_OUT) and \
+            all(os.path.getmtime(d) <= os.path.getmtime(MHAP_CLI_OUT) for d in deps):
+        return MHAP_CLI_OUT
+    os.makedirs(BIN_DIR, exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(HERE, "..", "include"),
+           "-o", MHAP_CLI_OUT + ".tmp", src, "-L" + OUT_DIR, "-lcanu_mhap", "-lz",
+           "-Wl,-rpath,$ORIGIN/../lib", "-Wl,--allow-shlib-undefined"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(MHAP_CLI_OUT + ".tmp", MHAP_CLI_OUT)
+    return MHAP_CLI_OUT
+
+
 def build(force: bool = False, verbose: bool = True, profile: bool = False) -> str:
     """profile=True builds the instrumented variant (in-kernel cycle stamps, OVL_DEBUG=1
     prints them) as libcanu_ovl_prof.so; load it with CANU_OVL_LIB."""

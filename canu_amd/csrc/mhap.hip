@@ -340,13 +340,14 @@ __global__ void __launch_bounds__(256) k_mh_ordered(OrderedArgs A) {
 }
 
 // MinHash index keys: (j << 32 | value ^ 0x80000000), value = read; invalid -> table H.
-__global__ void k_mh_index_keys(const int32_t *mh, uint32_t nreads, int32_t H, uint64_t *keys,
-                                uint32_t *vals) {
+// rows r0 .. r0 + nreads - 1 of the sketch (the indexed reads)
+__global__ void k_mh_index_keys(const int32_t *mh, uint32_t r0, uint32_t nreads, int32_t H,
+                                uint64_t *keys, uint32_t *vals) {
   size_t n = (size_t)nreads * H;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
        e += (size_t)gridDim.x * blockDim.x) {
-    uint32_t r = (uint32_t)(e / H), j = (uint32_t)(e % H);
-    int32_t v = mh[e];
+    uint32_t r = r0 + (uint32_t)(e / H), j = (uint32_t)(e % H);
+    int32_t v = mh[(size_t)r0 * H + e];
     keys[e] = (v == I32MAX) ? ((uint64_t)H << 32)
                             : (((uint64_t)j << 32) | ((uint32_t)v ^ 0x80000000u));
     vals[e] = r;
@@ -373,6 +374,7 @@ struct CandArgs {
   const uint64_t *toff;
   int32_t H;
   uint32_t q0, q1;              // queries [q0, q1), 0-based
+  uint32_t all_targets;         // 0: targets t > q (all-vs-all, each pair once); 1: t != q
   uint32_t min_matches;
   Cand *out;
   uint32_t *nout;
@@ -406,7 +408,7 @@ __global__ void __launch_bounds__(256) k_mh_candidates(CandArgs A) {
     const uint64_t end = A.toff[j + 1];
     for (uint64_t i = lo; i < end && A.keys[i] == key; i++) {
       const uint32_t t = A.vals[i];
-      if (t <= q) continue;
+      if (A.all_targets ? t == q : t <= q) continue;
       uint32_t sl = (t * 2654435761u) >> TSHIFT;
       uint32_t probes = 0;
       for (;;) {
@@ -851,6 +853,8 @@ int mhap_set_filter_kmers(mhap_ctx *c, const char *kmers, uint64_t n) {
 
 int mhap_sketch(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
+  if (!c->d_bases || !c->d_off)
+    return mfail(M_STATE, "no bases loaded (lengths only: import sketches instead)");
   if (bgn < c->first_iid || end >= c->first_iid + c->nreads || bgn > end)
     return mfail(M_BAD_PARAM, "sketch range %u-%u outside the loaded reads", bgn, end);
   MHC(hipSetDevice(c->device));
@@ -913,17 +917,48 @@ int mhap_copy_sketches(mhap_ctx *c, uint32_t first, uint32_t n, void *d_minhash,
   return M_OK;
 }
 
+int mhap_copy_sketches_host(mhap_ctx *c, uint32_t first, uint32_t n, void *h_minhash,
+                            void *h_ordered, void *h_ocount, int to_ctx) {
+  if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
+  if (n == 0) return M_OK;
+  if (first < c->first_iid || (uint64_t)first + n > (uint64_t)c->first_iid + c->nreads)
+    return mfail(M_BAD_PARAM, "rows %u..%u outside the loaded reads", first, first + n - 1);
+  if (!h_minhash || !h_ordered || !h_ocount) return mfail(M_BAD_PARAM, "null buffer");
+  MHC(hipSetDevice(c->device));
+  const size_t r0 = first - c->first_iid;
+  const size_t H = c->P.num_hashes, S = c->P.ordered_sketch;
+  struct { void *ctx; void *user; size_t bytes; } parts[3] = {
+      {c->minhash.p + r0 * H, h_minhash, 4 * H * n},
+      {c->ordered.p + r0 * S, h_ordered, 8 * S * n},
+      {c->ocount.p + r0, h_ocount, 4ull * n}};
+  for (auto &pt : parts) {
+    if (to_ctx) MHC(hipMemcpyAsync(pt.ctx, pt.user, pt.bytes, hipMemcpyHostToDevice, c->stream));
+    else        MHC(hipMemcpyAsync(pt.user, pt.ctx, pt.bytes, hipMemcpyDeviceToHost, c->stream));
+  }
+  MHC(hipStreamSynchronize(c->stream));
+  if (to_ctx) c->indexed = false;
+  return M_OK;
+}
+
 int mhap_build_index(mhap_ctx *c) {
   if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
+  return mhap_build_index_range(c, c->first_iid, c->first_iid + c->nreads - 1);
+}
+
+int mhap_build_index_range(mhap_ctx *c, uint32_t bgn, uint32_t end) {
+  if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
+  if (bgn < c->first_iid || end >= c->first_iid + c->nreads || bgn > end)
+    return mfail(M_BAD_PARAM, "index range %u-%u outside the loaded reads", bgn, end);
   MHC(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const int32_t H = (int32_t)c->P.num_hashes;
-  const size_t n = (size_t)c->nreads * H;
+  const uint32_t r0 = bgn - c->first_iid, nr = end - bgn + 1;
+  const size_t n = (size_t)nr * H;
   if (c->keys.alloc(n) || c->vals.alloc(n) || c->keys2.alloc(n) || c->vals2.alloc(n) ||
       c->toff.alloc(H + 1))
     return mfail(M_OOM, "index (%zu entries)", n);
   MHC(hipEventRecord(c->ev[0], s));
-  hipLaunchKernelGGL(k_mh_index_keys, dim3(4096), dim3(256), 0, s, c->minhash.p, c->nreads, H,
+  hipLaunchKernelGGL(k_mh_index_keys, dim3(4096), dim3(256), 0, s, c->minhash.p, r0, nr, H,
                      c->keys.p, c->vals.p);
   MHC(hipGetLastError());
   int end_bit = 32;
@@ -945,7 +980,19 @@ int mhap_build_index(mhap_ctx *c) {
   return M_OK;
 }
 
+static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_targets,
+                        uint64_t *n_out);
+
 int mhap_compare(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+  return compare_impl(c, bgn, end, 0, n_out);
+}
+
+int mhap_compare_all(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+  return compare_impl(c, bgn, end, 1, n_out);
+}
+
+static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_targets,
+                        uint64_t *n_out) {
   if (!c || !c->indexed) return mfail(M_STATE, "mhap_build_index() first");
   if (bgn < c->first_iid || end >= c->first_iid + c->nreads || bgn > end)
     return mfail(M_BAD_PARAM, "query range %u-%u outside the loaded reads", bgn, end);
@@ -962,7 +1009,8 @@ int mhap_compare(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
     if (c->cand.alloc(cap)) return mfail(M_OOM, "candidates");
     MHC(hipMemsetAsync(c->ctr.p, 0, 64, s));
     CandArgs CA{c->minhash.p, c->keys2.p, c->vals2.p, c->toff.p, (int32_t)c->P.num_hashes,
-                q0, q1, c->P.min_matches, c->cand.p, c->ctr.p, (uint32_t)cap, c->ctr.p + 1};
+                q0, q1, all_targets, c->P.min_matches, c->cand.p, c->ctr.p, (uint32_t)cap,
+                c->ctr.p + 1};
     MHC(hipEventRecord(c->ev[0], s));
     hipLaunchKernelGGL(k_mh_candidates, dim3((nq + 3) / 4), dim3(256),
                        2 * 4 * TSLOTS * sizeof(uint32_t), s, CA);

@@ -1,0 +1,362 @@
+// mhap_main.cpp -- canu_amd/bin/mhap: the MHAP command line canu's pipeline runs
+// (src/pipelines/canu/OverlapMhap.pm:374-498), over libcanu_mhap.so.  canu calls the jar
+// twice; a maintainer replaces `$javaPath ... -jar $bin/mhap-2.1.2.jar` with `$bin/mhap`
+// and keeps every option:
+//
+//   precompute.sh:  mhap <sketch options> [-f frequentMers.ignore.gz] -p ./$job.input.fasta -q .
+//                   -> ./$job.input.dat  (the block's sketches; canu renames it $job.dat)
+//   mhap.sh:        mhap <sketch options> -s ./blocks/$blk.dat [--no-self] -q queries/$qry
+//                   > ./results/$qry.mhap
+//
+// Read numbering follows the jar's (OverlapMhap.pm:227-232, mhapConvert.C:119-120): the
+// hash block's reads are 1..N, the query files' reads (in file-name order) N+1..N+M.  The
+// compute step reports the hash block against itself (each pair once) unless --no-self,
+// then every query read against every hash read, one line per overlap:
+//   query-id hash-id erate shared-min-mers 0 a-bgn a-end a-len b-rc b-bgn b-end b-len
+// The .dat format is this executable's own (the jar's is internal to it): a header, the
+// read lengths and the three sketch arrays of include/canu_mhap.h.
+//
+// The jar's tf-idf repeat weighting (--repeat-weight, --repeat-idf-scale,
+// --filter-threshold) is not implemented: those options are accepted with a warning and
+// the sketch is unweighted; -f k-mers at or above --filter-threshold are left out of the
+// sketch.  --no-tf / --supress-noise are rejected.  See DESIGN.md.
+#include <zlib.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include <dirent.h>
+#include <sys/stat.h>
+
+#include "canu_mhap.h"
+
+namespace {
+
+const char kMagic[8] = {'C', 'A', 'M', 'H', 'A', 'P', '0', '1'};
+
+struct Block {
+  uint32_t k = 0, H = 0, S = 0, ok = 0, n = 0;
+  std::vector<uint32_t> len;
+  std::vector<int32_t> minhash;
+  std::vector<uint64_t> ordered;
+  std::vector<uint32_t> ocount;
+};
+
+int usage(const char *prog) {
+  fprintf(stderr,
+          "usage: %s [sketch options] [-f filter.gz] -p reads.fasta -q outdir      (precompute)\n"
+          "       %s [sketch options] -s block.dat [--no-self] [-q dir|file.dat]  (compute)\n"
+          "sketch options (the jar's, as canu passes them):\n"
+          "  -k n  --num-hashes n  --num-min-matches n  --threshold x\n"
+          "  --ordered-sketch-size n  --ordered-kmer-size n  --min-olap-length n\n"
+          "  --num-threads n (ignored: one GPU)   CANU_MHAP_DEVICE picks the GPU\n"
+          "  --repeat-weight x  --repeat-idf-scale x  --filter-threshold x  (accepted, unweighted)\n",
+          prog, prog);
+  return 1;
+}
+
+bool read_fasta(const char *path, std::vector<uint8_t> &bases, std::vector<uint64_t> &off,
+                std::vector<uint32_t> &len) {
+  FILE *F = fopen(path, "r");
+  if (!F) return false;
+  char *line = nullptr;
+  size_t cap = 0;
+  ssize_t got;
+  bool in_read = false;
+  while ((got = getline(&line, &cap, F)) >= 0) {
+    if (got > 0 && line[0] == '>') {
+      off.push_back(bases.size());
+      len.push_back(0);
+      in_read = true;
+      continue;
+    }
+    if (!in_read) continue;
+    for (ssize_t i = 0; i < got; i++) {
+      char ch = line[i];
+      if (ch == '\n' || ch == '\r' || ch == ' ' || ch == '\t') continue;
+      ch = (char)(ch & ~0x20);
+      if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T') ch = 'N';
+      bases.push_back((uint8_t)ch);
+      len.back()++;
+    }
+  }
+  free(line);
+  fclose(F);
+  return true;
+}
+
+// canu's frequentMers.ignore.gz (Meryl.pm:699-712): a count line, then "kmer<TAB>fraction"
+// for both orientations.  gzopen reads plain files too.
+bool read_filter(const char *path, uint32_t k, double threshold, std::string &kmers,
+                 uint64_t &n) {
+  gzFile G = gzopen(path, "rb");
+  if (!G) return false;
+  char buf[4096];
+  n = 0;
+  while (gzgets(G, buf, sizeof buf)) {
+    char *tab = strchr(buf, '\t');
+    if (!tab) continue;                          // the count line
+    const size_t L = (size_t)(tab - buf);
+    const double frac = strtod(tab + 1, nullptr);
+    if (L != k || frac < threshold) continue;
+    kmers.append(buf, L);
+    n++;
+  }
+  gzclose(G);
+  return true;
+}
+
+bool write_dat(const std::string &path, const Block &b) {
+  FILE *F = fopen(path.c_str(), "wb");
+  if (!F) return false;
+  const uint32_t hdr[5] = {b.k, b.H, b.S, b.ok, b.n};
+  bool ok = fwrite(kMagic, 1, 8, F) == 8 && fwrite(hdr, 4, 5, F) == 5 &&
+            fwrite(b.len.data(), 4, b.n, F) == b.n &&
+            fwrite(b.minhash.data(), 4, b.minhash.size(), F) == b.minhash.size() &&
+            fwrite(b.ordered.data(), 8, b.ordered.size(), F) == b.ordered.size() &&
+            fwrite(b.ocount.data(), 4, b.n, F) == b.n;
+  return fclose(F) == 0 && ok;
+}
+
+bool read_dat(const std::string &path, Block &b, std::string &err) {
+  FILE *F = fopen(path.c_str(), "rb");
+  if (!F) { err = "cannot open '" + path + "': " + strerror(errno); return false; }
+  char magic[8];
+  uint32_t hdr[5];
+  bool ok = fread(magic, 1, 8, F) == 8 && memcmp(magic, kMagic, 8) == 0 &&
+            fread(hdr, 4, 5, F) == 5;
+  if (ok) {
+    b.k = hdr[0]; b.H = hdr[1]; b.S = hdr[2]; b.ok = hdr[3]; b.n = hdr[4];
+    b.len.resize(b.n);
+    b.minhash.resize((size_t)b.n * b.H);
+    b.ordered.resize((size_t)b.n * b.S);
+    b.ocount.resize(b.n);
+    ok = fread(b.len.data(), 4, b.n, F) == b.n &&
+         fread(b.minhash.data(), 4, b.minhash.size(), F) == b.minhash.size() &&
+         fread(b.ordered.data(), 8, b.ordered.size(), F) == b.ordered.size() &&
+         fread(b.ocount.data(), 4, b.n, F) == b.n;
+  }
+  fclose(F);
+  if (!ok) err = "'" + path + "' is not a sketch file of this mhap";
+  return ok;
+}
+
+bool is_dir(const char *p) {
+  struct stat st;
+  return stat(p, &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+std::string stem_dat(const std::string &fasta, const std::string &outdir) {
+  std::string base = fasta.substr(fasta.find_last_of('/') == std::string::npos
+                                      ? 0 : fasta.find_last_of('/') + 1);
+  for (const char *ext : {".fasta", ".fa", ".fna"}) {
+    const size_t e = strlen(ext);
+    if (base.size() > e && base.compare(base.size() - e, e, ext) == 0) {
+      base.resize(base.size() - e);
+      break;
+    }
+  }
+  return outdir + "/" + base + ".dat";
+}
+
+int fail_lib(const char *what) {
+  fprintf(stderr, "mhap: %s: %s\n", what, mhap_last_error());
+  return 1;
+}
+
+void print_records(mhap_ctx *ctx, uint64_t n) {
+  std::vector<mhap_record> r(n);
+  uint64_t got = 0;
+  if (n && mhap_fetch(ctx, r.data(), n, &got) != 0) return;
+  for (uint64_t i = 0; i < got; i++) {
+    const mhap_record &x = r[i];
+    printf("%u %u %.6f %u 0 %d %d %d %u %d %d %d\n", x.a_iid, x.b_iid, x.erate, x.count,
+           x.a_bgn, x.a_end, x.a_len, x.b_rc, x.b_bgn, x.b_end, x.b_len);
+  }
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  mhap_params P;
+  mhap_params_init(&P);
+  const char *fasta = nullptr, *qpath = nullptr, *spath = nullptr, *fpath = nullptr;
+  bool no_self = false;
+  double filter_threshold = 0.0;
+  std::vector<std::string> ignored;
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    const bool has = i + 1 < argc;
+    auto num = [&](const char *name) -> const char * {
+      if (!has) {
+        fprintf(stderr, "mhap: %s needs a value\n", name);
+        exit(usage(argv[0]));
+      }
+      return argv[++i];
+    };
+    if (a == "-k") P.k = (uint32_t)atoi(num("-k"));
+    else if (a == "--num-hashes") P.num_hashes = (uint32_t)atoi(num("--num-hashes"));
+    else if (a == "--num-min-matches") P.min_matches = (uint32_t)atoi(num("--num-min-matches"));
+    else if (a == "--threshold") P.threshold = atof(num("--threshold"));
+    else if (a == "--ordered-sketch-size") P.ordered_sketch = (uint32_t)atoi(num("--ordered-sketch-size"));
+    else if (a == "--ordered-kmer-size") P.ordered_k = (uint32_t)atoi(num("--ordered-kmer-size"));
+    else if (a == "--min-olap-length") P.min_olap = atoi(num("--min-olap-length"));
+    else if (a == "--num-threads") num("--num-threads");
+    else if (a == "--filter-threshold") {
+      filter_threshold = atof(num("--filter-threshold"));
+      ignored.push_back(a);
+    } else if (a == "--repeat-weight" || a == "--repeat-idf-scale") {
+      num(a.c_str());
+      ignored.push_back(a);
+    } else if (a == "--supress-noise" || a == "--no-tf") {
+      fprintf(stderr, "mhap: %s: tf-idf weighting options are not implemented\n", a.c_str());
+      return 1;
+    } else if (a == "--no-self") no_self = true;
+    else if (a == "-f") fpath = num("-f");
+    else if (a == "-p") fasta = num("-p");
+    else if (a == "-q") qpath = num("-q");
+    else if (a == "-s") spath = num("-s");
+    else if (a == "-h" || a == "--help") return usage(argv[0]);
+    else {
+      fprintf(stderr, "mhap: unknown option '%s'\n", a.c_str());
+      return usage(argv[0]);
+    }
+  }
+  if ((fasta != nullptr) == (spath != nullptr)) {
+    fprintf(stderr, "mhap: give either -p (precompute) or -s (compute)\n");
+    return usage(argv[0]);
+  }
+  if (fasta && !qpath) {
+    fprintf(stderr, "mhap: -p needs -q <output directory>\n");
+    return usage(argv[0]);
+  }
+  if (!ignored.empty()) {
+    fprintf(stderr, "mhap: WARNING:");
+    for (auto &s : ignored) fprintf(stderr, " %s", s.c_str());
+    fprintf(stderr, " accepted, but the sketch is unweighted (no tf-idf repeat weighting)\n");
+  }
+  const char *dev = getenv("CANU_MHAP_DEVICE");
+  mhap_ctx *ctx = nullptr;
+  if (mhap_ctx_create(&P, dev ? atoi(dev) : 0, &ctx) != 0) return fail_lib("context");
+
+  int rc = 0;
+  if (fasta) {
+    // ---- precompute: sketch one block of reads ----
+    std::vector<uint8_t> bases;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    if (!read_fasta(fasta, bases, off, len)) {
+      fprintf(stderr, "mhap: cannot read '%s': %s\n", fasta, strerror(errno));
+      mhap_ctx_destroy(ctx);
+      return 1;
+    }
+    Block b;
+    b.k = P.k; b.H = P.num_hashes; b.S = P.ordered_sketch; b.ok = P.ordered_k;
+    b.n = (uint32_t)len.size();
+    b.len = len;
+    b.minhash.resize((size_t)b.n * b.H);
+    b.ordered.resize((size_t)b.n * b.S);
+    b.ocount.resize(b.n);
+    if (b.n) {
+      if (mhap_load_reads(ctx, 1, b.n, bases.data(), off.data(), len.data()) != 0) {
+        rc = fail_lib("load");
+      } else if (fpath) {
+        std::string kmers;
+        uint64_t nk = 0;
+        if (!read_filter(fpath, P.k, filter_threshold, kmers, nk)) {
+          fprintf(stderr, "mhap: cannot read filter '%s'\n", fpath);
+          rc = 1;
+        } else if (mhap_set_filter_kmers(ctx, kmers.data(), nk) != 0) {
+          rc = fail_lib("filter");
+        }
+      }
+      if (!rc && mhap_sketch(ctx, 1, b.n) != 0) rc = fail_lib("sketch");
+      if (!rc && mhap_copy_sketches_host(ctx, 1, b.n, b.minhash.data(), b.ordered.data(),
+                                         b.ocount.data(), 0) != 0)
+        rc = fail_lib("sketch export");
+    }
+    const std::string out = stem_dat(fasta, qpath);
+    if (!rc && !write_dat(out, b)) {
+      fprintf(stderr, "mhap: cannot write '%s': %s\n", out.c_str(), strerror(errno));
+      rc = 1;
+    }
+    if (!rc) fprintf(stderr, "mhap: %u reads sketched into %s\n", b.n, out.c_str());
+  } else {
+    // ---- compute: hash block against itself and the query blocks ----
+    std::string err;
+    Block hb;
+    std::vector<Block> qb;
+    if (!read_dat(spath, hb, err)) { fprintf(stderr, "mhap: %s\n", err.c_str()); rc = 1; }
+    std::vector<std::string> qfiles;
+    if (!rc && qpath) {
+      if (is_dir(qpath)) {
+        DIR *D = opendir(qpath);
+        for (struct dirent *e; D && (e = readdir(D));) {
+          const std::string nm = e->d_name;
+          if (nm.size() > 4 && nm.compare(nm.size() - 4, 4, ".dat") == 0)
+            qfiles.push_back(std::string(qpath) + "/" + nm);
+        }
+        if (D) closedir(D);
+        std::sort(qfiles.begin(), qfiles.end());
+      } else {
+        qfiles.push_back(qpath);
+      }
+    }
+    for (const auto &f : qfiles) {
+      if (rc) break;
+      qb.emplace_back();
+      if (!read_dat(f, qb.back(), err)) { fprintf(stderr, "mhap: %s\n", err.c_str()); rc = 1; }
+    }
+    auto same = [&](const Block &x) {
+      return x.k == P.k && x.H == P.num_hashes && x.S == P.ordered_sketch && x.ok == P.ordered_k;
+    };
+    bool all_same = !rc && same(hb);
+    for (auto &q : qb) all_same = all_same && same(q);
+    if (!rc && !all_same) {
+      fprintf(stderr, "mhap: sketch files were made with other -k / --num-hashes / "
+                      "--ordered-sketch-size / --ordered-kmer-size\n");
+      rc = 1;
+    }
+    uint64_t nq = 0;
+    for (auto &q : qb) nq += q.n;
+    const uint64_t ntot = hb.n + nq;
+    if (!rc && ntot >= 0xFFFFFFF0ull) { fprintf(stderr, "mhap: too many reads\n"); rc = 1; }
+    if (!rc && hb.n) {
+      // one context holds the hash block (IDs 1..N) and the queries (N+1..), lengths only
+      std::vector<uint32_t> len(hb.len);
+      for (auto &q : qb) len.insert(len.end(), q.len.begin(), q.len.end());
+      if (mhap_load_reads_device(ctx, 1, (uint32_t)ntot, nullptr, nullptr, len.data()) != 0)
+        rc = fail_lib("lengths");
+      std::vector<const Block *> blocks{&hb};
+      for (auto &q : qb) blocks.push_back(&q);
+      uint32_t first = 1;
+      for (const Block *b : blocks) {
+        if (rc) break;
+        if (b->n && mhap_copy_sketches_host(ctx, first, b->n, (void *)b->minhash.data(),
+                                            (void *)b->ordered.data(), (void *)b->ocount.data(),
+                                            1) != 0)
+          rc = fail_lib("sketch import");
+        first += b->n;
+      }
+      if (!rc && mhap_build_index_range(ctx, 1, hb.n) != 0) rc = fail_lib("index");
+      uint64_t n = 0;
+      if (!rc && !no_self) {
+        if (mhap_compare(ctx, 1, hb.n, &n) != 0) rc = fail_lib("compare (self)");
+        else print_records(ctx, n);
+      }
+      if (!rc && nq) {
+        if (mhap_compare_all(ctx, hb.n + 1, (uint32_t)ntot, &n) != 0) rc = fail_lib("compare");
+        else print_records(ctx, n);
+      }
+    }
+    if (fflush(stdout) != 0) rc = 1;
+  }
+  mhap_ctx_destroy(ctx);
+  return rc;
+}

@@ -23,7 +23,8 @@ MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("count", "
 EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last_error",
            "mhap_abi_version", "mhap_load_reads", "mhap_load_reads_device",
            "mhap_set_filter_kmers", "mhap_sketch", "mhap_sketch_buffers", "mhap_copy_sketches",
-           "mhap_build_index",
+           "mhap_build_index", "mhap_build_index_range", "mhap_compare_all",
+           "mhap_copy_sketches_host",
            "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
 
 
@@ -70,6 +71,9 @@ def load_library(path: str | None = None):
     lib.mhap_sketch_buffers.argtypes = [V, P(V), P(V), P(V)]
     lib.mhap_copy_sketches.argtypes = [V, U32, U32, V, V, V, ctypes.c_int]
     lib.mhap_build_index.argtypes = [V]
+    lib.mhap_build_index_range.argtypes = [V, U32, U32]
+    lib.mhap_copy_sketches_host.argtypes = [V, U32, U32, V, V, V, ctypes.c_int]
+    lib.mhap_compare_all.argtypes = [V, U32, U32, P(U64)]
     lib.mhap_compare.argtypes = [V, U32, U32, P(U64)]
     lib.mhap_fetch.argtypes = [V, V, U64, P(U64)]
     lib.mhap_write_text.argtypes = [V, ctypes.c_char_p, U32, U32, U32]
@@ -239,14 +243,24 @@ class Mhap:
         self._check(self.lib.mhap_copy_sketches(self.ctx, first_iid, n, d_minhash, d_ordered,
                                                 d_ocount, 1 if to_ctx else 0))
 
-    def build_index(self) -> None:
-        self._check(self.lib.mhap_build_index(self.ctx))
+    def build_index(self, bgn: int | None = None, end: int | None = None) -> None:
+        """Index every loaded read, or reads bgn..end only (the jar's hash block)."""
+        if bgn is None and end is None:
+            self._check(self.lib.mhap_build_index(self.ctx))
+        else:
+            bgn = self.first_iid if bgn is None else bgn
+            end = self.first_iid + self.nreads - 1 if end is None else end
+            self._check(self.lib.mhap_build_index_range(self.ctx, bgn, end))
 
-    def compare(self, bgn: int | None = None, end: int | None = None) -> int:
+    def compare(self, bgn: int | None = None, end: int | None = None,
+                all_targets: bool = False) -> int:
+        """Queries bgn..end against the indexed reads with larger IDs, or (all_targets)
+        against every indexed read but themselves."""
         bgn = self.first_iid if bgn is None else bgn
         end = self.first_iid + self.nreads - 1 if end is None else end
         n = ctypes.c_uint64()
-        self._check(self.lib.mhap_compare(self.ctx, bgn, end, ctypes.byref(n)))
+        fn = self.lib.mhap_compare_all if all_targets else self.lib.mhap_compare
+        self._check(fn(self.ctx, bgn, end, ctypes.byref(n)))
         return n.value
 
     def fetch(self) -> np.ndarray:

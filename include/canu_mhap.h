@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHAP_ABI_VERSION 1
+#define MHAP_ABI_VERSION 2
 
 typedef struct {
   uint32_t k;               /* -k                      MinHash k-mer size, 1..32        */
@@ -114,12 +114,29 @@ int         mhap_sketch_buffers(mhap_ctx *ctx, void **d_minhash, void **d_ordere
 int         mhap_copy_sketches(mhap_ctx *ctx, uint32_t first_iid, uint32_t n, void *d_minhash,
                                void *d_ordered, void *d_ocount, int to_ctx);
 
+/* The same rows to / from host memory (the executable's .dat files).  A context loaded
+ * with mhap_load_reads_device(ctx, first, n, NULL, NULL, lengths) holds lengths only: it can
+ * import sketches and compare, not sketch. */
+int         mhap_copy_sketches_host(mhap_ctx *ctx, uint32_t first_iid, uint32_t n,
+                                    void *h_minhash, void *h_ordered, void *h_ocount,
+                                    int to_ctx);
+
 /* Build the MinHash index over all loaded reads' sketches. */
 int         mhap_build_index(mhap_ctx *ctx);
 
-/* Compare queries bgn_iid..end_iid against every loaded read with a larger ID (each pair
- * once); results stay on the device; *n_out = records found. */
+/* Build the MinHash index over the sketches of reads bgn_iid..end_iid only: the jar's
+ * hash block (-s block.dat) when the query blocks are loaded beside it. */
+int         mhap_build_index_range(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);
+
+/* Compare queries bgn_iid..end_iid against every indexed read with a larger ID (each pair
+ * once: the all-vs-all, and the jar's hash block against itself); results stay on the
+ * device; *n_out = records found. */
 int         mhap_compare(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid, uint64_t *n_out);
+
+/* Compare queries bgn_iid..end_iid against every indexed read but themselves: the jar's
+ * query blocks (-q) against its hash block, a_iid = the query, b_iid = the hash read. */
+int         mhap_compare_all(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid,
+                             uint64_t *n_out);
 
 /* Records of the last compare, sorted by (a_iid, b_iid). */
 int         mhap_fetch(mhap_ctx *ctx, mhap_record *out, uint64_t max_records,

@@ -156,17 +156,20 @@ def ordered_sketch(rs, i: int, p: dict):
     return h, pos.astype(np.int32), s
 
 
-def candidates(sk: np.ndarray, q_range, min_matches: int):
-    """Stage 2: [(q, t, count)] with t > q, 0-based read indices, sorted by (q, t)."""
+def candidates(sk: np.ndarray, q_range, min_matches: int, t_range=None):
+    """Stage 2: [(q, t, count)] with t > q, 0-based read indices, sorted by (q, t).  With
+    t_range ([lo, hi), 0-based: the jar's hash block) every t in it but q itself."""
     n = sk.shape[0]
     out = []
     for q in range(q_range[0], q_range[1]):
-        if q + 1 >= n:
+        lo, hi = (q + 1, n) if t_range is None else t_range
+        if lo >= hi:
             continue
-        eq = (sk[q + 1:] == sk[q][None, :]) & (sk[q][None, :] != INT32_MAX)
+        eq = (sk[lo:hi] == sk[q][None, :]) & (sk[q][None, :] != INT32_MAX)
         cnt = eq.sum(axis=1)
         for t in np.nonzero(cnt >= min_matches)[0]:
-            out.append((q, q + 1 + int(t), int(cnt[t])))
+            if lo + int(t) != q:
+                out.append((q, lo + int(t), int(cnt[t])))
     return out
 
 
@@ -207,9 +210,10 @@ def compare(A, B, la: int, lb: int, p: dict):
     return (min(D, 1.0), a_bgn, a_end, o, b_bgn, b_end)
 
 
-def run(rs, p: dict, q_range=None, skip_kmers=None) -> np.ndarray:
+def run(rs, p: dict, q_range=None, skip_kmers=None, t_range=None) -> np.ndarray:
     """All-vs-all over rs (queries in q_range, 0-based [lo, hi)): MHAP_DTYPE records with
-    1-based read IDs (rs.first_iid based), sorted by (a, b)."""
+    1-based read IDs (rs.first_iid based), sorted by (a, b).  t_range (0-based [lo, hi)):
+    the targets are the reads in it (every one but the query), not the later reads."""
     skip = None
     if skip_kmers:
         codes = []
@@ -220,7 +224,7 @@ def run(rs, p: dict, q_range=None, skip_kmers=None) -> np.ndarray:
         skip = np.unique(np.array(codes, dtype=U64))
     q_range = q_range or (0, rs.nreads)
     sk = sketch(rs, p, skip)
-    cands = candidates(sk, q_range, p["min_matches"])
+    cands = candidates(sk, q_range, p["min_matches"], t_range)
     cache = {}
 
     def osk(i):
