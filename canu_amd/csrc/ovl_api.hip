@@ -1496,14 +1496,26 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       EA.pair_next = x_ctr.p + 9;
       EA.defer = nullptr;
       EA.ndefer = nullptr;
-      n_ext_launch++;
-      if (gen.l16)
-        hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
-                           gen.lds, xs, EA);
-      else
-        hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
-                           gen.lds, xs, EA);
-      HIPC(hipGetLastError());
+      // without the pipeline the host waits for this chunk next anyway: read the last
+      // class's defer count and skip an empty generic launch
+      bool gen_needed = true;
+      if (!pipe && !ext_stage.empty()) {
+        uint32_t nd = 0;
+        HIPC(hipMemcpyAsync(&nd, x_ctr.p + ctr_defer[ext_stage.size() - 1], 4,
+                            hipMemcpyDeviceToHost, xs));
+        HIPC(hipStreamSynchronize(xs));
+        gen_needed = nd > 0;
+      }
+      if (gen_needed) {
+        n_ext_launch++;
+        if (gen.l16)
+          hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                             gen.lds, xs, EA);
+        else
+          hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                             gen.lds, xs, EA);
+        HIPC(hipGetLastError());
+      }
     }
     HIPC(hipEventRecord(c->xev[2 + slot], xs));
     pending[slot] = true;
