@@ -971,9 +971,23 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // A batch is sized by seed hits (node pool + list-ordered copy: 32 B per hit); the probe
   // window budget adapts to the hits-per-window ratio seen so far so that a batch's probe
   // results are all consumed (units beyond the hit budget would otherwise be re-probed).
-  // seed hits per batch (the node pool stays < 2^32); halved while the chain buffers do not
-  // fit the HBM the index leaves, as the probe-slot cap is for the probe records
-  uint64_t HIT_BUDGET = 1792ull << 20;
+  // seed hits per batch; halved while the chain buffers do not fit the HBM the index
+  // leaves, as the probe-slot cap is for the probe records
+  // 3.5 G: the 50k x 10 kb job in 2 chunks (1.27 s per step) rather than 4 (1.29 s) or 8
+  // (1.34 s) -- fewer re-probed windows and extension tails; node indices stay < 2^32
+  uint64_t HIT_BUDGET = 3584ull << 20;
+  {
+    // within the HBM left beside the index: the node pool and its list-ordered copy take
+    // ~33 B per hit; keep them under 60 % of what is free now plus what they already hold
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const uint64_t held = (c->fb.pool.n + c->fb.pnodes[0].n + c->fb.pnodes[1].n) * sizeof(Node);
+      HIT_BUDGET = std::min<uint64_t>(HIT_BUDGET, (uint64_t)((fr + held) * 0.6) / 33);
+    }
+  }
+  if (const char *e = getenv("OVL_HIT_BUDGET_M"))             // experiments: millions of hits
+    HIT_BUDGET = std::max<uint64_t>(16, strtoull(e, nullptr, 10)) << 20;
+  HIT_BUDGET = std::max<uint64_t>(HIT_BUDGET, 16ull << 20);
   uint64_t win_cap = 1536ull << 20;
   uint64_t WIN_BUDGET = 512ull << 20;           // probe slots per batch (8 B each)
   auto &d_rbase = c->fb.rbase;
@@ -1295,6 +1309,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         if (nc == 1 || hsum <= (16ull << 20))
           return fail(OVL_ERR_OOM, "chain buffers (%llu hits)", (unsigned long long)hsum);
         HIT_BUDGET = hsum / 2;                         // fewer units per chain launch
+        // the buffers that did fit were sized for the larger budget: drop them too
+        d_pool.release();
+        d_pnodes.release();
+        d_pairs.release();
         fit_hits();
         set_caps();
         attempt--;
