@@ -76,7 +76,10 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
   // PU windows per lane per step: their table slots are computed first and their first
   // 16-B entries loaded together, so each lane keeps PU random loads in flight (the
   // lookups are latency-bound); the rare longer probe sequences continue one by one.
-  constexpr int PU = 4;
+#ifndef OVL_PROBE_PU
+#define OVL_PROBE_PU 4
+#endif
+  constexpr int PU = OVL_PROBE_PU;
   const uint64_t smask = (1ull << A.X.slice_bits) - 1;
   for (uint32_t o0 = 0; o0 < nw; o0 += 64 * PU) {
     uint64_t M[PU], slot0[PU];
@@ -134,11 +137,17 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
       }
       out[o] = pr;
     };
-    static_assert(PU == 4, "finish() calls below");
+    static_assert(PU == 4 || PU == 8, "finish() calls below");
     finish(o0 + lane, ok[0], M[0], slot0[0], e[0]);
     finish(o0 + 64 + lane, ok[1], M[1], slot0[1], e[1]);
     finish(o0 + 128 + lane, ok[2], M[2], slot0[2], e[2]);
     finish(o0 + 192 + lane, ok[3], M[3], slot0[3], e[3]);
+    if constexpr (PU == 8) {
+      finish(o0 + 256 + lane, ok[4], M[4], slot0[4], e[4]);
+      finish(o0 + 320 + lane, ok[5], M[5], slot0[5], e[5]);
+      finish(o0 + 384 + lane, ok[6], M[6], slot0[6], e[6]);
+      finish(o0 + 448 + lane, ok[7], M[7], slot0[7], e[7]);
+    }
   }
   for (int s = 32; s > 0; s >>= 1) {
     hits += __shfl_xor(hits, s);
