@@ -87,6 +87,9 @@ def main():
         shutil.copy(stats[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     fetch, nf = counters(tag, "fetch")
     write, nw = counters(tag, "write")
+    if not fetch or not write:
+        sys.exit(f"no FETCH_SIZE / WRITE_SIZE passes for tag {tag} under {OUT}: "
+                 "profiles/traffic.json left as it is")
     avg_ns = {}
     if stats:
         for row in csv.DictReader(open(stats[0])):
