@@ -1260,6 +1260,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     float t = 0;
     (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
     ms_probe += t;
+    if (getenv("OVL_TIMING"))
+      fprintf(stderr, "OVL_TIMING probe launch: %u units, %llu windows, %.3f ms\n", nb,
+              (unsigned long long)acc, t);
     // algorithmic bytes: per window one 16-B table entry and one 8-B Probe record, plus the
     // packed query (2 bits per base); see DESIGN.md
     probe_bytes += acc * 24 + acc / 4;
