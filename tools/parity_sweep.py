@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Randomised GPU-vs-oracle parity sweep (beyond tests/test_gpu_parity.py's fixed cases).
 
-Each case draws a read set (count, length, error rate, seed) and an option mix (k,
+Each case draws a read set (count, length, error rate, seed, ragged lengths, 'n' bases)
+and an option mix (k,
 maxErate, minimum overlap, -G partial, -m multiple-per-pair) and compares the HIP path's
 ovOverlap records and counters with the oracle bit for bit.  Run on a GPU box:
 
@@ -45,7 +46,11 @@ def one_case(rng, i):
     if rng.random() < 0.25:
         P.Unique_Olap_Per_Pair = False
     P = P.finalize()
-    rs = synth_reads(n, L, glen, err, seed=int(rng.integers(1, 1 << 30)))
+    # ragged lengths (the extension's length classes) and 'n' bases (the generic kernel)
+    jitter = float(rng.choice([0.0, 0.0, 0.3]))
+    n_rate = float(rng.choice([0.0, 0.0, 0.001]))
+    rs = synth_reads(n, L, glen, err, seed=int(rng.integers(1, 1 << 30)), len_jitter=jitter,
+                     n_rate=n_rate)
     t0 = time.time()
     oic = OverlapInCore(P, device=0)
     oic.load_reads(rs)
