@@ -203,6 +203,8 @@ struct ovl_ctx {
     DBuf<uint32_t> xctr[2], xnout;
     DBuf<unsigned long long> chits;
     DBuf<uint8_t> otmp;
+    DBuf<uint64_t> ok64a, ok64b, dkey;       // -l orders
+    DBuf<uint32_t> oa, ob, ucnt, useg;
     DBuf<Node> pool, pnodes[2];
     DBuf<PairRec> pairs[2];
     DBuf<unsigned long long> stats;
@@ -273,8 +275,6 @@ int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
   if (p->kmer_len > 31) return fail(OVL_ERR_BAD_PARAM, "kmer length must be <= 31");
   if (!(p->max_erate > 0.0) || p->max_erate >= 1.0)
     return fail(OVL_ERR_BAD_PARAM, "maxErate out of range");
-  if (p->frag_olap_limit != UINT64_MAX)
-    return fail(OVL_ERR_UNSUPPORTED, "-l (frag olap limit) is not implemented on the GPU path");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(OVL_ERR_NO_DEVICE, "no HIP device");
@@ -400,6 +400,100 @@ __global__ void k_pair_order_keys(const PairRec *pairs, uint32_t n, uint32_t *ke
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     keys[i] = pairs[i].node_cnt;
     idx[i] = i;
+  }
+}
+
+// ---- -l (Frag_Olap_Limit): the reference's per-unit pair orders -----------------------
+// Process_String_Olaps (Process_String_Overlaps.C:687) walks a query's targets in
+// String_Olap_Space order -- Add_Ref (Find_Overlaps.C:158) gives a new target its hash
+// slot (StrNum ^ StrNum >> 8) & 255 when that slot is free, else the next overflow entry
+// (256, 257, .. in first-hit order) -- and, past the limit, sorted by average diagonal
+// (qsort By_Diag_Sum, glibc's stable merge sort: ties keep String_Olap_Space order).
+// A target's first hit is its smallest window (diag_bgn); targets first hit in the same
+// window come in the occurrence list's order, iid-descending.
+
+// per pair: first-hit keys, the unit's pair count, and the average diagonal (the
+// reference sums diagonals in a double: exact for integers, so the sum over nodes is the
+// same number; each node of length Len holds Len - k + 1 hits on its diagonal)
+__global__ void k_olim_keys(const PairRec *pairs, const Node *pnodes, uint32_t n, int32_t k,
+                            uint32_t *ktgt, uint64_t *kfirst, uint32_t *idx, uint64_t *dkey,
+                            uint32_t *ucnt) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const PairRec P = pairs[i];
+    ktgt[i] = ~P.tgt;
+    kfirst[i] = ((uint64_t)P.unit << 24) | (uint32_t)P.diag_bgn;
+    idx[i] = i;
+    int64_t sum = 0;
+    for (uint32_t j = 0; j < P.node_cnt; j++) {
+      const Node nd = pnodes[P.node_off + j];
+      sum += (int64_t)(nd.Len - k + 1) * (int64_t)(nd.Offset - nd.Start);
+    }
+    const double avg = (double)sum / (double)P.diag_ct;
+    const uint64_t b = __builtin_bit_cast(uint64_t, avg);
+    dkey[i] = (b >> 63) ? ~b : (b | (1ull << 63));     // order-preserving
+    atomicAdd(&ucnt[P.unit], 1u);
+  }
+}
+
+__global__ void k_gather_u64(const uint64_t *src, const uint32_t *idx, uint32_t n, uint64_t *dst) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    dst[i] = src[idx[i]];
+}
+
+__global__ void k_gather_unit(const PairRec *pairs, const uint32_t *idx, uint32_t n, uint32_t *dst) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    dst[i] = pairs[idx[i]].unit;
+}
+
+// One wave per unit over its pairs in first-hit order: String_Olap_Space index per pair,
+// written as the sort key unit << 32 | index (ks) next to the pair index (ki).
+__global__ void __launch_bounds__(256) k_olim_slots(const PairRec *pairs, const uint32_t *first,
+                                                    const uint32_t *useg, uint32_t nunits,
+                                                    uint32_t str_off, uint64_t *ks, uint32_t *ki) {
+  __shared__ uint32_t s_first[4][256];
+  __shared__ uint8_t s_taken[4][256];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t *fst = s_first[wave];
+  uint8_t *taken = s_taken[wave];
+  for (uint32_t i = lane; i < 256; i += 64) { fst[i] = 64; taken[i] = 0; }
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
+    const uint32_t b = useg[u], e = useg[u + 1];
+    uint32_t novf = 0;
+    for (uint32_t c0 = b; c0 < e; c0 += 64) {
+      const uint32_t i = c0 + lane;
+      const bool valid = i < e;
+      uint32_t pi = 0, h = 0;
+      if (valid) {
+        pi = first[i];
+        const uint32_t sn = pairs[pi].tgt + str_off;   // StrNum: index in the hash batch
+        h = (sn ^ (sn >> 8)) & 255u;
+        atomicMin(&fst[h], lane);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const bool own = valid && fst[h] == lane && !taken[h];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (valid) fst[h] = 64;
+      if (own) taken[h] = 1;
+      const uint64_t om = __ballot(valid && !own);
+      const uint32_t slot = own ? h : 256u + novf + (uint32_t)__builtin_popcountll(om & ((1ull << lane) - 1));
+      novf += (uint32_t)__builtin_popcountll(om);
+      if (valid) {
+        ks[i] = ((uint64_t)u << 32) | slot;
+        ki[i] = pi;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    for (uint32_t i = lane; i < 256; i += 64) taken[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -758,6 +852,8 @@ static void release_find_buffers(ovl_ctx *c) {
   f.uflags.release(); f.done.release(); f.dset.release(); f.big.release();
   f.defer.release(); f.defer2.release(); f.okey.release(); f.oidx.release();
   f.okey2.release(); f.oidx2.release(); f.otmp.release(); f.pool.release();
+  f.ok64a.release(); f.ok64b.release(); f.dkey.release(); f.oa.release(); f.ob.release();
+  f.ucnt.release(); f.useg.release();
   f.rows.release(); f.rowdir.release(); f.deltas.release();
 }
 
@@ -1002,7 +1098,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // chained (two buffer slots).  Measured slower (50k x 10 kb: 1.37-1.41 s vs 1.31 s per
   // job): the extension keeps every CU's issue slots busy, so the co-running probe and chain
   // only take them from it.  Default: one stream, one slot.
-  const bool pipe = getenv("OVL_PIPELINE") != nullptr;
+  // -l: every pair through the ordered generic kernel (a unit's pairs one after another)
+  const bool ordered = c->P.frag_olap_limit != UINT64_MAX;
+  const bool pipe = getenv("OVL_PIPELINE") != nullptr && !ordered;
   hipStream_t xs = pipe ? c->xstream : s;
   const bool window = c->P.use_window_filter && c->P.max_erate <= 0.06;
   if (window && !c->have_qual)
@@ -1127,6 +1225,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     gen.waves = std::max<uint32_t>(gen.wpb, (waves / gen.wpb) * gen.wpb);
     const void *kfn = gen.l16 ? reinterpret_cast<const void *>(k_extend<false, true>)
                               : reinterpret_cast<const void *>(k_extend<false, false>);
+    if (ordered)
+      kfn = gen.l16 ? reinterpret_cast<const void *>(k_extend<false, true, true>)
+                    : reinterpret_cast<const void *>(k_extend<false, false, true>);
     if (gen.lds > 64 * 1024)
       HIPC(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen.lds));
   }
@@ -1201,7 +1302,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
                   ecap_of(c->max_len), c->max_len);
     if (hx[7]) return fail(OVL_ERR_HIP, "extension capacity exceeded (flags %u)", hx[7]);
     uint32_t left = slot_pairs[sl];
-    for (size_t ci = 0; ci < ext_stage.size(); ci++) {
+    for (size_t ci = 0; ci < ext_stage.size() && !ordered; ci++) {
       const uint32_t nd = hx[ctr_defer[ci]];
       if (getenv("OVL_DEBUG"))
         fprintf(stderr, "OVL_DEBUG class %zu (reads <= %u): deferred %u of %u pairs\n", ci,
@@ -1457,9 +1558,71 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     EA.list = nullptr;
     EA.defer = nullptr;
     EA.ndefer = nullptr;
+    EA.olim = c->P.frag_olap_limit;
+    EA.nunits = nc;
+    EA.useg = nullptr;
+    EA.ord_slot = nullptr;
+    EA.ord_diag = nullptr;
+    EA.dkey = nullptr;
     slot_pairs[slot] = npairs;
     HIPC(hipMemsetAsync(x_ctr.p, 0, 64, xs));
-    if (npairs) {
+    if (npairs && ordered) {
+      // the reference's two pair orders per unit (see k_olim_keys): String_Olap_Space
+      // order and By_Diag_Sum order, by stable radix sorts
+      auto &fb = c->fb;
+      const int n = (int)npairs;
+      size_t t1 = 0, t2 = 0, t3 = 0;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, fb.okey.p, fb.okey2.p, fb.oa.p,
+                                              fb.ob.p, n, 0, 32, xs));
+      HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, fb.ok64a.p, fb.ok64b.p, fb.oa.p,
+                                              fb.ob.p, n, 0, 64, xs));
+      HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, fb.ucnt.p, fb.useg.p, (int)nc + 1, xs));
+      const size_t tmp = std::max(std::max(t1, t2), t3);
+      HIPC(hipStreamSynchronize(xs));
+      if (fb.okey.grow(npairs) || fb.okey2.grow(npairs) || fb.oa.grow(npairs) ||
+          fb.ob.grow(npairs) || fb.oidx.grow(npairs) || fb.oidx2.grow(npairs) ||
+          fb.ok64a.grow(npairs) || fb.ok64b.grow(npairs) || fb.dkey.grow(npairs) ||
+          fb.ucnt.grow((size_t)nc + 1) || fb.useg.grow((size_t)nc + 1) ||
+          fb.otmp.grow(std::max<size_t>(tmp, 1)))
+        return fail(OVL_ERR_OOM, "-l pair orders");
+      const dim3 grid(std::min<uint32_t>((npairs + 255) / 256, 4096)), blk(256);
+      HIPC(hipMemsetAsync(fb.ucnt.p, 0, 4ull * (nc + 1), xs));
+      // first-hit order: by ~tgt, then (stably) by (unit, diag_bgn)
+      hipLaunchKernelGGL(k_olim_keys, grid, blk, 0, xs, d_pairs.p, d_pnodes.p, npairs, (int32_t)k,
+                         fb.okey.p, fb.ok64a.p, fb.oa.p, fb.dkey.p, fb.ucnt.p);
+      HIPC(hipGetLastError());
+      HIPC(hipcub::DeviceScan::ExclusiveSum(fb.otmp.p, t3, fb.ucnt.p, fb.useg.p, (int)nc + 1, xs));
+      size_t tt = t1;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.okey.p, fb.okey2.p, fb.oa.p,
+                                              fb.ob.p, n, 0, 32, xs));
+      hipLaunchKernelGGL(k_gather_u64, grid, blk, 0, xs, fb.ok64a.p, fb.ob.p, npairs, fb.ok64b.p);
+      tt = t2;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64b.p, fb.ok64a.p, fb.ob.p,
+                                              fb.oa.p, n, 0, 64, xs));
+      // String_Olap_Space indices, then the order by (unit, index)
+      hipLaunchKernelGGL(k_olim_slots, dim3(std::min<uint32_t>((nc + 3) / 4, 8192)), blk, 0, xs,
+                         d_pairs.p, fb.oa.p, fb.useg.p, nc,
+                         c->first_iid - c->hash_bgn_iid, fb.ok64b.p, fb.ob.p);
+      HIPC(hipGetLastError());
+      tt = t2;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64b.p, fb.ok64a.p, fb.ob.p,
+                                              fb.oidx.p, n, 0, 64, xs));       // oidx: ord_slot
+      // By_Diag_Sum: stably by the diagonal key, then stably by unit
+      hipLaunchKernelGGL(k_gather_u64, grid, blk, 0, xs, fb.dkey.p, fb.oidx.p, npairs, fb.ok64a.p);
+      tt = t2;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64a.p, fb.ok64b.p, fb.oidx.p,
+                                              fb.oa.p, n, 0, 64, xs));
+      hipLaunchKernelGGL(k_gather_unit, grid, blk, 0, xs, d_pairs.p, fb.oa.p, npairs, fb.okey.p);
+      tt = t1;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.okey.p, fb.okey2.p, fb.oa.p,
+                                              fb.oidx2.p, n, 0, 32, xs));      // oidx2: ord_diag
+      HIPC(hipGetLastError());
+      EA.useg = fb.useg.p;
+      EA.ord_slot = fb.oidx.p;
+      EA.ord_diag = fb.oidx2.p;
+      EA.dkey = fb.dkey.p;
+    }
+    if (npairs && !ordered) {
       // the extension-only buffers are shared by the slots: regrowing one waits for xs
       auto &fb = c->fb;
       size_t tmp = 0;
@@ -1486,7 +1649,21 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       }
     }
     HIPC(hipEventRecord(c->xev[slot], xs));
-    if (npairs) {
+    if (npairs && ordered) {
+      EA.e_cap = gen.ecap;
+      EA.rows_cap = gen.stride;
+      EA.sw_words = 0;
+      EA.stage_len = 0;
+      EA.pair_next = x_ctr.p + 9;
+      n_ext_launch++;
+      if (gen.l16)
+        hipLaunchKernelGGL((k_extend<false, true, true>), dim3(gen.waves / gen.wpb),
+                           dim3(64 * gen.wpb), gen.lds, xs, EA);
+      else
+        hipLaunchKernelGGL((k_extend<false, false, true>), dim3(gen.waves / gen.wpb),
+                           dim3(64 * gen.wpb), gen.lds, xs, EA);
+      HIPC(hipGetLastError());
+    } else if (npairs) {
       // the staged classes in turn, each deferring what it cannot take to the next list
       // (whose length the next launch reads from the device counter); the generic kernel
       // takes the last list, or every pair when no class exists

@@ -57,6 +57,15 @@ struct ExtendArgs {
   int32_t window;               // -w: Use_Window_Filter
   uint32_t *overflow;
   unsigned long long *dbg;      // optional counters (null: off)
+  // -l (Frag_Olap_Limit), the ordered kernel: one wave per unit runs its pairs one after
+  // another in the reference's order, counting the unit's A / B overlaps
+  // (Process_String_Overlaps.C:721-790)
+  uint64_t olim;
+  uint32_t nunits;
+  const uint32_t *useg;         // unit u's pairs: [useg[u], useg[u+1]) of ord_slot / ord_diag
+  const uint32_t *ord_slot;     // String_Olap_Space order (Add_Ref's hash slots)
+  const uint32_t *ord_diag;     // By_Diag_Sum order, ties in String_Olap_Space order (stable)
+  const uint64_t *dkey;         // per pair: its average diagonal as an order-preserving key
 };
 
 // debug counters (dbg != null): 0 ped calls 1 rows 2 chunks 3 slide words 4 tb steps
@@ -1350,10 +1359,11 @@ __device__ bool lies_on_alignment(int32_t start, int32_t offset, int32_t s_lo, i
 // Returns false when the pair must be redone by the generic kernel (register window
 // overflow); nothing has been output for it then, and removed nodes are marked ~Len so the
 // generic kernel can restore them.
-template <bool FAST, bool L16, typename SS>
+template <bool FAST, bool L16, bool ORD, typename SS>
 __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &un,
                              const SS &S, const SS &T, const WaveMem &WM, int32_t *stk,
-                             int32_t *RD, int32_t *LD, unsigned long long *st, uint32_t lane) {
+                             int32_t *RD, int32_t *LD, unsigned long long *st, uint32_t lane,
+                             int32_t *ab) {
   uint32_t S_ID = X.R.first_iid + un.r, T_ID = X.R.first_iid + P.tgt;
   int32_t S_Len = S.len, t_len = T.len;
   Node *nodes = X.pnodes + P.node_off;
@@ -1409,26 +1419,36 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     wave_argmax(bv, bi);
     Node M = nodes[bi];
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
-    PROF_T(px0);
-    ExtOut eo = extend_alignment<FAST, L16>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+    // -l: no extension once the unit has its limit of overlaps off that end (:481-487); the
+    // match is still dropped with the previous extension's alignment (kind, S_Lo.., deltas)
+    bool hit_limit = false;
+    if constexpr (ORD) {
+      const int32_t a_hang = M.Start - M.Offset, b_hang = a_hang + S_Len - t_len;
+      hit_limit = ((uint64_t)ab[0] >= X.olim && a_hang <= 0) ||
+                  ((uint64_t)ab[1] >= X.olim && b_hang <= 0);
+    }
+    if (!hit_limit) {
+      PROF_T(px0);
+      ExtOut eo = extend_alignment<FAST, L16>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
 #ifdef OVL_PROFILE
-    PROF_T(px1);
-    if (X.dbg && lane == 0) atomicAdd(&X.dbg[15], px1 - px0);
+      PROF_T(px1);
+      if (X.dbg && lane == 0) atomicAdd(&X.dbg[15], px1 - px0);
 #endif
-    if (FAST && eo.kind < 0) return false;
-    kind = eo.kind;
-    S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
-    ld_len = eo.ld_len;
-    if (kind == K_DOVETAIL || X.partial) {
-      if (1 + S_Hi - S_Lo >= X.min_olap_len && 1 + T_Hi - T_Lo >= X.min_olap_len) {
-        int32_t olap_len = 1 + ((S_Hi - S_Lo) < (T_Hi - T_Lo) ? (S_Hi - S_Lo) : (T_Hi - T_Lo));
-        double quality = (double)eo.Errors / olap_len;
-        if (eo.Errors <= X.error_bound[olap_len]) {
-          const int32_t slot = add_overlap(X, S_Lo, S_Hi, T_Lo, T_Hi, quality, ld_len, ol, ct);
-          if (X.window && slot >= 0) {               // memcpy(olap[i].delta, Left_Delta)
-            int32_t *od = LD + (2 + slot) * (X.e_cap + 8);
-            for (int32_t i = lane; i < ld_len; i += 64) od[i] = LD[i];
-            vm_sync();
+      if (FAST && eo.kind < 0) return false;
+      kind = eo.kind;
+      S_Lo = eo.S_Lo; S_Hi = eo.S_Hi; T_Lo = eo.T_Lo; T_Hi = eo.T_Hi;
+      ld_len = eo.ld_len;
+      if (kind == K_DOVETAIL || X.partial) {
+        if (1 + S_Hi - S_Lo >= X.min_olap_len && 1 + T_Hi - T_Lo >= X.min_olap_len) {
+          int32_t olap_len = 1 + ((S_Hi - S_Lo) < (T_Hi - T_Lo) ? (S_Hi - S_Lo) : (T_Hi - T_Lo));
+          double quality = (double)eo.Errors / olap_len;
+          if (eo.Errors <= X.error_bound[olap_len]) {
+            const int32_t slot = add_overlap(X, S_Lo, S_Hi, T_Lo, T_Hi, quality, ld_len, ol, ct);
+            if (X.window && slot >= 0) {               // memcpy(olap[i].delta, Left_Delta)
+              int32_t *od = LD + (2 + slot) * (X.e_cap + 8);
+              for (int32_t i = lane; i < ld_len; i += 64) od[i] = LD[i];
+              vm_sync();
+            }
           }
         }
       }
@@ -1566,6 +1586,10 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
       }
       outputs++;
       st[4]++;
+      if constexpr (ORD) {                             // A / B_Olaps_For_Frag (:631-635)
+        if (ol[i].s_lo == 0) ab[0]++;
+        if (ol[i].s_hi >= S_Len - 1) ab[1]++;
+      }
       if (!X.partial) {
         if (bhg <= 0) st[5]++;
         else          st[6]++;
@@ -1603,7 +1627,8 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
 // L16, staged kernel: every read < 16384 bases, so the traceback log holds 16-bit cells.
 // L16, generic kernel: GR -- the rows and the Edit_Match_Limit table stay in global memory
 // (error limits past what a CU's LDS holds; see wave_ped).
-template <bool STAGE, bool L16>
+// ORD (with STAGE = false): the -l kernel, one unit per wave (see ExtendArgs.olim).
+template <bool STAGE, bool L16, bool ORD = false>
 __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1651,6 +1676,33 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
   unsigned long long st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t npairs = X.npairs_dev ? __builtin_amdgcn_readfirstlane(*X.npairs_dev) : X.npairs;
 
+  if constexpr (ORD) {
+    static_assert(!STAGE, "the -l kernel is the generic one");
+    for (;;) {
+      uint32_t ui = 0;
+      if (lane == 0) ui = atomicAdd(X.pair_next, 1u);
+      ui = __shfl(ui, 0);
+      if (ui >= X.nunits) break;
+      const uint32_t b = X.useg[ui], e = X.useg[ui + 1];
+      int32_t ab[2] = {0, 0};                // A_ / B_Olaps_For_Frag (Find_Overlaps.C:306)
+      auto run = [&](uint32_t pi) {
+        PairRec P = X.pairs[pi];
+        Unit un = X.units[P.unit];
+        Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
+        Strand T = strand_fwd(X.R, P.tgt);
+        process_pair<false, L16, true>(X, P, un, S, T, WM, stk, RD, LD, st, lane, ab);
+        lds_sync();
+      };
+      if ((uint64_t)(e - b) <= X.olim) {     // Process_String_Olaps.C:721
+        for (uint32_t i = b; i < e; i++) run(X.ord_slot[i]);
+      } else {                               // :746-790: by average diagonal, >= 0 first
+        uint32_t start = b;
+        while (start < e && X.dkey[X.ord_diag[start]] < (1ull << 63)) start++;
+        for (uint32_t i = start; i < e && (uint64_t)ab[0] < X.olim; i++) run(X.ord_diag[i]);
+        for (uint32_t i = start; i > b && (uint64_t)ab[1] < X.olim; i--) run(X.ord_diag[i - 1]);
+      }
+    }
+  } else
   for (;;) {
     uint32_t pi = 0;
     if (lane == 0) pi = atomicAdd(X.pair_next, 1u);
@@ -1676,7 +1728,7 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
         StrandLP TL = stage_strand(T, tw, lane);
         lds_sync();
         PROF_T(pp0);
-        ok = process_pair<true, L16>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane);
+        ok = process_pair<true, L16, false>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
 #ifdef OVL_PROFILE
         PROF_T(pp1);
         if (X.dbg && lane == 0) atomicAdd(&X.dbg[13], pp1 - pp0);
@@ -1684,7 +1736,7 @@ __global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
       }
       if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
     } else {
-      process_pair<false, L16>(X, P, un, S, T, WM, stk, RD, LD, st, lane);
+      process_pair<false, L16, false>(X, P, un, S, T, WM, stk, RD, LD, st, lane, nullptr);
     }
     lds_sync();
   }

@@ -95,7 +95,7 @@ def _frequent_mers(rs, k=22, n=40):
 
 @needs_ref
 @pytest.mark.gpu
-@pytest.mark.parametrize("job", ["utg", "partial_threads"])
+@pytest.mark.parametrize("job", ["utg", "partial_threads", "partial_limit"])
 def test_gpu_cli_canu_job(cli, job):
     """overlap.sh's command line on a reference-written gkpStore: the .ovb read back by the
     reference's ovFile reader equals the reference overlapInCore's records, the .counts
@@ -106,8 +106,9 @@ def test_gpu_cli_canu_job(cli, job):
     hashlen = int(sum(int(rs.lengths[i - 1]) + 1 for i in range(hb, he + 1)))
     hashlen //= 3                                       # three hash batches per job
     threads = 4 if job == "utg" else 16
+    lim = ["-l", "4"] if job == "partial_limit" else []      # -l: Frag_Olap_Limit
     P = oracle.default_params(kmer_len=22, max_erate=0.06, min_olap_len=500,
-                              partial=int(job != "utg"))
+                              partial=int(job != "utg"), **({"frag_olap_limit": 4} if lim else {}))
     with tempfile.TemporaryDirectory() as wd:
         fm = os.path.join(wd, "asm.ms22.frequentMers.fasta")
         mers = _frequent_mers(rs)
@@ -128,7 +129,7 @@ def test_gpu_cli_canu_job(cli, job):
         argv = [cli] + (["-G"] if job != "utg" else []) + [
             "-t", str(threads), "-k", "22", "-k", fm, "--hashbits", "23", "--hashload", "0.75",
             "--maxerate", "0.06", "--minlength", "500", "--minkmers",
-            *opt, "--hashstrings", str(he - hb + 1), "--hashdatalen", str(hashlen),
+            *opt, *lim, "--hashstrings", str(he - hb + 1), "--hashdatalen", str(hashlen),
             "-o", os.path.join(jobdir, "000001.ovb.WORKING"),
             "-s", os.path.join(jobdir, "000001.stats"), store]
         cp = subprocess.run(argv, capture_output=True, text=True, timeout=300)
