@@ -792,7 +792,9 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
       const int32_t k = run < lim ? run : lim;
       NR[j] = q + 1 + k;                       // lim >= 0 inside the band
       RM[j] = lmin - k;                        // inside: lim - k >= 0; outside: > 0
-      need[j] = __builtin_amdgcn_ballot_w64(run == 31) & __builtin_amdgcn_ballot_w64(lim > 31);
+      // run == 31 && lim > 31  <=>  min(run, lim - 1) == 31 (run <= 31): one ballot, no
+      // scalar AND of two
+      need[j] = __builtin_amdgcn_ballot_w64((run < lim - 1 ? run : lim - 1) == 31);
       any |= need[j];
     }
 #ifdef OVL_PROFILE
@@ -824,25 +826,37 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
     PROF_ADD(pc_cont, pt_b, pt_cont);
     // ---- C: end test and Edit_Match_Limit pruning, one pass ---------------------------
     // (scalar work per chunk kept minimal: the end masks are only OR-ed -- the end row is
-    // rare and re-scanned below -- and the kept range is a min/max of window offsets:
-    // s_ff1 / s_flbit give -1 on an empty mask, so an empty chunk contributes ~0u to the
-    // min, and an empty chunk's 0 to the max is harmless because the max only matters
-    // when some chunk has a kept lane, at an offset >= 0)
+    // rare and re-scanned below -- and the kept range is two unsigned mins, of window
+    // offsets and of reversed offsets: s_ff1 / s_flbit give -1 on an empty mask, so an
+    // empty chunk contributes ~0u to both)
     uint64_t endany = 0;
-    uint32_t nlo = 0xffffffffu;
-    int32_t nro = -1;
+    uint32_t nlo = 0xffffffffu;                // min window offset of a kept lane
+    uint32_t nhi = 0xffffffffu;                // min reversed offset (64J-1 - o) of one
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
       endany |= __builtin_amdgcn_ballot_w64(RM[j] == 0);
       const uint64_t km = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
-      const uint32_t f = (uint32_t)__builtin_ctzg(km, -1);
-      const uint32_t c = f | (uint32_t)(64 * j);
-      nlo = c < nlo ? c : nlo;
-      const int32_t l = __builtin_clzg(km, -1);
-      nro = km ? 64 * j + 63 - l : nro;
+      // s_ff1 / s_flbit give ~0u on an empty mask, which the unsigned mins ignore: no
+      // compare-and-select per chunk (the compiler does not know that of ctz / clz and
+      // adds one; 3 scalar instructions of 12 per chunk, -1.6 % extension time)
+      uint32_t f1, fb;
+      asm("s_ff1_i32_b64 %0, %1" : "=s"(f1) : "s"(km));
+      asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(km));
+      const uint32_t c1 = f1 | (uint32_t)(64 * j);
+      nlo = c1 < nlo ? c1 : nlo;
+      const uint32_t g = fb | (uint32_t)(64 * (J - 1 - j));
+      nhi = g < nhi ? g : nhi;
     }
+    const int32_t nro = 64 * J - 1 - (int32_t)nhi;
+
+    PROF_T(pt_chunks);
+    PROF_ADD(pc_chunks, pt_row, pt_chunks);
+    PROF_ADD(pc_c, pt_cont, pt_chunks);
+#ifdef OVL_PROFILE
+    pc_rows++;
+#endif
     if (endany) {                              // the first d in order that reached the end
 #pragma unroll
       for (int j = 0; j < J; j++) {
@@ -855,21 +869,15 @@ __device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, co
           // row e-1 at d+1 (R still holds row e-1)
           end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
                  : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
-          ended = true;
           break;
         }
       }
+      ended = true;
+      break;                                   // end reached
     }
-    const int32_t nl = (nlo == 0xffffffffu) ? NONE : B + (int32_t)nlo;
+    if (nlo == 0xffffffffu) break;             // Left > Right
+    const int32_t nl = B + (int32_t)nlo;
     const int32_t nr = B + nro;
-
-    PROF_T(pt_chunks);
-    PROF_ADD(pc_chunks, pt_row, pt_chunks);
-    PROF_ADD(pc_c, pt_cont, pt_chunks);
-#ifdef OVL_PROFILE
-    pc_rows++;
-#endif
-    if (ended || nl == NONE) break;            // end reached, or Left > Right
 
     // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
     // traceback (cells up to nr+2 are read), longest row with the first d on ties: one
