@@ -544,15 +544,18 @@ typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 
 // Set_Right_Delta / Set_Left_Delta (forward.C:48, reverse.C:52) over the row log of
 // wave_ped_reg: row k's stripe holds L[k][d] (-2 outside the pruned band).  For 16 rows at a
-// time the previous rows are loaded into registers (lane = diagonal offset -17..17 from the
-// walk's position) and the walk is scalar, three readlanes per row.
+// time the previous rows are loaded into registers (lane = diagonal offset -31..31 from the
+// window's first position), every lane's step is decided in parallel, and the walk is
+// scalar, one readlane per row.
 template <bool L16>
 __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t tb_e,
                                                     int32_t tb_d, int32_t last, int32_t *dst,
                                                     uint32_t lane, int32_t &last_out,
                                                     int32_t &nd_out) {
   constexpr int W = 64 * OVL_RJ;               // cells per logged row, cell = d mod W
-  constexpr int TBR = 30;                      // rows per window: lanes cover dc-31..dc+31
+  // rows per window (lanes cover dc-31..dc+31): 16 keeps the unrolled walk and its code
+  // registers within wave_ped_reg's 80 VGPRs (24 spills; 16 vs 24: -1 % extension time)
+  constexpr int TBR = 16;
   g_ci32 *rows = (g_ci32 *)WM.rows;
   typedef __attribute__((address_space(1))) const int16_t g_ci16;
   g_ci16 *rows16 = (g_ci16 *)WM.rows;
@@ -573,29 +576,40 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
       if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
       else               V[i] = rows[(size_t)kk * W + cell];
     }
+    // Every lane's winner first, lane-parallel (VALU, DPP neighbours): C[i] at lane x is
+    // (the value the walk would take as `last`) << 2 | (from + 1), with the reference's
+    // order -- d-1 only if strictly better than d, d+1 only if strictly better than both.
+    // The walk is then one readlane and a few scalar operations per row; the window's
+    // deltas collect in one VGPR (lane j = its j-th delta) stored once per window.
+    const int32_t nsteps = kh < TBR ? kh : TBR;
 #pragma unroll
     for (int i = 0; i < TBR; i++) {
-      if (kh - i < 1) break;
-      const int32_t x = 31 + d - dc;
-      const int32_t pm = __builtin_amdgcn_readlane(V[i], x - 1);
-      const int32_t p0 = __builtin_amdgcn_readlane(V[i], x);
-      const int32_t pp = __builtin_amdgcn_readlane(V[i], x + 1);
-      int32_t mx = 1 + p0;
-      int32_t from = 0;
-      if (pm > mx) { from = -1; mx = pm; }
-      if (1 + pp > mx) { from = 1; mx = 1 + pp; }
-      if (from < 0) {
-        if (lane == 0) gdst[nd] = mx - last - 1;
-        nd++;
-        last = pm;
-        d--;
-      } else if (from > 0) {
-        if (lane == 0) gdst[nd] = last - (mx - 1);
-        nd++;
-        last = pp;
-        d++;
+      const int32_t v = V[i];
+      const int32_t vm = dpp_from_lower(v, -2), vp = dpp_from_upper(v, -2);
+      const int32_t a = v + 1, c = vp + 1;
+      const int32_t m = vm > a ? vm : a;
+      const int32_t f = c > m ? 2 : (vm > a ? 0 : 1);
+      V[i] = ((f == 0 ? vm : vp) << 2) | f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int32_t buf = 0, nb = 0;
+    int32_t x = 31;                            // lane of diagonal d: 31 + d - dc
+#pragma unroll
+    for (int i = 0; i < TBR; i++) {
+      if (i < nsteps) {
+        const int32_t w = __builtin_amdgcn_readlane(V[i], x);
+        const int32_t f3 = w & 3, nl = w >> 2;   // f3: 0 d-1, 1 d, 2 d+1
+        const int32_t val = f3 == 0 ? nl - last - 1 : last - nl;
+        buf = (int32_t)lane == nb ? val : buf;
+        const int32_t mv = f3 != 1;
+        nb += mv;
+        last = mv ? nl : last;
+        x += f3 - 1;
       }
     }
+    d = dc + x - 31;
+    if ((int32_t)lane < nb) gdst[nd + (int32_t)lane] = buf;
+    nd += nb;
   }
   last_out = last;
   nd_out = nd;
