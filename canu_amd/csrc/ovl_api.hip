@@ -685,7 +685,18 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   A.R = c->reads();
   A.h0 = h0;
   A.h1 = h1;
-  uint32_t nblk = std::max<uint32_t>(1, std::min<uint32_t>(h1 - h0, 4u * c->n_cu));
+  // coarse passes: 2 blocks of 16 waves per CU (32 waves: the coarse scatter is latency-
+  // bound -- a dependent packed-base load, LDS atomic and 16-B store per window -- and its
+  // 32 KB of LDS histograms per block would cap 4-wave blocks at 20 waves per CU).
+  // Measured on 50k x 10 kb: 256 threads x 4 per CU 35.7 ms index, 512 x 4 34.0, 1024 x 2
+  // 32.4 (with the parallel fine-bucket scan)
+#ifndef OVL_COARSE_BPCU
+#define OVL_COARSE_BPCU 2
+#endif
+#ifndef OVL_COARSE_THREADS
+#define OVL_COARSE_THREADS 1024
+#endif
+  uint32_t nblk = std::max<uint32_t>(1, std::min<uint32_t>(h1 - h0, OVL_COARSE_BPCU * c->n_cu));
   A.reads_per_block = (h1 - h0 + nblk - 1) / nblk;
   if (A.reads_per_block == 0) A.reads_per_block = 1;
   A.k = k;
@@ -695,10 +706,10 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   A.n_skip = n_skip;
   A.cb_bits = cb;
   A.fb_bits = fb;
-  hipLaunchKernelGGL(k_coarse_hist, dim3(nblk), dim3(256), 0, s, A, hist.p);
+  hipLaunchKernelGGL(k_coarse_hist, dim3(nblk), dim3(OVL_COARSE_THREADS), 0, s, A, hist.p);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, hist.p, cstart.p, ncb, misc.p + 0);
   HIPC(hipMemcpyAsync(cursor.p, cstart.p, 4 * ncb, hipMemcpyDeviceToDevice, s));
-  hipLaunchKernelGGL(k_coarse_scatter, dim3(nblk), dim3(256), 0, s, A, cursor.p, c->d_tmpR.p);
+  hipLaunchKernelGGL(k_coarse_scatter, dim3(nblk), dim3(OVL_COARSE_THREADS), 0, s, A, cursor.p, c->d_tmpR.p);
   FineArgs F;
   F.inR = c->d_tmpR.p;
   F.midR = c->d_midR.p;
@@ -749,7 +760,14 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
     HIPC(hipStreamSynchronize(s));
   }
   uint32_t maxd = std::max<uint32_t>(hm[2], 1);
-  c->slice_bits = std::max<uint32_t>(1, ceil_log2(2ull * maxd));
+#ifndef OVL_SLICE_Q
+#define OVL_SLICE_Q 8
+#endif
+  // slots per slice >= OVL_SLICE_Q / 4 x the largest fine bucket's distinct k-mers (and
+  // always more than it, so every probe sequence meets an empty slot).  2x: a denser table
+  // (1.25x / 1.5x: 16 -> 8 GB at 50k x 10 kb) builds 1.5 ms faster but lengthens the probe
+  // sequences, +2.7 ms in k_probe
+  c->slice_bits = std::max<uint32_t>(1, ceil_log2((uint64_t)OVL_SLICE_Q * maxd / 4 + 1));
   c->tab_bits = cb + fb + c->slice_bits;
   if (c->d_tab.alloc(1ull << c->tab_bits)) return fail(OVL_ERR_OOM, "table 2^%u", c->tab_bits);
   TableArgs T;

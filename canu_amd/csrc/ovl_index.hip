@@ -205,6 +205,9 @@ __device__ void wave_bitonic(uint64_t *sM, uint64_t *sP, uint32_t n2, uint32_t l
 
 #define OVL_FINE_WAVES  8
 #define OVL_FB_MAX      4096
+#ifndef OVL_FINE_PSCAN
+#define OVL_FINE_PSCAN  1
+#endif
 
 struct FineArgs {
   const Rec2 *inR;               // coarse-bucketed records
@@ -237,10 +240,35 @@ k_fine(FineArgs A) {
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     atomicAdd(&h[(uint32_t)(A.inR[s0 + i].m >> shift) & (nf - 1)], 1u);
   __syncthreads();
+#if OVL_FINE_PSCAN
+  {
+    // exclusive scan of the nf <= 4096 bins: each thread a run of nf/512 bins, a wave scan
+    // of the runs, then the 8 wave totals (a one-thread serial scan of 4096 bins is a chain
+    // of dependent LDS round trips, ~0.1 ms per block)
+    __shared__ uint32_t s_wsum[OVL_FINE_WAVES];
+    const uint32_t per = (nf + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t run = 0;
+    for (uint32_t f = b0; f < b0 + per && f < nf; f++) run += h[f];
+    uint32_t inc = run;
+    const uint32_t ln = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o);
+      if (ln >= (uint32_t)o) inc += v;
+    }
+    if (ln == 63) s_wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t acc = inc - run;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) acc += s_wsum[w];
+    for (uint32_t f = b0; f < b0 + per && f < nf; f++) { cur[f] = acc; acc += h[f]; }
+  }
+#else
   if (threadIdx.x == 0) {                        // nf <= 4096: serial scan is cheap
     uint32_t acc = 0;
     for (uint32_t f = 0; f < nf; f++) { cur[f] = acc; acc += h[f]; }
   }
+#endif
   __syncthreads();
   for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) {
     A.fstart[cb * nf + f] = s0 + cur[f];
