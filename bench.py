@@ -143,12 +143,14 @@ def main() -> None:
     traffic = load_traffic()
     # Dominant kernel: k_extend (the banded edit-distance extension).  Its algorithmic HBM
     # bytes per pair are the two packed strands it stages (2 bits/base + guard word each),
-    # the pair's seed-match nodes (16 B each) and its output records (24 B each); per launch
+    # the pair's seed-match nodes (16 B each, read once: the Add_Match lists, not the seed
+    # hits they merge -- rounds before r02v counted 16 B per hit, ~7x the bytes) and its
+    # output records (24 B each); per launch
     # = the step's bytes / the step's launches, over the launches' average duration (HIP
     # events on the library's stream).
     avg_len = total_bases / max(n, 1)
     strand = 8.0 * (np.ceil(avg_len / 32.0) + 1.0)
-    ext_bytes = st["pairs"] * 2 * strand + st["seed_hits"] * 16 + st["total_overlaps"] * 24
+    ext_bytes = st["pairs"] * 2 * strand + st["seed_nodes"] * 16 + st["total_overlaps"] * 24
     roof = None
     n_ext = max(int(st.get("extend_launches", 0)), 1)
     if st["ms_extend"] > 0:
@@ -237,7 +239,7 @@ def main() -> None:
             "gbp_vs_gbp_per_sec": round(gbp_vs_gbp, 4),
             "breakdown_ms": {"index": round(st["ms_index"], 2), "seed": round(st["ms_seed"], 2),
                              "extend": round(st["ms_extend"], 2)},
-            "seed_hits": st["seed_hits"], "pairs": st["pairs"],
+            "seed_hits": st["seed_hits"], "seed_nodes": st["seed_nodes"], "pairs": st["pairs"],
             "setup_s": round(setup_s, 1),
             "roofline": roof,
             "probe_roofline": probe_roof,

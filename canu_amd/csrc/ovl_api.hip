@@ -1295,7 +1295,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     return rc;
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
-  uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0;
+  uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0, nodes_tot = 0;
   uint64_t staged_pairs = 0, long_pairs = 0, generic_pairs = 0;
   uint32_t chain_retries = 0;
   uint32_t n_probe_launch = 0, n_ext_launch = 0;
@@ -1529,6 +1529,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     }
     uint32_t npairs = hc[3];
     npairs_tot += npairs;
+    nodes_tot += hc[2];                                  // pnodes_next: the lists' nodes
 
     // ---- the extension of this chunk, queued on xs (the host does not wait for it) ----
     nout_ub += 3ull * npairs;
@@ -1780,6 +1781,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   c->stats.bad_short_window += hs[8];
   c->stats.bad_long_window += hs[9];
   c->stats.pairs += npairs_tot;
+  c->stats.seed_nodes += nodes_tot;
   c->stats.ms_seed += ms_probe + ms_chain;
   c->stats.ms_extend += ms_ext;
   c->stats.ms_probe_kernel += ms_probe;

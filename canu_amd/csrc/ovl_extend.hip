@@ -633,8 +633,14 @@ __device__ __forceinline__ double uni(double v) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// The row loop stays a call: inlined into process_pair (always_inline) the kernel keeps 80
+// VGPRs but spills 576 B per lane inside the loop -- extension 218 -> 297 ms (+37 %) on the
+// 10k-read job (r02v A/B).
+#ifndef OVL_PED_ATTR
+#define OVL_PED_ATTR noinline
+#endif
 template <int DIR, typename SS, bool L16>
-__device__ __attribute__((noinline)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
+__device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
                                                          int32_t a0, int32_t m, const SS &T,
                                                          int32_t t0, int32_t n, int32_t limit,
                                                          const WaveMem &WM, int32_t *dst,

@@ -62,7 +62,7 @@ class _Stats(ctypes.Structure):
          ("staged_pairs", ctypes.c_uint64), ("long_pairs", ctypes.c_uint64),
          ("generic_pairs", ctypes.c_uint64), ("ext_waves", ctypes.c_uint32),
          ("generic_waves", ctypes.c_uint32), ("stage_len", ctypes.c_uint32),
-         ("long_stage_len", ctypes.c_uint32)]
+         ("long_stage_len", ctypes.c_uint32), ("seed_nodes", ctypes.c_uint64)]
 
 
 class _HashLimits(ctypes.Structure):

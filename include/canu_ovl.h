@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 2
+#define OVL_ABI_VERSION 3
 
 typedef enum {
   OVL_OK               =  0,
@@ -232,6 +232,8 @@ typedef struct {
   uint32_t generic_waves;          /* waves of the generic launch                        */
   uint32_t stage_len;              /* longest read of the full-occupancy class           */
   uint32_t long_stage_len;         /* longest read of the long-read class (0: none)      */
+  uint64_t seed_nodes;             /* match nodes (Add_Match lists) handed to the extension
+                                      (ABI 3) */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);
