@@ -1751,8 +1751,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   if (c->dbg.p) {
     unsigned long long dd[32];
     (void)hipMemcpy(dd, c->dbg.p, 256, hipMemcpyDeviceToHost);
-    fprintf(stderr, "OVL_DEBUG cyc_A=%llu cyc_B=%llu cyc_cont=%llu cyc_C=%llu\n", dd[16], dd[17],
-            dd[18], dd[19]);
+    fprintf(stderr, "OVL_DEBUG cyc_A=%llu cyc_B=%llu cyc_cont=%llu cyc_C=%llu cyc_argmax=%llu "
+            "cyc_remove=%llu nodes=%llu\n", dd[16], dd[17], dd[18], dd[19], dd[20], dd[21],
+            dd[22]);
     fprintf(stderr, "OVL_DEBUG ped=%llu rows=%llu chunks=%llu slide_iters=%llu tb=%llu iters=%llu "
             "cyc_chunks=%llu cyc_tb=%llu pairs=%llu maxrows=%llu cyc_rest=%llu cyc_ped=%llu "
             "cyc_calls=%llu cyc_pair=%llu cyc_stage=%llu cyc_extend=%llu\n",

@@ -1437,8 +1437,17 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
   int32_t kind = K_NONE, S_Lo = 0, S_Hi = 0, T_Lo = 0, T_Hi = 0;
   int32_t remaining = nn;
   int32_t ld_len = 0;
+#ifdef OVL_PROFILE
+  if (X.dbg && lane == 0) atomicAdd(&X.dbg[22], (unsigned long long)nn);
+#endif
+  // Measured and not kept (r02v A/B, 10k reads, records identical): finding the next longest
+  // match inside the removal pass, which loads every node anyway (214.5 vs 215.4 ms); and
+  // skipping the removal pass when an extension reproduces the alignment the survivors were
+  // last tested against, coordinates and deltas compared (217 / 214 vs 222 ms: the compare,
+  // the saved deltas and the state carried across the row-loop calls cost more than the pass)
   while (remaining > 0) {
     // longest remaining match, first in list order on ties (:473-480)
+    PROF_T(pa0);
     int32_t bv = -1, bi = 0x7fffffff;
     for (int32_t i = lane; i < nn; i += 64) {
       int32_t L = nodes[i].Len;
@@ -1447,6 +1456,9 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     wave_argmax(bv, bi);
     Node M = nodes[bi];
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
+#ifdef OVL_PROFILE
+    { PROF_T(pa1); const int32_t mx = M.Len; if (X.dbg && lane == 0 && mx >= 0) atomicAdd(&X.dbg[20], pa1 - pa0); }
+#endif
     // -l: no extension once the unit has its limit of overlaps off that end (:481-487); the
     // match is still dropped with the previous extension's alignment (kind, S_Lo.., deltas)
     bool hit_limit = false;
@@ -1483,6 +1495,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     }
     if (consistent) break;
     // drop the longest match and every match on this alignment (:517-531)
+    PROF_T(pr0);
     int32_t removed = 0;
     const bool on_aln = (kind == K_DOVETAIL || X.partial);
     // thresholds and diagonals as int16 when every read is < 16384 (the staged kernel's
@@ -1552,6 +1565,10 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     for (int s = 32; s > 0; s >>= 1) removed += __shfl_xor(removed, s);
     remaining -= removed;
     vm_sync();
+#ifdef OVL_PROFILE
+    PROF_T(pr1);
+    if (X.dbg && lane == 0) atomicAdd(&X.dbg[21], pr1 - pr0);
+#endif
   }
 
   int32_t outputs = 0;
