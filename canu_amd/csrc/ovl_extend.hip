@@ -1014,11 +1014,29 @@ struct ExtOut {
 };
 
 // Extend_Alignment (prefixEditDistance-extend.C:86).  Leaves the merged Left_Delta in LD.
+#ifndef OVL_UNI_STATE
+#define OVL_UNI_STATE 1
+#endif
+
+#if OVL_UNI_STATE
+#define UNI(v) uni(v)
+#else
+#define UNI(v) (v)
+#endif
 template <bool FAST, bool L16, typename SS>
-__device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS &S,
+__device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS &S,
                                    int32_t S_Len, const SS &T, int32_t T_Len,
                                    const WaveMem &WM, int32_t *stk, int32_t *RD,
                                    int32_t *LD, uint32_t lane) {
+  // The match, the lengths and the row-loop results are wave-uniform: held in SGPRs they
+  // survive the two row-loop calls without the per-lane spills a VGPR copy needs (141 -> 132
+  // spill stores in the staged kernel; extension 217-218 -> 214-217 ms on 10k reads, r02v
+  // A/B, records identical).  SGPR copies of the pair's and unit's fields too (125 spill
+  // stores) measured the same, and were left out
+  Node M;
+  M.Start = UNI(Mv.Start); M.Offset = UNI(Mv.Offset); M.Len = UNI(Mv.Len); M.Next = Mv.Next;
+  S_Len = UNI(S_Len);
+  T_Len = UNI(T_Len);
   ExtOut r;
   int32_t right_errors = 0, left_errors = 0, leftover = 0;
   int32_t rmte = 1, lmte = 1;
@@ -1050,6 +1068,8 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &M, const SS 
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc1 - pc0);
 #endif
     if (po.ovf) { r.kind = -1; return r; }
+    po.err = UNI(po.err); po.mte = UNI(po.mte); po.a_len = UNI(po.a_len);
+    po.t_len = UNI(po.t_len); po.nd = UNI(po.nd); po.leftover = UNI(po.leftover);
     right_errors = po.err;
     rmte = po.mte;
     if (s_first) { S_Hi = po.a_len; T_Hi = po.t_len; }
