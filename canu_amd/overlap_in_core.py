@@ -91,6 +91,9 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
 _lib = None
 
 
+ABI_VERSION = 3          # OVL_ABI_VERSION of include/canu_ovl.h
+
+
 def load_library(path: str | None = None):
     """Load libcanu_ovl.so.  Raises if it was not built -- there is no fallback.
     CANU_OVL_LIB names another build of the same library (e.g. the profiling build)."""
@@ -101,6 +104,11 @@ def load_library(path: str | None = None):
     if not os.path.exists(path):
         raise OvlError(-1, f"{path} missing: run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
+    # the structs below mirror include/canu_ovl.h of this ABI: a library of another ABI
+    # would read or write past them (ovl_stats grew in ABI 3)
+    if lib.ovl_abi_version() != ABI_VERSION:
+        raise OvlError(-1, f"{path} has ABI {lib.ovl_abi_version()}, this binding expects "
+                           f"{ABI_VERSION}: rebuild with __graft_entry__.build()")
     P = ctypes.POINTER
     lib.ovl_params_init.argtypes = [P(_Params)]
     lib.ovl_params_finalize.argtypes = [P(_Params)]
