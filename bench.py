@@ -187,9 +187,10 @@ def main() -> None:
             probe_roof["traffic_frac"] = round(probe_roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
 
     # BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone (the
-    # Add_Ref hit list of every query, both orientations, written to HBM, not copied out)
+    # Add_Ref hit list of every query, both orientations, written to HBM, not copied out);
+    # a 1-GPU figure (at N > 1 a rank would report only its own shard's hits)
     seed_only = None
-    if not args.no_seed_only:
+    if world == 1 and not args.no_seed_only:
         oic.build_hash_index(q_lo, n)
         n_hits = oic.seed_hits(q_lo, q_hi, fetch=False)
         st1 = oic.stats()
