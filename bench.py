@@ -26,6 +26,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "overlaps/sec + Gbp-vs-Gbp/sec, 50k×10kb ONT reads, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+PROBE_BYTES_PER_WINDOW = 24.25  # k_probe: 16-B table entry + 8-B record + the 2-bit query
+RAND_LOOKUP_GPS = 39.2          # G random 16-B loads/s, 16 GiB table (tools/rand_ceiling.hip)
 
 
 def main() -> None:
@@ -185,6 +187,14 @@ def main() -> None:
         if tb:
             probe_roof["traffic_gbs"] = round(tb / (avg_ms * 1e-3) / 1e9, 1)
             probe_roof["traffic_frac"] = round(probe_roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
+        # the achievable bound of a one-random-lookup-per-window probe: independent random
+        # 16-B loads over a 16 GiB table (this workload's) sustain 39.2 G/s at any depth of
+        # memory-level parallelism (tools/rand_ceiling.hip, profiles/r02w_rand_ceiling.log)
+        wps = achieved * 1e9 / PROBE_BYTES_PER_WINDOW
+        probe_roof["random_lookup_ceiling"] = {
+            "windows_per_s": round(wps / 1e9, 2), "ceiling_gloads_per_s": RAND_LOOKUP_GPS,
+            "frac_of_ceiling": round(wps / 1e9 / RAND_LOOKUP_GPS, 3),
+            "source": "profiles/r02w_rand_ceiling.log (16 GiB table)"}
 
     # BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone (the
     # Add_Ref hit list of every query, both orientations, written to HBM, not copied out);
