@@ -5,15 +5,26 @@ One step = one full overlapInCore job over the resident read set: Build_Hash_Ind
 all reads (-h 1-N) and Find_Overlaps for every query read in both orientations (-r), with
 seed extension and ovOverlap output (BASELINE configs[2]).  Reads are generated
 synthetically (no datasets here), packed into HBM before the timed region; records stay in
-HBM.  With --gpus N (torchrun, one process per GPU) every rank generates 1/N of the reads,
-the packed read store is all-gathered over RCCL, every rank builds the index and searches
-its own query range (ranges balanced by pair count), independent per-shard output.
+HBM.  After the timed region the last step's records are fetched and compared with the
+reference's own output for the same reads (tests/golden/bench50k.json: count, SHA-256 of
+the sorted records, an additive multiset hash, the -s counters) -> "parity".
+
+--gpus N: one process per GPU.  Under a launcher (torch.distributed.run sets WORLD_SIZE)
+the world must have N ranks; without one, N > 1 starts N ranks itself (canu_amd/launch.py).
+Every rank generates 1/N of the reads, the packed read store is all-gathered over RCCL,
+every rank indexes its query shard's reads lo..n and searches its own query range; the
+shards' outputs are independent (no data-path collective).
+
+--workload configs4-rank: one rank's job of BASELINE configs[4]'s 8-GPU plan at 1/8 scale
+(500k x 12 kb +-20 % at 15x; the plan of canu_amd/dist.hash_block_jobs; one
+`-h lo-hi -r 1-hi` OverlapDriver job with canu's --hashbits 23 --hashload 0.75 batches).
 
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -26,35 +37,59 @@ sys.path.insert(0, ROOT)
 
 METRIC = "overlaps/sec + Gbp-vs-Gbp/sec, 50k×10kb ONT reads, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+CLOCK_GHZ = 2.4                # MI355X_MICROARCH.md: max clock
+N_CU, N_SIMD = 256, 1024
 PROBE_BYTES_PER_WINDOW = 24.25  # k_probe: 16-B table entry + 8-B record + the 2-bit query
 RAND_LOOKUP_GPS = 39.2          # G random 16-B loads/s, 16 GiB table (tools/rand_ceiling.hip)
+GOLDEN = os.path.join(ROOT, "tests", "golden", "bench50k.json")
 
 
-def main() -> None:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: the launcher's WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=50_000)
-    ap.add_argument("--read-len", type=int, default=10_000)
-    ap.add_argument("--coverage", type=float, default=25.0)
+    ap.add_argument("--workload", choices=("configs2", "configs4-rank"), default="configs2")
+    ap.add_argument("--reads", type=int, default=None)
+    ap.add_argument("--read-len", type=int, default=None)
+    ap.add_argument("--coverage", type=float, default=None)
     ap.add_argument("--read-error", type=float, default=0.015)
     ap.add_argument("--k", type=int, default=22)
     ap.add_argument("--maxerate", type=float, default=0.06)
     ap.add_argument("--minlength", type=int, default=500)
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample-reads", type=int, default=1000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--rank-job", type=int, default=0,
+                    help="configs4-rank on one GPU: which of the 8 ranks' jobs to time")
+    ap.add_argument("--cpu-sample-reads", type=int, default=1500)
+    ap.add_argument("--cpu-batches", type=int, default=5)
+    ap.add_argument("--cpu-max-threads", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the record digest check")
     ap.add_argument("--no-seed-only", action="store_true",
                     help="skip the configs[1] seed-hit figure (profiling passes)")
     ap.add_argument("--no-shard-timing", action="store_true",
                     help="skip the per-shard timing (1 GPU: each of the 8 query shards in turn)")
-    args = ap.parse_args()
+    a = ap.parse_args(argv)
+    c4 = a.workload == "configs4-rank"
+    if a.reads is None:
+        a.reads = 500_000 if c4 else 50_000
+    if a.read_len is None:
+        a.read_len = 12_000 if c4 else 10_000
+    if a.coverage is None:
+        a.coverage = 15.0 if c4 else 25.0
+    if a.seed is None:
+        a.seed = 5 if c4 else 1
+    return a
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+def main() -> None:
+    args = parse_args()
+    from canu_amd import launch
+    # decide BEFORE anything touches the GPU: N ranks of this script in a child launcher
+    if launch.needs_spawn(args.gpus):
+        sys.exit(launch.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    rank, world, local = launch.world_from_env(args.gpus)
     # rehearsal knobs (1-GPU box): CANU_DEVICE pins every rank to one device,
     # CANU_DIST_BACKEND=gloo replaces RCCL; the driver's multi-GPU runs use neither
     local = int(os.environ.get("CANU_DEVICE", local))
@@ -69,51 +104,28 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-
-    from canu_amd.synth import synth_reads, random_genome
-    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
-    from canu_amd.dist import gather_read_store, query_shards
-
-    n = args.reads
-    genome_len = int(n * args.read_len / args.coverage)
-    gen_kw = dict(n_reads=n, read_len=args.read_len, genome_len=genome_len,
-                  error_rate=args.read_error, seed=args.seed)
-
-    # ---- setup: each rank generates its slice, then the read store is all-gathered ----
-    t_setup = time.time()
-    genome = random_genome(np.random.default_rng(args.seed), genome_len)
-    lo = n * rank // world
-    hi = n * (rank + 1) // world
-    part = synth_reads(genome=genome, read_range=(lo, hi), **gen_kw)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
     dev = torch.device("cuda", local)
-    if world == 1:
-        bases = torch.from_numpy(part.bases).to(dev)
-        lengths = part.lengths
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
+
+    def reduce(v, op, dtype):
+        t = torch.tensor([v], dtype=dtype, device=red_dev)
+        if dist:
+            dist.all_reduce(t, op=op)
+        return t.item()
+
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    if args.workload == "configs4-rank":
+        job = Configs4Rank(args, rank, world, dist, dev)
     else:
-        bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(dev), part.lengths,
-                                           dist, dev)          # RCCL over xGMI
-    offsets = np.zeros(n, dtype=np.uint64)
-    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
-    d_offsets = torch.from_numpy(offsets.view(np.int64)).to(dev)
-    total_bases = int(lengths.sum(dtype=np.uint64))
-
-    P = OicParameters(Kmer_Len=args.k, maxErate=float(np.float32(args.maxerate)),
-                      Min_Olap_Len=args.minlength).finalize()
-    oic = OverlapInCore(P, device=local)
-    oic.load_reads_device(1, bases.data_ptr(), d_offsets.data_ptr(), lengths)
-    torch.cuda.synchronize()
-    shards = query_shards(n, world)
-    q_lo, q_hi = shards[rank]
+        job = Configs2(args, rank, world, dist, dev)
+    t_setup = time.time()
+    job.setup(OicParameters, OverlapInCore)
     setup_s = time.time() - t_setup
-
-    # each rank indexes reads q_lo..n only: its queries' targets all have larger IDs
-    # (Find_Overlaps.C:328), so records and counters equal the whole index's
-    def step() -> int:
-        oic.build_hash_index(q_lo, n)
-        return oic.find_overlaps(q_lo, q_hi)
+    oic = job.oic
 
     for _ in range(args.warmup):
-        step()
+        job.step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -121,7 +133,7 @@ def main() -> None:
     t0 = time.perf_counter()
     nrec = 0
     for _ in range(args.steps):
-        nrec = step()
+        nrec = job.step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -129,109 +141,27 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     st = oic.stats()
 
-    red = dev if backend == "nccl" else torch.device("cpu")
-    el = torch.tensor([elapsed], dtype=torch.float64, device=red)
-    nr = torch.tensor([nrec], dtype=torch.int64, device=red)
-    if dist:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(nr, op=dist.ReduceOp.SUM)
-    elapsed = float(el.item())
-    total_ovl = int(nr.item())
+    SUM, MAX = (dist.ReduceOp.SUM, dist.ReduceOp.MAX) if dist else (None, None)
+    elapsed = float(reduce(elapsed, MAX, torch.float64))
+    total_ovl = int(reduce(nrec, SUM, torch.int64))
     value = total_ovl * args.steps / elapsed
     ms_step = 1000.0 * elapsed / args.steps
-    gbp = total_bases / 1e9
+    gbp = job.total_bases / 1e9
     gbp_vs_gbp = gbp * gbp / 2.0 * args.steps / elapsed    # all-vs-all, each pair once
 
-    traffic = load_traffic()
-    # Dominant kernel: k_extend (the banded edit-distance extension).  Its algorithmic HBM
-    # bytes per pair are the two packed strands it stages (2 bits/base + guard word each),
-    # the pair's seed-match nodes (16 B each, read once: the Add_Match lists, not the seed
-    # hits they merge -- rounds before r02v counted 16 B per hit, ~7x the bytes) and its
-    # output records (24 B each); per launch
-    # = the step's bytes / the step's launches, over the launches' average duration (HIP
-    # events on the library's stream).
-    avg_len = total_bases / max(n, 1)
-    strand = 8.0 * (np.ceil(avg_len / 32.0) + 1.0)
-    ext_bytes = st["pairs"] * 2 * strand + st["seed_nodes"] * 16 + st["total_overlaps"] * 24
-    roof = None
-    n_ext = max(int(st.get("extend_launches", 0)), 1)
-    if st["ms_extend"] > 0:
-        per_launch = ext_bytes / n_ext
-        avg_ms = st["ms_extend"] / n_ext
-        achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": _traffic(traffic, "k_extend"), "kernel": "k_extend",
-                "limiter": "instruction issue of the greedy O(ND) rows: the per-row scalar "
-                           "control (SALU, shared by a CU's 4 SIMDs) first, then integer VALU; "
-                           "no MFMA shape, HBM far from busy",
-                "issue": traffic.get("k_extend", {}).get("issue"),
-                "algorithmic_bytes_per_launch": int(per_launch), "launches": n_ext,
-                "avg_launch_ms": round(avg_ms, 3)}
-    # The north star's roofline target: the hash-probe kernel (one 16-B table entry and one
-    # 8-B probe record per query window, plus the 2-bit query).
-    probe_roof = None
-    n_pr = max(int(st.get("probe_launches", 0)), 1)
-    if st["ms_probe_kernel"] > 0:
-        per_launch = st["probe_bytes"] / n_pr
-        avg_ms = st["ms_probe_kernel"] / n_pr
-        achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        probe_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                      "traffic": _traffic(traffic, "k_probe"), "kernel": "k_probe",
-                      "algorithmic_bytes_per_launch": int(per_launch), "launches": n_pr,
-                      "avg_launch_ms": round(avg_ms, 3)}
-        # the same launch against the roofline in the bytes it actually moves (PMC traffic
-        # per launch over this run's launch time): one 64-B sector per 16-B slot probed
-        tb = probe_roof["traffic"]
-        if tb:
-            probe_roof["traffic_gbs"] = round(tb / (avg_ms * 1e-3) / 1e9, 1)
-            probe_roof["traffic_frac"] = round(probe_roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
-        # the achievable bound of a one-random-lookup-per-window probe: independent random
-        # 16-B loads over a 16 GiB table (this workload's) sustain 39.2 G/s at any depth of
-        # memory-level parallelism (tools/rand_ceiling.hip, profiles/r02w_rand_ceiling.log)
-        wps = achieved * 1e9 / PROBE_BYTES_PER_WINDOW
-        probe_roof["random_lookup_ceiling"] = {
-            "windows_per_s": round(wps / 1e9, 2), "ceiling_gloads_per_s": RAND_LOOKUP_GPS,
-            "frac_of_ceiling": round(wps / 1e9 / RAND_LOOKUP_GPS, 3),
-            "source": "profiles/r02w_rand_ceiling.log (16 GiB table)"}
+    # ---- parity of the last step's records against the reference's digest ------------
+    parity = None
+    if not args.no_parity:
+        parity = job.parity(st, reduce, SUM, torch)
 
-    # BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone (the
-    # Add_Ref hit list of every query, both orientations, written to HBM, not copied out);
-    # a 1-GPU figure (at N > 1 a rank would report only its own shard's hits)
-    seed_only = None
-    if world == 1 and not args.no_seed_only:
-        oic.build_hash_index(q_lo, n)
-        n_hits = oic.seed_hits(q_lo, q_hi, fetch=False)
-        st1 = oic.stats()
-        seed_only = {"workload": "configs[1]: hash index + seed-hit list, same reads",
-                     "seed_hits": n_hits, "ms_index": round(st1["ms_index"], 2),
-                     "ms_seed_hits": round(st1["ms_seed_hits"], 2),
-                     "seed_hits_per_s": round(n_hits / ((st1["ms_index"] + st1["ms_seed_hits"])
-                                                        * 1e-3), 1)}
+    roof, probe_roof, traffic_note = rooflines(args, job, st, world)
 
-    # Multi-GPU evidence from one GPU: the 8-way query shards (dist.query_shards) one after
-    # another, each with its own index build, as each rank of an 8-GPU job runs them
-    shard = None
-    if world == 1 and not args.no_shard_timing:
-        shard_ms = []
-        for lo8, hi8 in query_shards(n, 8):
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            oic.build_hash_index(lo8, n)
-            oic.find_overlaps(lo8, hi8)
-            torch.cuda.synchronize()
-            shard_ms.append(round(1000.0 * (time.perf_counter() - t1), 1))
-        shard = {"shards": 8, "shard_ms": shard_ms,
-                 "projected_speedup_8": round(sum(shard_ms) / max(shard_ms), 2),
-                 "projected_vs_1gpu_step": round(ms_step / max(shard_ms), 2),
-                 "note": "the 8 ranks' jobs (index over the shard's lo..n, then its queries) "
-                         "timed in turn on one GPU; projected_speedup_8 = sum / max, "
-                         "projected_vs_1gpu_step = this run's 1-GPU step / the slowest rank; "
-                         "the driver's 8-GPU run measures the real curve"}
+    seed_only = job.seed_only() if world == 1 and not args.no_seed_only else None
+    shard = job.shard_timing(ms_step) if world == 1 and not args.no_shard_timing else None
+    xgmi = job.index_allgather_timing(torch) if world > 1 and backend == "nccl" else None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "configs2":
         cpu = cpu_baseline(args)
 
     if rank == 0:
@@ -240,13 +170,9 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "u8/2-bit bases, int32 edit rows", "data": "synthetic",
-            "config": {"workload": "configs[2]: 50k synthetic ONT reads x 10 kb, full "
-                                   "overlapInCore (seed + banded extend), all-vs-all",
-                       "reads": n, "read_len": args.read_len, "coverage": args.coverage,
-                       "read_error": args.read_error, "k": args.k,
-                       "maxerate": P.maxErate, "minlength": args.minlength,
-                       "parallelism": f"query-shard{world}"},
+            "config": job.config(P_maxerate=job.P.maxErate, world=world, backend=backend),
             "overlaps_per_step": total_ovl,
+            "parity": parity,
             "gbp_vs_gbp_per_sec": round(gbp_vs_gbp, 4),
             "breakdown_ms": {"index": round(st["ms_index"], 2), "seed": round(st["ms_seed"], 2),
                              "extend": round(st["ms_extend"], 2)},
@@ -254,8 +180,10 @@ def main() -> None:
             "setup_s": round(setup_s, 1),
             "roofline": roof,
             "probe_roofline": probe_roof,
+            "traffic_source": traffic_note,
             "seed_only": seed_only,
             "shard_timing": shard,
+            "index_allgather": xgmi,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -264,33 +192,385 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-def _traffic(t: dict, k: str):
-    """HBM bytes per launch of kernel k from the committed PMC passes (same unit as
-    algorithmic_bytes_per_launch), or None."""
-    v = t.get(k)
-    return None if v is None else v.get("hbm_bytes_per_launch")
+class Configs2:
+    """BASELINE configs[2]: the all-vs-all job over one index, query shards per rank."""
+
+    def __init__(self, args, rank, world, dist, dev):
+        self.args, self.rank, self.world, self.dist, self.dev = args, rank, world, dist, dev
+
+    def workload_key(self) -> dict:
+        a = self.args
+        return {"workload": "configs2", "reads": a.reads, "read_len": a.read_len,
+                "coverage": a.coverage, "read_error": a.read_error, "seed": a.seed, "k": a.k,
+                "maxerate": float(np.float32(a.maxerate)), "minlength": a.minlength}
+
+    def setup(self, OicParameters, OverlapInCore):
+        import torch
+        from canu_amd.synth import synth_reads, random_genome
+        from canu_amd.dist import gather_read_store, query_shards
+        a, n = self.args, self.args.reads
+        genome_len = int(n * a.read_len / a.coverage)
+        genome = random_genome(np.random.default_rng(a.seed), genome_len)
+        lo = n * self.rank // self.world
+        hi = n * (self.rank + 1) // self.world
+        part = synth_reads(n_reads=n, read_len=a.read_len, genome_len=genome_len,
+                           error_rate=a.read_error, seed=a.seed, genome=genome,
+                           read_range=(lo, hi))
+        if self.world == 1:
+            bases = torch.from_numpy(part.bases).to(self.dev)
+            lengths = part.lengths
+        else:
+            bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(self.dev),
+                                               part.lengths, self.dist, self.dev)  # RCCL
+        offsets = np.zeros(n, dtype=np.uint64)
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+        self._keep = (bases, torch.from_numpy(offsets.view(np.int64)).to(self.dev))
+        self.total_bases = int(lengths.sum(dtype=np.uint64))
+        self.n = n
+        self.P = OicParameters(Kmer_Len=a.k, maxErate=float(np.float32(a.maxerate)),
+                               Min_Olap_Len=a.minlength).finalize()
+        self.oic = OverlapInCore(self.P, device=self.dev.index)
+        self.oic.load_reads_device(1, bases.data_ptr(), self._keep[1].data_ptr(), lengths)
+        torch.cuda.synchronize()
+        self.q_lo, self.q_hi = query_shards(n, self.world)[self.rank]
+
+    # each rank indexes reads q_lo..n only: its queries' targets all have larger IDs
+    # (Find_Overlaps.C:328), so records and counters equal the whole index's
+    def step(self) -> int:
+        self.oic.build_hash_index(self.q_lo, self.n)
+        return self.oic.find_overlaps(self.q_lo, self.q_hi)
+
+    def config(self, P_maxerate, world, backend):
+        a = self.args
+        return {"workload": "configs[2]: 50k synthetic ONT reads x 10 kb, full "
+                            "overlapInCore (seed + banded extend), all-vs-all",
+                "reads": a.reads, "read_len": a.read_len, "coverage": a.coverage,
+                "read_error": a.read_error, "k": a.k, "maxerate": P_maxerate,
+                "minlength": a.minlength, "parallelism": f"query-shard{world}",
+                "dist_backend": backend if world > 1 else None}
+
+    def parity(self, st, reduce, SUM, torch):
+        """The last step's records (and -s counters) vs the reference's digest of the same
+        reads, when this run's workload is the one the digest was made for."""
+        from canu_amd import digest
+        try:
+            with open(GOLDEN) as f:
+                g = json.load(f)
+        except (OSError, ValueError):
+            return {"checked": False, "reason": f"{os.path.relpath(GOLDEN, ROOT)} missing"}
+        gw = g["workload"]
+        mine = self.workload_key()
+        same = all(np.isclose(float(gw[k]), float(mine[k])) for k in
+                   ("reads", "read_len", "coverage", "read_error", "seed", "k", "maxerate",
+                    "minlength"))
+        if not same:
+            return {"checked": False, "reason": "workload differs from the digest's"}
+        t0 = time.time()
+        rec = self.oic.fetch()
+        mh = digest.multiset_hash(rec)
+        # the multiset hash adds up over the ranks' disjoint query shards; the sum is taken
+        # as two 32-bit halves so the int64 all-reduce cannot overflow
+        lo = int(reduce(mh & 0xFFFFFFFF, SUM, torch.int64))
+        hi = int(reduce(mh >> 32, SUM, torch.int64))
+        total_mh = (lo + (hi << 32)) & ((1 << 64) - 1)
+        n_all = int(reduce(int(rec.shape[0]), SUM, torch.int64))
+        names = {"kmer_hits_without_olap": "kmer_hits_without_olap",
+                 "kmer_hits_with_olap": "kmer_hits_with_olap", "multi_overlaps": "multi",
+                 "total_overlaps": "total", "contained_overlaps": "contained",
+                 "dovetail_overlaps": "dovetail"}
+        counters_ok = True
+        for mine_k, ref_k in names.items():
+            v = int(reduce(int(st[mine_k]), SUM, torch.int64))
+            if v != int(g["stats"][ref_k]):
+                counters_ok = False
+        out = {"checked": True, "records": n_all, "ref_records": g["records"],
+               "multiset_hash": f"{total_mh:016x}",
+               "multiset_ok": f"{total_mh:016x}" == g["multiset_hash"],
+               "counters_ok": counters_ok, "golden": os.path.relpath(GOLDEN, ROOT)}
+        if self.world == 1:
+            out["sha256_ok"] = digest.sha256_sorted(rec) == g["sha256_sorted"]
+        out["ok"] = bool(out["multiset_ok"] and counters_ok and n_all == g["records"] and
+                         out.get("sha256_ok", True))
+        out["check_s"] = round(time.time() - t0, 2)
+        return out
+
+    def seed_only(self):
+        """BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone
+        (the Add_Ref hit list of every query, both orientations, written to HBM)."""
+        self.oic.build_hash_index(self.q_lo, self.n)
+        n_hits = self.oic.seed_hits(self.q_lo, self.q_hi, fetch=False)
+        st1 = self.oic.stats()
+        return {"workload": "configs[1]: hash index + seed-hit list, same reads",
+                "seed_hits": n_hits, "ms_index": round(st1["ms_index"], 2),
+                "ms_seed_hits": round(st1["ms_seed_hits"], 2),
+                "seed_hits_per_s": round(n_hits / ((st1["ms_index"] + st1["ms_seed_hits"])
+                                                   * 1e-3), 1)}
+
+    def shard_timing(self, ms_step):
+        """The 8-way query shards (dist.query_shards) one after another on this GPU, each
+        with its own index build, as each rank of an 8-GPU job runs them."""
+        import torch
+        from canu_amd.dist import query_shards
+        shard_ms = []
+        for lo8, hi8 in query_shards(self.n, 8):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            self.oic.build_hash_index(lo8, self.n)
+            self.oic.find_overlaps(lo8, hi8)
+            torch.cuda.synchronize()
+            shard_ms.append(round(1000.0 * (time.perf_counter() - t1), 1))
+        return {"shards": 8, "shard_ms": shard_ms,
+                "projected_speedup_8": round(sum(shard_ms) / max(shard_ms), 2),
+                "projected_vs_1gpu_step": round(ms_step / max(shard_ms), 2),
+                "note": "the 8 ranks' jobs (index over the shard's lo..n, then its queries) "
+                        "timed in turn on one GPU; projected_speedup_8 = sum / max, "
+                        "projected_vs_1gpu_step = this run's 1-GPU step / the slowest rank; "
+                        "the driver's 8-GPU run measures the real curve"}
+
+    def index_allgather_timing(self, torch):
+        """What the north star's 'all-gather the shared k-mer index at setup' would cost on
+        this node: an RCCL all_gather of a 1/N slice per rank of a buffer the size of the
+        full index (keys, positions, table) -- timed here, beside the index build each rank
+        does instead (Multi-GPU)."""
+        st = self.oic.stats()
+        # the full index of 50k x 10 kb: 8 B positions + 8 B keys per window + the 16 GiB
+        # table (DESIGN.md data layout) -- scaled by this run's bases
+        windows = self.total_bases
+        nbytes = int(16 * windows + (16 << 30) * self.total_bases / 500e6)
+        per = (nbytes // self.world) & ~255
+        src = torch.empty(per, dtype=torch.uint8, device=self.dev)
+        dst = torch.empty(per * self.world, dtype=torch.uint8, device=self.dev)
+        self.dist.all_gather_into_tensor(dst, src)           # warm the communicator
+        torch.cuda.synchronize()
+        self.dist.barrier()
+        t0 = time.perf_counter()
+        self.dist.all_gather_into_tensor(dst, src)
+        torch.cuda.synchronize()
+        ms = 1000.0 * (time.perf_counter() - t0)
+        del src, dst
+        ms_t = torch.tensor([ms], dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(ms_t, op=self.dist.ReduceOp.MAX)
+        return {"index_bytes": nbytes, "allgather_ms": round(float(ms_t.item()), 2),
+                "rank_index_build_ms": round(st["ms_index"], 2),
+                "note": "RCCL all_gather of an index-sized buffer (each rank 1/N of it) vs "
+                        "the index build each rank runs over its shard's reads lo..n"}
 
 
-def load_traffic() -> dict:
-    """Per-kernel HBM traffic of one default bench step from the committed rocprofv3 PMC
-    passes (profiles/traffic.json, tools/pmc_traffic.py): (r x FETCH_SIZE + WRITE_SIZE) KiB
-    with r the read correction calibrated per access pattern (profiles/calib_traffic.json:
-    2 for coalesced streams, 1 for k_probe's random 16-B table loads).  Empty when absent."""
+class Configs4Rank(Configs2):
+    """One rank's job of configs[4]'s plan (4M x 12 kb on 8 GPUs) at 1/8 scale: the hash
+    block `-h lo-hi` searched by `-r 1-hi`, OverlapDriver batches inside (overlapInCore.C:
+    191-300) with canu's --hashbits 23 --hashload 0.75.  At N ranks the plan has N jobs and
+    rank r runs job r; on one GPU `--rank-job` picks one of the 8-way plan's jobs."""
+
+    HASHBITS, HASHLOAD = 23, 0.75
+
+    def setup(self, OicParameters, OverlapInCore):
+        import torch
+        from canu_amd.synth import synth_reads_parallel
+        from canu_amd.dist import gather_read_store, hash_block_jobs
+        a, n = self.args, self.args.reads
+        genome_len = int(n * a.read_len / a.coverage)
+        lo = n * self.rank // self.world
+        hi = n * (self.rank + 1) // self.world
+        part = synth_reads_parallel(n, a.read_len, genome_len, a.read_error, seed=a.seed,
+                                    len_jitter=0.2, read_range=(lo, hi),
+                                    workers=max(1, 16 // self.world))
+        if self.world == 1:
+            bases = torch.from_numpy(part.bases).to(self.dev)
+            lengths = part.lengths
+        else:
+            bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(self.dev),
+                                               part.lengths, self.dist, self.dev)
+        del part
+        offsets = np.zeros(n, dtype=np.uint64)
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+        self._keep = (bases, torch.from_numpy(offsets.view(np.int64)).to(self.dev))
+        self.total_bases = int(lengths.sum(dtype=np.uint64))
+        self.n = n
+        plan_ranks = 8 if self.world == 1 else self.world
+        load = self.HASHLOAD * (1 << self.HASHBITS) * 21
+        self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load)
+        ji = a.rank_job if self.world == 1 else self.rank
+        self.job = self.jobs[ji]
+        (h_lo, h_hi), (r_lo, r_hi) = self.job["h"], self.job["r"]
+        hashed = int(lengths[h_lo - 1:h_hi].sum(dtype=np.uint64)) + (h_hi - h_lo + 1)
+        self.P = OicParameters(Kmer_Len=a.k, maxErate=float(np.float32(a.maxerate)),
+                               Min_Olap_Len=a.minlength, bgnHashID=h_lo, endHashID=h_hi,
+                               bgnRefID=r_lo, endRefID=r_hi, Hash_Mask_Bits=self.HASHBITS,
+                               Max_Hash_Load=self.HASHLOAD, Max_Hash_Strings=10_000_000,
+                               Max_Hash_Data_Len=hashed + 1024, Num_PThreads=16).finalize()
+        self.oic = OverlapInCore(self.P, device=self.dev.index)
+        self.oic.load_reads_device(1, bases.data_ptr(), self._keep[1].data_ptr(), lengths)
+        torch.cuda.synchronize()
+
+    def step(self) -> int:
+        return self.oic.overlap_driver(store_num_reads=self.n)
+
+    def config(self, P_maxerate, world, backend):
+        a = self.args
+        return {"workload": "configs[4] rank job at 1/8 scale: 500k ONT reads x 12 kb "
+                            "(+-20 %) at 15x, one `-h lo-hi -r 1-hi` OverlapDriver job of the "
+                            f"{len(self.jobs)}-rank plan, --hashbits {self.HASHBITS} "
+                            f"--hashload {self.HASHLOAD}",
+                "reads": a.reads, "read_len": a.read_len, "coverage": a.coverage,
+                "read_error": a.read_error, "k": a.k, "maxerate": P_maxerate,
+                "minlength": a.minlength, "job": {"h": list(self.job["h"]),
+                                                  "r": list(self.job["r"]),
+                                                  "index": a.rank_job if world == 1 else "rank"},
+                "hash_batches": self.oic.stats()["hash_batches"],
+                "parallelism": f"hash-block{world}",
+                "dist_backend": backend if world > 1 else None}
+
+    def parity(self, st, reduce, SUM, torch):
+        return {"checked": False, "reason": "no reference digest at this size; the rank-job "
+                "union and oic_ref parity are tests/test_configs4.py (-m gpu)"}
+
+    def seed_only(self):
+        return None
+
+    def shard_timing(self, ms_step):
+        return None
+
+    def index_allgather_timing(self, torch):
+        return None
+
+
+def source_hash() -> str:
+    """SHA-256 (16 hex) of the HIP sources the PMC counters were taken from."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "canu_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.startswith("ovl_") and (name.endswith(".hip") or name.endswith(".h")):
+            with open(os.path.join(csrc, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(job, world: int):
+    """Per-kernel PMC figures (profiles/traffic.json, tools/pmc_traffic.py) when they were
+    taken on THIS workload (one rank) and THESE sources; else ({}, why not)."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            return json.load(f)
+            t = json.load(f)
     except (OSError, ValueError):
-        return {}
+        return {}, "profiles/traffic.json missing"
+    meta = t.get("_method", {})
+    if world != 1:
+        return {}, "PMC counters are per-workload single-GPU figures: not used at N > 1"
+    if meta.get("workload") != job.workload_key():
+        return {}, f"PMC passes ({meta.get('tag')}) were taken on another workload"
+    if meta.get("src_sha") != source_hash():
+        return {}, f"PMC passes ({meta.get('tag')}) were taken on other kernel sources"
+    return t, f"profiles/traffic.json ({meta.get('tag')}, same workload and sources)"
+
+
+def rooflines(args, job, st, world):
+    """The dominant kernel (k_extend) against the roofline that binds it -- instruction
+    issue -- with its HBM figures beside; and the hash-probe kernel against HBM."""
+    traffic, note = load_traffic(job, world) if args.workload == "configs2" else ({}, None)
+    n = job.n
+    avg_len = job.total_bases / max(n, 1)
+    strand = 8.0 * (np.ceil(avg_len / 32.0) + 1.0)
+    # algorithmic HBM bytes of k_extend per pair: both packed strands, 16 B per seed-match
+    # node (the Add_Match lists), 24 B per record written
+    ext_bytes = st["pairs"] * 2 * strand + st["seed_nodes"] * 16 + st["total_overlaps"] * 24
+    roof = None
+    n_ext = max(int(st.get("extend_launches", 0)), 1)
+    if st["ms_extend"] > 0:
+        per_launch = ext_bytes / n_ext
+        avg_ms = st["ms_extend"] / n_ext
+        hbm_gbs = per_launch / (avg_ms * 1e-3) / 1e9
+        ext = traffic.get("k_extend", {})
+        tb = ext.get("hbm_bytes_per_launch")
+        hbm = {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hbm_gbs / HBM_PEAK_GBS, 5), "traffic": tb,
+               "traffic_gbs": round(tb / (avg_ms * 1e-3) / 1e9, 1) if tb else None,
+               "traffic_frac": round(tb / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+               if tb else None}
+        iss = ext.get("issue")
+        roof = {"kernel": "k_extend", "algorithmic_bytes_per_launch": int(per_launch),
+                "launches": n_ext, "avg_launch_ms": round(avg_ms, 3)}
+        if iss:
+            # wave-instructions per launch from PMC (deterministic for a workload and build)
+            # over this run's launch time, against the issue peaks: one SALU per CU-cycle
+            # (one scalar unit per CU), one VALU per 2 cycles per SIMD (wave64 on SIMD-32)
+            launches = ext.get("launches_per_step", 1)
+            secs = avg_ms * 1e-3
+            salu = iss["salu_insts"] / launches / secs / 1e9
+            valu = iss["valu_insts"] / launches / secs / 1e9
+            salu_pk = N_CU * CLOCK_GHZ
+            valu_pk = N_SIMD * CLOCK_GHZ / 2.0
+            bind = "SALU" if salu / salu_pk >= valu / valu_pk else "VALU"
+            a, p = (salu, salu_pk) if bind == "SALU" else (valu, valu_pk)
+            roof.update({"bound": "issue", "achieved": round(a, 1), "peak": round(p, 1),
+                         "unit": f"G {bind} wave-instructions/s", "frac": round(a / p, 4),
+                         "traffic": tb, "binding_unit": bind,
+                         "salu_frac": round(salu / salu_pk, 4),
+                         "valu_frac": round(valu / valu_pk, 4), "hbm": hbm,
+                         "limiter": "instruction issue of the greedy O(ND) rows (per-row "
+                                    "scalar control on the CU's one scalar unit, integer "
+                                    "VALU beside it); HBM moves the row log and spills "
+                                    "(hbm.traffic_gbs), not the algorithmic bytes"})
+        else:
+            roof.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": hbm["frac"], "traffic": None,
+                         "limiter": "issue-bound (see DESIGN.md); no PMC issue counters "
+                                    "for this workload/build, so the HBM figure is given"})
+    probe_roof = None
+    n_pr = max(int(st.get("probe_launches", 0)), 1)
+    if st["ms_probe_kernel"] > 0:
+        per_launch = st["probe_bytes"] / n_pr
+        avg_ms = st["ms_probe_kernel"] / n_pr
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9
+        tb = traffic.get("k_probe", {}).get("hbm_bytes_per_launch")
+        probe_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                      "traffic": tb, "kernel": "k_probe",
+                      "algorithmic_bytes_per_launch": int(per_launch), "launches": n_pr,
+                      "avg_launch_ms": round(avg_ms, 3)}
+        if tb:
+            probe_roof["traffic_gbs"] = round(tb / (avg_ms * 1e-3) / 1e9, 1)
+            probe_roof["traffic_frac"] = round(probe_roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
+        wps = achieved * 1e9 / PROBE_BYTES_PER_WINDOW
+        probe_roof["random_lookup_ceiling"] = {
+            "windows_per_s": round(wps / 1e9, 2), "ceiling_gloads_per_s": RAND_LOOKUP_GPS,
+            "frac_of_ceiling": round(wps / 1e9 / RAND_LOOKUP_GPS, 3),
+            "source": "profiles/r02w_rand_ceiling.log (16 GiB table)"}
+    return roof, probe_roof, note
+
+
+def cpu_share() -> dict:
+    """The CPUs this process may use: the cgroup quota (cpu.max) and the affinity mask."""
+    out = {"host_cpus": os.cpu_count()}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        out["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        out["cgroup_cpu_max"] = f"{q} {per}"
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        out["cgroup_cpu_max"] = None
+    out["quota_cpus"] = quota
+    usable = out["affinity"] or 1
+    if quota is not None:
+        usable = min(usable, max(1, int(quota)))
+    out["usable"] = usable
+    return out
 
 
 def cpu_baseline(args) -> dict | None:
     """The reference overlapInCore (oracle/_ref/oic_ref, built from its sources) on a
     bounded sample of the same workload: fewer reads, same read length / error / coverage,
-    with canu's production hash settings -- utgOvlHashBits 23, utgOvlHashLoad 0.75
-    (Defaults.pm:687-688) -- and the sample split into three hash batches (--hashstrings).
-    Threads: the GPU box's CPU share (16 per GPU), not os.cpu_count(), which there reports
-    the whole host; a per-core figure is given for scaling to other hosts."""
+    canu's production hash settings -- utgOvlHashBits 23, utgOvlHashLoad 0.75
+    (Defaults.pm:687-688) -- and the sample split into --cpu-batches hash batches
+    (--hashstrings), as canu's jobs are.  Threads: min(64, the CPUs this process may use:
+    cgroup quota and affinity); a 64-core figure is only reported when 64 were usable."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import oracle
@@ -299,27 +579,35 @@ def cpu_baseline(args) -> dict | None:
         return None
     if not oracle.reference_available():
         return None
+    share = cpu_share()
+    threads = max(1, min(args.cpu_max_threads, share["usable"]))
     ns = args.cpu_sample_reads
     gl = int(ns * args.read_len / args.coverage)
     rs = synth_reads(ns, args.read_len, gl, args.read_error, seed=args.seed + 1000)
     p = oracle.default_params(kmer_len=args.k, max_erate=args.maxerate,
                               min_olap_len=args.minlength)
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
-    # three hash batches by --hashstrings (a --hashdatalen below the range's bases trips
-    # the reference's assert at Build_Hash_Index.C:523)
-    strings = (rs.nreads + 2) // 3
+    # hash batches by --hashstrings (a --hashdatalen below the range's bases trips the
+    # reference's assert at Build_Hash_Index.C:523)
+    nb = max(1, args.cpu_batches)
+    strings = (rs.nreads + nb - 1) // nb
     datalen = rs.total_bases() + rs.nreads + 1
     rec, secs, wall = oracle.run_reference(
         rs, p, threads=threads, hash_bits=23, with_time=True,
         batching={"hashstrings": strings, "hashdatalen": datalen, "hashload": 0.75})
     v = len(rec) / secs
-    return {"value": round(v, 1), "unit": "overlaps/s", "cores": threads,
-            "kind": "reference", "per_core": round(v / threads, 1),
-            "host_cpus": os.cpu_count(),
-            "sample": f"{ns} reads x {args.read_len} bp at {args.coverage:.0f}x "
-                      f"(genome {gl} bp), --hashbits 23 --hashload 0.75 --hashstrings {strings} "
-                      f"(3 hash batches), reference OverlapDriver() wall {secs:.2f}s incl. its "
-                      f".ovb writing, {len(rec)} overlaps"}
+    out = {"value": round(v, 1), "unit": "overlaps/s", "cores": threads,
+           "kind": "reference", "per_core": round(v / threads, 1), "cpu_share": share,
+           "sample": f"{ns} reads x {args.read_len} bp at {args.coverage:.0f}x "
+                     f"(genome {gl} bp), --hashbits 23 --hashload 0.75 --hashstrings "
+                     f"{strings} ({nb} hash batches), -t {threads}, reference OverlapDriver() "
+                     f"wall {secs:.2f}s incl. its .ovb writing, {len(rec)} overlaps"}
+    if threads >= 64:
+        out["host64_measured"] = round(v, 1)
+    else:
+        out["host64_measured"] = None
+        out["host64_note"] = (f"{threads}-core share of this host (cgroup/affinity); a 64-core "
+                              "figure was not measurable here")
+    return out
 
 
 if __name__ == "__main__":

@@ -33,7 +33,8 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 1024 SIMDs x 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: the launcher's WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=200_000)
@@ -46,9 +47,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from canu_amd import launch
+    # decide BEFORE anything touches the GPU: N ranks of this script in a child launcher
+    if launch.needs_spawn(args.gpus):
+        sys.exit(launch.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    rank, world, local = launch.world_from_env(args.gpus)
     # rehearsal knobs (1-GPU box): CANU_DEVICE pins every rank to one device,
     # CANU_DIST_BACKEND=gloo replaces RCCL; the driver's multi-GPU runs use neither
     local = int(os.environ.get("CANU_DEVICE", local))
@@ -63,6 +66,7 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
 
     from canu_amd.synth import synth_reads, random_genome
     from canu_amd.mhap import Mhap, MhapParameters
@@ -188,7 +192,8 @@ def main() -> None:
                        "coverage": args.coverage, "read_error": args.read_error,
                        "sensitivity": args.sensitivity, "num_hashes": H,
                        "ordered_sketch": S, "k": P.k, "ordered_k": P.ordered_kmer_size,
-                       "parallelism": f"query-shard{world}"},
+                       "parallelism": f"query-shard{world}",
+                       "dist_backend": backend if world > 1 else None},
             "overlaps_per_step": total_ovl, "candidates_per_step": total_cand,
             "gbp_vs_gbp_per_sec": round(gbp * gbp / 2.0 * args.steps / elapsed, 3),
             "breakdown_ms": {k: round(v / args.steps, 2) for k, v in ms.items()},

@@ -146,6 +146,49 @@ def synth_reads(n_reads: int, read_len: int, genome_len: int, error_rate: float,
                    first_iid=1 + lo, starts=starts, strands=strands)
 
 
+_PAR = {}
+
+
+def _par_slice(lo_hi):
+    g = _PAR
+    return synth_reads(g["n"], g["len"], g["glen"], g["err"], seed=g["seed"],
+                       len_jitter=g["jit"], genome=g["genome"], read_range=lo_hi)
+
+
+def concat_read_sets(parts: list[ReadSet], first_iid: int) -> ReadSet:
+    lengths = np.concatenate([p.lengths for p in parts])
+    offsets = np.zeros(lengths.shape[0], dtype=np.uint64)
+    if lengths.shape[0] > 1:
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    return ReadSet(bases=np.concatenate([p.bases for p in parts]), offsets=offsets,
+                   lengths=lengths, quals=None, first_iid=first_iid,
+                   starts=np.concatenate([p.starts for p in parts]),
+                   strands=np.concatenate([p.strands for p in parts]))
+
+
+def synth_reads_parallel(n_reads: int, read_len: int, genome_len: int, error_rate: float,
+                         seed: int = 1, len_jitter: float = 0.0,
+                         read_range: tuple[int, int] | None = None,
+                         workers: int = 8) -> ReadSet:
+    """synth_reads over [lo, hi) in `workers` forked processes (read i depends only on
+    (seed, i), so the slices concatenate to exactly what one synth_reads call returns)."""
+    import multiprocessing as mp
+    lo, hi = read_range if read_range else (0, n_reads)
+    genome = random_genome(np.random.default_rng(seed), genome_len)
+    if workers <= 1 or hi - lo < 1024:
+        return synth_reads(n_reads, read_len, genome_len, error_rate, seed=seed,
+                           len_jitter=len_jitter, genome=genome, read_range=(lo, hi))
+    _PAR.update(n=n_reads, len=read_len, glen=genome_len, err=error_rate, seed=seed,
+                jit=len_jitter, genome=genome)
+    pieces = max(workers * 4, 1)
+    cuts = [(lo + (hi - lo) * i // pieces, lo + (hi - lo) * (i + 1) // pieces)
+            for i in range(pieces)]
+    with mp.get_context("fork").Pool(workers) as pool:
+        parts = pool.map(_par_slice, cuts)
+    _PAR.clear()
+    return concat_read_sets(parts, first_iid=1 + lo)
+
+
 def profile(name: str, seed: int = 1, **over) -> ReadSet:
     kw = dict(PROFILES[name])
     kw.update(over)

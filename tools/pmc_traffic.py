@@ -12,7 +12,11 @@ reported at half their bytes (r = 2, as MI355X_MICROARCH.md documents), random 1
 bytes of streaming stores exactly (calibrated 1.00) and counts a scattered 16-B store as
 the 32 B it writes (2.00), so it is taken as is.
 
-    python tools/pmc_traffic.py <tag>
+    python tools/pmc_traffic.py <tag> [the bench.py arguments of the profiled run]
+
+traffic.json's _method also records the workload key of the profiled run and the hash of
+the HIP sources it ran (bench.source_hash): bench.py uses the figures only for a run of the
+same workload on the same sources, and reports traffic: null otherwise.
 """
 import csv
 import glob
@@ -110,7 +114,12 @@ def main():
             if k in iss:
                 traffic[k]["issue"] = iss[k]
             f.write(f"{k},{n},{avg_ns.get(k, 0):.0f},{fk:.1f},{wk:.1f},{b:.0f}\n")
-    traffic["_method"] = {"hbm_bytes": "(r * FETCH_SIZE + WRITE_SIZE) KiB",
+    sys.path.insert(0, ROOT)
+    import bench
+    bargs = bench.parse_args(sys.argv[2:])
+    traffic["_method"] = {"workload": bench.Configs2(bargs, 0, 1, None, None).workload_key(),
+                          "src_sha": bench.source_hash(),
+                          "hbm_bytes": "(r * FETCH_SIZE + WRITE_SIZE) KiB",
                           "read_correction": {"default": 2.0, **READ_CORR},
                           "calibration": "profiles/calib_traffic.json (tools/calib_traffic.hip)",
                           "tag": tag}
