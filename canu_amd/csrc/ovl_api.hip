@@ -204,6 +204,8 @@ struct ovl_ctx {
     DBuf<unsigned long long> chits;
     DBuf<uint8_t> otmp;
     DBuf<uint64_t> ok64a, ok64b, dkey;       // -l orders
+    DBuf<uint64_t> hcnt, hbase;              // ovl_seed_hits: per-unit hit counts / bases
+    DBuf<uint4> hbuf;                        // ovl_seed_hits: one piece of the hit list
     DBuf<uint32_t> oa, ob, ucnt, useg;
     DBuf<Node> pool, pnodes[2];
     DBuf<PairRec> pairs[2];
@@ -871,13 +873,17 @@ static void release_find_buffers(ovl_ctx *c) {
   f.defer.release(); f.defer2.release(); f.okey.release(); f.oidx.release();
   f.okey2.release(); f.oidx2.release(); f.otmp.release(); f.pool.release();
   f.ok64a.release(); f.ok64b.release(); f.dkey.release(); f.oa.release(); f.ob.release();
-  f.ucnt.release(); f.useg.release();
+  f.ucnt.release(); f.useg.release(); f.hcnt.release(); f.hbase.release(); f.hbuf.release();
   f.rows.release(); f.rowdir.release(); f.deltas.release();
 }
+
+// HBM figures of the last index_window_cap call, for error messages
+static thread_local uint64_t g_cap_free = 0, g_cap_reserve = 0;
 
 static uint64_t index_window_cap(ovl_ctx *c) {
   uint64_t cap = 0xFFFFFFF0ull - 64 - c->h_skip.size();
   size_t fr = 0, tot = 0;
+  g_cap_free = g_cap_reserve = 0;
   if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
     const auto &f = c->fb;
     const uint64_t held = 2ull * c->d_tmpR.n * sizeof(Rec2) + 2ull * c->d_occ.n * 8 +
@@ -885,7 +891,12 @@ static uint64_t index_window_cap(ovl_ctx *c) {
                           (f.pool.n + f.pnodes[0].n + f.pnodes[1].n) * sizeof(Node) +
                           (f.pairs[0].n + f.pairs[1].n) * sizeof(PairRec) +
                           4ull * (f.rows.n + f.rowdir.n + f.deltas.n);
-    const uint64_t avail = fr + held, reserve = 64ull << 30;
+    // the search and extension buffers of the batch are sized by budget (up to ~64 GB on a
+    // 288 GB part): keep that much aside, or a fifth of a smaller device
+    const uint64_t avail = fr + held;
+    const uint64_t reserve = std::min<uint64_t>(64ull << 30, (uint64_t)tot / 5);
+    g_cap_free = avail;
+    g_cap_reserve = reserve;
     cap = std::min<uint64_t>(cap, avail > reserve ? (avail - reserve) / 112 : 0);
   }
   if (const char *e = getenv("OVL_TEST_INDEX_WINDOW_CAP"))
@@ -962,8 +973,10 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
     const uint64_t wcap = index_window_cap(c);
     if (!load_may_cut && windows > wcap)
       return fail(OVL_ERR_UNSUPPORTED, "hash batch %u-%u holds %llu k-mers, more than one index "
-                  "on this GPU (%llu); lower --hashstrings", bgn, e,
-                  (unsigned long long)windows, (unsigned long long)wcap);
+                  "on this GPU (%llu: %.1f GB free or held by this context, %.1f GB kept for "
+                  "the search buffers); lower --hashstrings", bgn, e,
+                  (unsigned long long)windows, (unsigned long long)wcap, g_cap_free / 1e9,
+                  g_cap_reserve / 1e9);
     const uint64_t tw = std::min(target, wcap);
     uint32_t eb = e;
     if (tw < windows) {
@@ -1819,8 +1832,9 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
   // buffer of at most 256 M hits (4 GB), in pieces of whole units
   const uint64_t WIN_BUDGET = 512ull << 20, HIT_BUF = 256ull << 20;
   auto &fb = c->fb;
-  DBuf<uint64_t> ucnt, ubase;
-  DBuf<uint4> hbuf;
+  // kept in the context (grow-only): a repeated call allocates nothing
+  DBuf<uint64_t> &ucnt = fb.hcnt, &ubase = fb.hbase;
+  DBuf<uint4> &hbuf = fb.hbuf;
   uint64_t total = 0, copied = 0;
   float ms_tot = 0;
   const uint32_t nu = (uint32_t)units.size();
@@ -1866,18 +1880,26 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
     std::vector<uint64_t> cnt(nb);
     HIPC(hipMemcpyAsync(cnt.data(), ucnt.p, 8ull * nb, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    // write pass, in pieces of whole units that fit the hit buffer
+    // write pass, in pieces of whole units that fit the hit buffer: every unit's base
+    // within its piece is computed once (one host pass over the batch) and uploaded once;
+    // the hit buffer only grows (one allocation at the largest piece)
+    std::vector<uint64_t> base(nb, 0);
+    std::vector<uint32_t> cuts{0};
+    uint64_t hmax = 1;
     for (uint32_t p0 = 0; p0 < nb;) {
       uint32_t p1 = p0;
       uint64_t h = 0;
-      while (p1 < nb && (h + cnt[p1] <= HIT_BUF || p1 == p0)) h += cnt[p1++];
-      std::vector<uint64_t> base(nb, 0);
-      uint64_t a2 = 0;
-      for (uint32_t i = p0; i < p1; i++) { base[i] = a2; a2 += cnt[i]; }
-      if (hbuf.alloc(std::max<uint64_t>(a2, 1)))
-        return fail(OVL_ERR_OOM, "seed-hit list (%llu hits)", (unsigned long long)a2);
-      HIPC(hipMemcpyAsync(ubase.p, base.data(), 8ull * nb, hipMemcpyHostToDevice, s));
-      HA.unit_base = ubase.p;
+      while (p1 < nb && (h + cnt[p1] <= HIT_BUF || p1 == p0)) { base[p1] = h; h += cnt[p1++]; }
+      hmax = std::max<uint64_t>(hmax, h);
+      cuts.push_back(p1);
+      p0 = p1;
+    }
+    if (hbuf.grow(hmax))
+      return fail(OVL_ERR_OOM, "seed-hit list (%llu hits)", (unsigned long long)hmax);
+    HIPC(hipMemcpyAsync(ubase.p, base.data(), 8ull * nb, hipMemcpyHostToDevice, s));
+    for (size_t pc = 0; pc + 1 < cuts.size(); pc++) {
+      const uint32_t p0 = cuts[pc], p1 = cuts[pc + 1];
+      const uint64_t a2 = base[p1 - 1] + cnt[p1 - 1];
       HA.out = hbuf.p;
       HA.units = fb.units[0].p + p0;
       HA.rbase = fb.rbase.p + p0;
@@ -1892,7 +1914,6 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
       }
       HIPC(hipStreamSynchronize(s));
       total += a2;
-      p0 = p1;
     }
     HIPC(hipEventRecord(c->ev[3], s));
     HIPC(hipStreamSynchronize(s));

@@ -19,6 +19,11 @@ import numpy as np
 # b > a >= lo (Find_Overlaps.C:328 keeps targets with a larger ID), so its rank indexes
 # reads lo..n only: the same records and counters, a smaller index, and occurrence lists
 # (chain work) shortened by (n - lo) / n.
+# One exception: under -l (Frag_Olap_Limit) the order a query's targets are processed in
+# comes from String_Olap_Space slots that hash the target's number WITHIN the hash batch
+# (Find_Overlaps.C:158-200), so a shard indexing lo..n reproduces the reference's
+# `-h lo-n -r lo-hi` job exactly, not `-h 1-n`: once a limit is reached, other overlaps may
+# be kept.  canu never passes -l to overlapInCore; bench.py does not use it.
 SHARD_COSTS = {"index_per_read": 37.0 / 50_000, "probe_per_query": 37.0 / 50_000,
                "chain_per_query": 87.0 / 50_000, "pair": 1146.0 / (50_000 ** 2 / 2)}
 

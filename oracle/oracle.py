@@ -351,13 +351,15 @@ def run_oracle_driver(rs, params: dict, hash_range=(1, UINT32_MAX), ref_range=(1
 
 def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
                   skip_kmers=None, minkmers: bool = False, extra=None, workdir=None,
-                  with_time=False, batching: dict | None = None, with_stats=False):
+                  with_time=False, batching: dict | None = None, with_stats=False,
+                  libs=None):
     """Run the reference overlapInCore (built from its sources) on `rs`.
 
     By default the whole read set is one hash batch and one ref range, so every pair (a<b)
     is searched once, as the reference's full -h/-r ranges do.  `batching` instead passes
     the hash-batch options as given ({"hashstrings": .., "hashdatalen": .., "hashload": ..},
-    missing ones at the reference defaults, overlapInCore.H:447-450)."""
+    missing ones at the reference defaults, overlapInCore.H:447-450).  `libs` (one library
+    number >= 1 per read) spreads the reads over gkpStore libraries for -H / -R."""
     from canu_amd.synth import write_reads_file  # input writer only
     if not reference_available():
         raise FileNotFoundError(REF_BIN)
@@ -385,6 +387,10 @@ def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
                 for i, k in enumerate(skip_kmers):
                     f.write(f">{i}\n{k if isinstance(k, str) else k.decode()}\n")
             args += ["--skip", sk]
+        if libs is not None:
+            lp = os.path.join(wd, "libs.bin")
+            np.ascontiguousarray(libs, dtype="<u4").tofile(lp)
+            args += ["--libs", lp]
         if extra:
             args += list(extra)
         t0 = time.time()

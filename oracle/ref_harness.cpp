@@ -90,6 +90,7 @@ int main(int argc, char **argv) {
   bool        gkpOnly  = false;   //  build <workdir>/ref.gkpStore and stop (mhapConvert's -G)
   const char *skipPath = NULL;
   const char *statPath = NULL;    //  -s: main()'s statistics text (overlapInCore.C:569-591)
+  const char *libsPath = NULL;    //  --libs: one uint32 library number (1..) per read
 
   for (int arg = 4; arg < argc; arg++) {
     const char *a = argv[arg];
@@ -113,6 +114,9 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-t"))            G.Num_PThreads = strtoull(argv[++arg], NULL, 10);
     else if (!strcmp(a, "-h"))            AS_UTL_decodeRange(argv[++arg], G.bgnHashID, G.endHashID);
     else if (!strcmp(a, "-r"))            AS_UTL_decodeRange(argv[++arg], G.bgnRefID, G.endRefID);
+    else if (!strcmp(a, "-H"))            AS_UTL_decodeRange(argv[++arg], G.minLibToHash, G.maxLibToHash);
+    else if (!strcmp(a, "-R"))            AS_UTL_decodeRange(argv[++arg], G.minLibToRef, G.maxLibToRef);
+    else if (!strcmp(a, "--libs"))        libsPath = argv[++arg];
     else if (!strcmp(a, "--skip"))        skipPath = argv[++arg];
     else if (!strcmp(a, "--time"))        timeIt = true;
     else if (!strcmp(a, "--gkp-only"))    gkpOnly = true;
@@ -146,9 +150,27 @@ int main(int argc, char **argv) {
   mkdir(work.c_str(), 0755);
   std::string gkp = work + "/ref.gkpStore";
 
+  //  reads may be spread over several libraries (-H / -R filter on gkRead_libraryID())
+  std::vector<uint32_t> rlib(nreads, 1);
+  if (libsPath) {
+    FILE *L = fopen(libsPath, "rb");
+    if (!L || (nreads && fread(rlib.data(), 4, nreads, L) != nreads)) die("bad --libs file");
+    fclose(L);
+  }
+  uint32_t nlibs = 1;
+  for (uint32_t i = 0; i < nreads; i++) {
+    if (rlib[i] < 1) die("library numbers start at 1");
+    nlibs = rlib[i] > nlibs ? rlib[i] : nlibs;
+  }
+
   {
     gkStore   *store = gkStore::gkStore_open(gkp.c_str(), gkStore_create);
-    gkLibrary *lib   = store->gkStore_addEmptyLibrary("synthetic");
+    std::vector<gkLibrary *> libs(nlibs + 1, NULL);
+    for (uint32_t l = 1; l <= nlibs; l++) {
+      char ln[32];
+      snprintf(ln, sizeof(ln), l == 1 ? "synthetic" : "synthetic%u", l);
+      libs[l] = store->gkStore_addEmptyLibrary(ln);
+    }
     uint32_t   maxl  = 0;
     for (uint32_t i = 0; i < nreads; i++) maxl = lens[i] > maxl ? lens[i] : maxl;
     std::vector<char> S(maxl + 1), Q(maxl + 1);
@@ -164,6 +186,7 @@ int main(int argc, char **argv) {
         Q[0] = 0;
       }
       snprintf(H, sizeof(H), "read%u", i + 1);
+      gkLibrary  *lib = libs[rlib[i]];
       gkRead     *nr = store->gkStore_addEmptyRead(lib);
       gkReadData *nd = nr->gkRead_encodeSeqQlt(H, S.data(), Q.data(), lib->gkLibrary_defaultQV());
       store->gkStore_stashReadData(nr, nd);

@@ -188,3 +188,57 @@ def test_gpu_driver_load_cut_within_window_cap(built, monkeypatch):
     monkeypatch.setenv("OVL_TEST_INDEX_WINDOW_CAP", "20000")
     with pytest.raises(OvlError, match="load limit"):
         run()
+
+
+def _lib_case():
+    """Reads spread over three gkpStore libraries, -H 1-2 (hash libraries 1 and 2 only) and
+    -R 2-3 (search from libraries 2 and 3 only), small hash batches (Build_Hash_Index.C:
+    500-503 / :554-556, Process_Overlaps.C:108-109): a skipped read still counts towards
+    --hashstrings, so the filters move batch ends."""
+    rs = synth_reads(n_reads=150, read_len=2500, genome_len=45_000, error_rate=0.02, seed=26,
+                     len_jitter=0.3)
+    libs = (np.random.default_rng(26).integers(1, 4, size=rs.nreads)).astype(np.uint32)
+    return rs, libs, dict(hashstrings=40), 4, ["-H", "1-2", "-R", "2-3"]
+
+
+@pytest.mark.skipif(not oracle.reference_available(), reason="oracle/_ref/oic_ref not built")
+def test_reference_library_filters_take_effect():
+    """CPU: the reference run with -H / -R differs from the unfiltered one, and no record
+    pairs two reads the filters exclude from both roles."""
+    rs, libs, batch, threads, extra = _lib_case()
+    P = _params()
+    ref = oracle.run_reference(rs, P, threads=threads, hash_bits=22, batching=batch,
+                               libs=libs, extra=extra)
+    plain = oracle.run_reference(rs, P, threads=threads, hash_bits=22, batching=batch)
+    assert 0 < ref.shape[0] < plain.shape[0]
+    la, lb = libs[ref["a"] - 1], libs[ref["b"] - 1]
+    # one read of each pair was hashed (library 1-2), the other searched (library 2-3)
+    ok = ((la <= 2) & (lb >= 2)) | ((lb <= 2) & (la >= 2))
+    assert ok.all()
+
+
+@pytest.mark.gpu
+def test_gpu_driver_library_filters(built):
+    """ovl_set_read_libraries + -H / -R through ovl_overlap_driver: records and every -s
+    counter equal the reference's, run on a gkpStore with the same libraries."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    rs, libs, batch, threads, extra = _lib_case()
+    P = _params()
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=batch["hashstrings"], Num_PThreads=threads,
+                      minLibToHash=1, maxLibToHash=2, minLibToRef=2, maxLibToRef=3).finalize()
+    oic = OverlapInCore(O, device=0)
+    try:
+        oic.load_reads(rs)
+        oic.set_read_libraries(libs)
+        got = oic.fetch(oic.overlap_driver())
+        st = oic.stats()
+    finally:
+        oic.close()
+    if not oracle.reference_available():
+        pytest.skip("oracle/_ref/oic_ref not built")
+    ref, rst = oracle.run_reference(rs, P, threads=threads, hash_bits=22, batching=batch,
+                                    libs=libs, extra=extra, with_stats=True)
+    assert got.shape == ref.shape and np.array_equal(got, ref)
+    for rk, ok in STAT_KEYS:
+        assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
