@@ -43,6 +43,11 @@ def main() -> None:
     ap.add_argument("--read-error", type=float, default=0.05)
     ap.add_argument("--sensitivity", default="normal")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--weighting", choices=("canu", "none"), default="canu",
+                    help="canu: --repeat-weight 0.9 --repeat-idf-scale 10 with a -f table "
+                         "(OverlapMhap.pm:382); none: MHAP 1.x unweighted sketches")
+    ap.add_argument("--freq-kmers", type=int, default=100_000,
+                    help="-f table size (16-mers sampled from the reads, graded fractions)")
     ap.add_argument("--cpu-sample-reads", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -94,8 +99,14 @@ def main() -> None:
     total_bases = int(lengths.sum(dtype=np.uint64))
 
     P = MhapParameters.sensitivity(args.sensitivity)
+    freq = None
+    if args.weighting == "canu":
+        P.canu_weighting()
+        freq = freq_table(genome, args.freq_kmers, P.k, args.seed)
     m = Mhap(P, device=local)
     m.load_reads_device(1, bases.data_ptr(), d_offsets.data_ptr(), lengths)
+    if freq is not None:
+        m.set_kmer_frequencies(*freq)
     H, S = P.num_hashes, P.ordered_sketch_size
     if world > 1:
         mh_l = torch.empty((hi - lo, H), dtype=torch.int32, device=dev)
@@ -178,7 +189,7 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, P)
+        cpu = cpu_baseline(args, P, freq)
 
     if rank == 0:
         line = {
@@ -191,6 +202,10 @@ def main() -> None:
                                    "all-vs-all", "reads": n, "read_len": args.read_len,
                        "coverage": args.coverage, "read_error": args.read_error,
                        "sensitivity": args.sensitivity, "num_hashes": H,
+                       "weighting": (f"canu (--repeat-weight 0.9 --repeat-idf-scale 10 "
+                                     f"--filter-threshold {P.filter_threshold}, -f table of "
+                                     f"{args.freq_kmers} 16-mers)") if freq is not None
+                                    else "none (unweighted)",
                        "ordered_sketch": S, "k": P.k, "ordered_k": P.ordered_kmer_size,
                        "parallelism": f"query-shard{world}",
                        "dist_backend": backend if world > 1 else None},
@@ -205,7 +220,22 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, P) -> dict | None:
+def freq_table(genome, n: int, k: int, seed: int):
+    """A -f table the way canu's is shaped (Meryl.pm:699-716: k-mer, fraction; both strands):
+    n/2 k-mers drawn from the genome with fractions graded from the filter threshold up."""
+    rng = np.random.default_rng(seed + 77)
+    g = genome.tobytes().decode()
+    comp = str.maketrans("ACGT", "TGCA")
+    km, fr = [], []
+    for j, p in enumerate(rng.integers(0, len(g) - k, size=max(n // 2, 0))):
+        m = g[int(p):int(p) + k]
+        f = 5e-6 * 1.3 ** (j % 24)
+        km += [m, m.translate(comp)[::-1]]
+        fr += [f, f]
+    return km, np.array(fr, dtype=np.float64)
+
+
+def cpu_baseline(args, P, freq=None) -> dict | None:
     """The numpy restatement (oracle/mhap_oracle.py, one core) on a bounded sample of the
     same workload: fewer reads, same read length / error / coverage."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -218,7 +248,7 @@ def cpu_baseline(args, P) -> dict | None:
     gl = int(ns * args.read_len / args.coverage)
     rs = synth_reads(ns, args.read_len, gl, args.read_error, seed=args.seed + 1000)
     t0 = time.perf_counter()
-    rec = mhap_oracle.run(rs, P.as_oracle())
+    rec = mhap_oracle.run(rs, P.as_oracle(), freq=freq)
     secs = time.perf_counter() - t0
     return {"value": round(len(rec) / secs, 2), "unit": "overlaps/s", "cores": 1,
             "kind": "port",

@@ -225,6 +225,167 @@ __global__ void __launch_bounds__(256) k_mh_sketch(SketchArgs A) {
   }
 }
 
+// ---- weighted MinHash (MHAP 2.x tf-idf repeat weighting, restated; canu_mhap.h) --------
+// Each distinct k-mer of a read counts once with weight w >= 1 (w draws of its xorshift64
+// chain per hash function), so the reads' k-mers are first made distinct and counted:
+//   k_mh_kmer_keys  one block per read: (read index << 2k | canonical code) per valid k-mer
+//                   (a sentinel for the rest), RKK consecutive positions per thread
+//   radix sort      of the batch's keys (hipcub): each read's k-mers contiguous, equal
+//                   k-mers adjacent -- tf is a run length
+//   k_mh_sketch_w   one block per read over its sorted run: run starts only, weight from
+//                   the run length and the -f table, then the sketch loop of k_mh_sketch
+//                   with w draws per slot and function
+constexpr int RKK = 16;           // positions per thread in k_mh_kmer_keys
+constexpr int RKW = 16;           // distinct k-mers per thread per round in k_mh_sketch_w
+
+struct KeyArgs {
+  const uint8_t *bases;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint32_t r0, nreads;
+  int32_t k;
+  const uint64_t *koff;         // per read of the batch: its first key
+  uint64_t sentinel;            // key of an invalid position (sorts after every real key)
+  uint64_t *keys;
+  unsigned long long *kmers;
+};
+
+__global__ void __launch_bounds__(256) k_mh_kmer_keys(KeyArgs A) {
+  const uint32_t ri = blockIdx.x, r = A.r0 + ri;
+  const int32_t k = A.k;
+  const uint8_t *s = A.bases + A.off[r];
+  const int32_t L = (int32_t)A.len[r];
+  const int32_t npos = L - k + 1;
+  uint64_t *out = A.keys + A.koff[ri];
+  const uint64_t hi = (uint64_t)ri << (2 * k);
+  unsigned long long nk = 0;
+  for (int32_t base = 0; base < npos; base += 256 * RKK) {
+    const int32_t p0 = base + (int32_t)threadIdx.x * RKK;
+    if (p0 >= npos) continue;
+    Roller R(k);
+    for (int32_t i = 0; i < k - 1; i++) R.push(base_code(s[p0 + i]));
+#pragma unroll
+    for (int i = 0; i < RKK; i++) {
+      const int32_t p = p0 + i;
+      if (p < npos) {
+        const bool ok = R.push(base_code(s[p + k - 1]));
+        out[p] = ok ? (hi | R.canon()) : A.sentinel;
+        nk += ok;
+      }
+    }
+  }
+  if (A.kmers) {
+    for (int s2 = 32; s2 > 0; s2 >>= 1) nk += __shfl_xor(nk, s2);
+    if ((threadIdx.x & 63) == 0 && nk) atomicAdd(A.kmers, nk);
+  }
+}
+
+struct WSketchArgs {
+  const uint64_t *keys;         // sorted
+  uint64_t nkeys;
+  uint32_t r0, nreads;
+  int32_t k, H;
+  const uint64_t *fcodes;       // -f k-mers (canonical, sorted) ...
+  const double *fmult;          // ... and their multipliers m(c)
+  uint32_t nf;
+  double dmult;                 // m(c) of every other k-mer
+  int32_t no_tf;
+  int32_t *minhash;             // [read][H]
+};
+
+__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t n, uint64_t v) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Stage 1, weighted (oracle: mhap_oracle.sketch_weighted)
+__global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
+  extern __shared__ int32_t s_min[];               // [4 waves][H]
+  __shared__ uint64_t s_rng[2];
+  const uint32_t ri = blockIdx.x, r = A.r0 + ri;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int32_t H = A.H, k = A.k;
+  const uint64_t cmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1);
+  for (int32_t j = tid; j < 4 * H; j += 256) s_min[j] = I32MAX;
+  if (tid == 0) {
+    s_rng[0] = lower_bound_u64(A.keys, A.nkeys, (uint64_t)ri << (2 * k));
+    s_rng[1] = lower_bound_u64(A.keys, A.nkeys, (uint64_t)(ri + 1) << (2 * k));
+  }
+  __syncthreads();
+  const uint64_t s0 = s_rng[0], s1 = s_rng[1];
+  int32_t *wm = s_min + wave * H;
+  for (uint64_t base = s0; base < s1; base += 256 * RKW) {
+    const uint64_t p0 = base + (uint64_t)tid * RKW;
+    uint32_t XL[RKW], XH[RKW];
+    int32_t W[RKW];
+    uint32_t vm = 0;
+#pragma unroll
+    for (int i = 0; i < RKW; i++) {
+      XL[i] = XH[i] = 0;
+      W[i] = 0;
+      const uint64_t p = p0 + i;
+      if (p < s1) {
+        const uint64_t key = A.keys[p];
+        if (p == s0 || A.keys[p - 1] != key) {           // a run start: a distinct k-mer
+          uint64_t e = p + 1;
+          while (e < s1 && A.keys[e] == key) e++;
+          const uint64_t c = key & cmask;
+          double m = A.dmult;
+          if (A.nf) {
+            const uint64_t q = lower_bound_u64(A.fcodes, A.nf, c);
+            if (q < A.nf && A.fcodes[q] == c) m = A.fmult[q];
+          }
+          const double tf = A.no_tf ? 1.0 : (double)(e - p);
+          const double wf = floor(tf * m + 0.5);
+          W[i] = wf < 1.0 ? 1 : (int32_t)wf;
+          const uint64_t x = splitmix64(c);
+          XL[i] = (uint32_t)x;
+          XH[i] = (uint32_t)(x >> 32);
+          vm |= 1u << i;
+        }
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(vm != 0) == 0) continue;
+    // empty slots take a copy of a live slot's chain and weight (min is idempotent)
+    {
+      uint32_t l0 = 0, h0 = 0;
+      int32_t w0 = 0;
+#pragma unroll
+      for (int i = RKW - 1; i >= 0; i--)
+        if ((vm >> i) & 1u) { l0 = XL[i]; h0 = XH[i]; w0 = W[i]; }
+#pragma unroll
+      for (int i = 0; i < RKW; i++)
+        if (!((vm >> i) & 1u)) { XL[i] = l0; XH[i] = h0; W[i] = w0; }
+    }
+    const bool live = vm != 0;
+    for (int32_t j = 0; j < H; j++) {
+      int32_t m = I32MAX;
+#pragma unroll
+      for (int i = 0; i < RKW; i++) {
+        for (int32_t t = 0; t < W[i]; t++) {
+          xs64(XL[i], XH[i]);
+          const int32_t v = (int32_t)XL[i];
+          m = v < m ? v : m;
+        }
+      }
+      m = live ? m : I32MAX;
+      m = wave_min(m);
+      if (lane == 0 && m < wm[j]) wm[j] = m;
+    }
+  }
+  __syncthreads();
+  for (int32_t j = tid; j < H; j += 256) {
+    int32_t m = s_min[j];
+    for (int w = 1; w < 4; w++) m = s_min[w * H + j] < m ? s_min[w * H + j] : m;
+    A.minhash[(size_t)r * H + j] = m;
+  }
+}
+
 struct OrderedArgs {
   const uint8_t *bases;
   const uint64_t *off;
@@ -690,6 +851,14 @@ struct mhap_ctx {
   MBuf<uint32_t> d_len;
   MBuf<uint64_t> filter;
   uint32_t nfilter = 0;
+  // repeat weighting (mhap_set_kmer_frequencies): weighted sketch when repeat_weight >= 0
+  mhap_weighting W{-1.0, 10.0, 1e-5, 0};
+  bool weighted = false;
+  MBuf<uint64_t> fcodes, wkeys, wkeys2;
+  MBuf<double> fmult;
+  uint32_t nf = 0;
+  double dmult = 1.0;
+  MBuf<uint8_t> wsort_tmp;
   MBuf<int32_t> minhash;
   MBuf<uint64_t> ordered;
   MBuf<uint32_t> ocount;
@@ -851,6 +1020,144 @@ int mhap_set_filter_kmers(mhap_ctx *c, const char *kmers, uint64_t n) {
   return M_OK;
 }
 
+void mhap_weighting_init(mhap_weighting *w) {
+  w->repeat_weight = -1.0;
+  w->repeat_idf_scale = 10.0;
+  w->filter_threshold = 1e-5;
+  w->no_tf = 0;
+}
+
+static bool kmer_code(const char *km, uint32_t k, uint64_t *canon) {
+  uint64_t f = 0, r = 0;
+  for (uint32_t t = 0; t < k; t++) {
+    const char ch = km[t] | 0x20;
+    const uint64_t b = ch == 'a' ? 0 : ch == 'c' ? 1 : ch == 'g' ? 2 : ch == 't' ? 3 : 9;
+    if (b > 3) return false;
+    f = (f << 2) | b;
+    r |= (3 - b) << (2 * t);
+  }
+  *canon = f < r ? f : r;
+  return true;
+}
+
+int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *fractions,
+                              uint64_t n, const mhap_weighting *w) {
+  if (!c || !w) return mfail(M_STATE, "null argument");
+  if (n && (!kmers || !fractions)) return mfail(M_BAD_PARAM, "null k-mers / fractions");
+  if (!(w->filter_threshold > 0.0) || !(w->repeat_idf_scale >= 1.0))
+    return mfail(M_BAD_PARAM, "filter_threshold must be > 0 and repeat_idf_scale >= 1");
+  const uint32_t k = c->P.k;
+  if (w->repeat_weight >= 0.0 && 2 * k > 56)
+    return mfail(M_BAD_PARAM, "weighted sketches need k <= 28 (read index beside the code)");
+  c->W = *w;
+  c->weighted = w->repeat_weight >= 0.0;
+  // the -f k-mers at or above the threshold, canonical (both strands are listed), the
+  // largest fraction per k-mer
+  std::vector<std::pair<uint64_t, double>> F;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t cc;
+    if (!kmer_code(kmers + i * k, k, &cc)) continue;
+    if (!(fractions[i] >= w->filter_threshold)) continue;
+    F.emplace_back(cc, fractions[i]);
+  }
+  std::sort(F.begin(), F.end());
+  std::vector<uint64_t> codes;
+  std::vector<double> fr;
+  for (size_t i = 0; i < F.size(); i++) {
+    if (!codes.empty() && codes.back() == F[i].first) {
+      fr.back() = std::max(fr.back(), F[i].second);
+      continue;
+    }
+    codes.push_back(F[i].first);
+    fr.push_back(F[i].second);
+  }
+  MHC(hipSetDevice(c->device));
+  if (!c->weighted) {                 // MHAP 1.x: the repeats are dropped
+    if (c->filter.alloc(codes.size())) return mfail(M_OOM, "filter");
+    if (!codes.empty())
+      MHC(hipMemcpy(c->filter.p, codes.data(), 8 * codes.size(), hipMemcpyHostToDevice));
+    c->nfilter = (uint32_t)codes.size();
+    c->nf = 0;
+    return M_OK;
+  }
+  c->nfilter = 0;
+  // multipliers m(c) = r + (1 - r) * (1 + (X - 1) * (idf - idf_min) / (idf_max - idf_min))
+  const double r = w->repeat_weight, X = w->repeat_idf_scale;
+  const double idf_max = log(1.0 / w->filter_threshold);
+  double idf_min = idf_max;
+  std::vector<double> idf(codes.size());
+  for (size_t i = 0; i < codes.size(); i++) {
+    idf[i] = log(1.0 / fr[i]);
+    idf_min = std::min(idf_min, idf[i]);
+  }
+  auto mult = [&](double v) {
+    if (r >= 1.0 || codes.empty()) return 1.0;
+    const double sc = idf_max > idf_min ? 1.0 + (X - 1.0) * (v - idf_min) / (idf_max - idf_min) : X;
+    return r + (1.0 - r) * sc;
+  };
+  std::vector<double> m(codes.size());
+  for (size_t i = 0; i < codes.size(); i++) m[i] = mult(idf[i]);
+  c->dmult = mult(idf_max);
+  if (c->fcodes.alloc(codes.size()) || c->fmult.alloc(codes.size()))
+    return mfail(M_OOM, "k-mer frequency table");
+  if (!codes.empty()) {
+    MHC(hipMemcpy(c->fcodes.p, codes.data(), 8 * codes.size(), hipMemcpyHostToDevice));
+    MHC(hipMemcpy(c->fmult.p, m.data(), 8 * m.size(), hipMemcpyHostToDevice));
+  }
+  c->nf = (uint32_t)codes.size();
+  return M_OK;
+}
+
+// The weighted MinHash of reads r0 .. r0+nr-1 in batches of <= WKEY_BUDGET positions: keys,
+// radix sort, sketch (the ordered sketch is the caller's, unweighted as in the jar).
+static int sketch_weighted(mhap_ctx *c, uint32_t r0, uint32_t nr) {
+  hipStream_t s = c->stream;
+  const uint32_t k = c->P.k;
+  const uint64_t WKEY_BUDGET = 1ull << 30;                  // 8 GB of keys per buffer
+  const uint32_t idx_bits = 64 - 2 * k;
+  const uint64_t max_reads = idx_bits >= 32 ? 0xFFFFFFF0ull : (1ull << idx_bits) - 2;
+  for (uint32_t a = 0; a < nr;) {
+    std::vector<uint64_t> koff;
+    uint64_t tot = 0;
+    uint32_t b = a;
+    while (b < nr && b - a < max_reads && b - a < (1u << 20)) {
+      const int64_t np = (int64_t)c->h_len[r0 + b] - (int64_t)k + 1;
+      const uint64_t add = np > 0 ? (uint64_t)np : 0;
+      if (tot + add > WKEY_BUDGET && b > a) break;
+      koff.push_back(tot);
+      tot += add;
+      b++;
+    }
+    const uint32_t nb = b - a;
+    const uint32_t end_bit = 2 * k + (uint32_t)std::max<int>(1, 64 - __builtin_clzll((uint64_t)nb + 1));
+    const uint64_t sentinel = end_bit >= 64 ? ~0ull : ((1ull << end_bit) - 1);
+    MBuf<uint64_t> d_koff;
+    if (d_koff.alloc(nb) || c->wkeys.alloc(std::max<uint64_t>(tot, 1)) ||
+        c->wkeys2.alloc(std::max<uint64_t>(tot, 1)))
+      return mfail(M_OOM, "weighted-sketch keys (%llu)", (unsigned long long)tot);
+    MHC(hipMemcpyAsync(d_koff.p, koff.data(), 8ull * nb, hipMemcpyHostToDevice, s));
+    KeyArgs KA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)k, d_koff.p, sentinel,
+               c->wkeys.p, c->kctr.p};
+    hipLaunchKernelGGL(k_mh_kmer_keys, dim3(nb), dim3(256), 0, s, KA);
+    MHC(hipGetLastError());
+    size_t tb = 0;
+    // key counts can pass 2^31: the 64-bit-count form of the sort
+    MHC(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
+                                          (int)end_bit, s));
+    if (c->wsort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
+    MHC(hipcub::DeviceRadixSort::SortKeys(c->wsort_tmp.p, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
+                                          (int)end_bit, s));
+    WSketchArgs WA{c->wkeys2.p, tot, r0 + a, nb, (int32_t)k, (int32_t)c->P.num_hashes,
+                   c->nf ? c->fcodes.p : nullptr, c->nf ? c->fmult.p : nullptr, c->nf,
+                   c->dmult, c->W.no_tf, c->minhash.p};
+    hipLaunchKernelGGL(k_mh_sketch_w, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
+    MHC(hipGetLastError());
+    MHC(hipStreamSynchronize(s));                           // d_koff is freed here
+    a = b;
+  }
+  return M_OK;
+}
+
 int mhap_sketch(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
   if (!c->d_bases || !c->d_off)
@@ -863,13 +1170,19 @@ int mhap_sketch(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   MHC(hipMemsetAsync(c->kctr.p, 0, 8, s));
   MHC(hipEventRecord(c->ev[0], s));
   // one block per read; launches of <= 65535 * 16 reads keep grids modest
+  if (c->weighted) {
+    const int rc = sketch_weighted(c, r0, nr);
+    if (rc) return rc;
+  }
   for (uint32_t a = 0; a < nr; a += 1u << 20) {
     const uint32_t nb = std::min<uint32_t>(nr - a, 1u << 20);
-    SketchArgs SA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.k,
-                  (int32_t)c->P.num_hashes, c->nfilter ? c->filter.p : nullptr, c->nfilter,
-                  c->minhash.p, c->kctr.p};
-    hipLaunchKernelGGL(k_mh_sketch, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, SA);
-    MHC(hipGetLastError());
+    if (!c->weighted) {
+      SketchArgs SA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.k,
+                    (int32_t)c->P.num_hashes, c->nfilter ? c->filter.p : nullptr, c->nfilter,
+                    c->minhash.p, c->kctr.p};
+      hipLaunchKernelGGL(k_mh_sketch, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, SA);
+      MHC(hipGetLastError());
+    }
     OrderedArgs OA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.ordered_k,
                    (int32_t)c->P.ordered_sketch, c->ordered.p, c->ocount.p};
     hipLaunchKernelGGL(k_mh_ordered, dim3(nb), dim3(256), 0, s, OA);

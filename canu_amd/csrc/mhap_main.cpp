@@ -17,9 +17,11 @@
 // read lengths and the three sketch arrays of include/canu_mhap.h.
 //
 // The jar's tf-idf repeat weighting (--repeat-weight, --repeat-idf-scale,
-// --filter-threshold) is not implemented: those options are accepted with a warning and
-// the sketch is unweighted; -f k-mers at or above --filter-threshold are left out of the
-// sketch.  --no-tf / --supress-noise are rejected.  See DESIGN.md.
+// --filter-threshold, --no-tf, -f with its fractions) is restated from the published MHAP
+// 2.x algorithm in include/canu_mhap.h (mhap_weighting); parity with the jar itself is
+// unpinned.  Without --repeat-weight (or with a negative one) the sketch is
+// MHAP 1.x's unweighted one and -f k-mers at or above --filter-threshold are left out.
+// --supress-noise is rejected.
 #include <zlib.h>
 
 #include <algorithm>
@@ -56,7 +58,8 @@ int usage(const char *prog) {
           "  -k n  --num-hashes n  --num-min-matches n  --threshold x\n"
           "  --ordered-sketch-size n  --ordered-kmer-size n  --min-olap-length n\n"
           "  --num-threads n (ignored: one GPU)   CANU_MHAP_DEVICE picks the GPU\n"
-          "  --repeat-weight x  --repeat-idf-scale x  --filter-threshold x  (accepted, unweighted)\n",
+          "  --repeat-weight x  --repeat-idf-scale x  --filter-threshold x  --no-tf\n"
+          "                                      (tf-idf repeat weighting, canu_mhap.h)\n",
           prog, prog);
   return 1;
 }
@@ -93,20 +96,18 @@ bool read_fasta(const char *path, std::vector<uint8_t> &bases, std::vector<uint6
 
 // canu's frequentMers.ignore.gz (Meryl.pm:699-712): a count line, then "kmer<TAB>fraction"
 // for both orientations.  gzopen reads plain files too.
-bool read_filter(const char *path, uint32_t k, double threshold, std::string &kmers,
-                 uint64_t &n) {
+// The -f file (Meryl.pm:699-716): a count line, then "kmer<TAB>fraction" lines.
+bool read_filter(const char *path, uint32_t k, std::string &kmers, std::vector<double> &fr) {
   gzFile G = gzopen(path, "rb");
   if (!G) return false;
   char buf[4096];
-  n = 0;
   while (gzgets(G, buf, sizeof buf)) {
     char *tab = strchr(buf, '\t');
     if (!tab) continue;                          // the count line
     const size_t L = (size_t)(tab - buf);
-    const double frac = strtod(tab + 1, nullptr);
-    if (L != k || frac < threshold) continue;
+    if (L != k) continue;
     kmers.append(buf, L);
-    n++;
+    fr.push_back(strtod(tab + 1, nullptr));
   }
   gzclose(G);
   return true;
@@ -188,8 +189,8 @@ int main(int argc, char **argv) {
   mhap_params_init(&P);
   const char *fasta = nullptr, *qpath = nullptr, *spath = nullptr, *fpath = nullptr;
   bool no_self = false;
-  double filter_threshold = 0.0;
-  std::vector<std::string> ignored;
+  mhap_weighting W;
+  mhap_weighting_init(&W);
   for (int i = 1; i < argc; i++) {
     const std::string a = argv[i];
     const bool has = i + 1 < argc;
@@ -208,14 +209,12 @@ int main(int argc, char **argv) {
     else if (a == "--ordered-kmer-size") P.ordered_k = (uint32_t)atoi(num("--ordered-kmer-size"));
     else if (a == "--min-olap-length") P.min_olap = atoi(num("--min-olap-length"));
     else if (a == "--num-threads") num("--num-threads");
-    else if (a == "--filter-threshold") {
-      filter_threshold = atof(num("--filter-threshold"));
-      ignored.push_back(a);
-    } else if (a == "--repeat-weight" || a == "--repeat-idf-scale") {
-      num(a.c_str());
-      ignored.push_back(a);
-    } else if (a == "--supress-noise" || a == "--no-tf") {
-      fprintf(stderr, "mhap: %s: tf-idf weighting options are not implemented\n", a.c_str());
+    else if (a == "--filter-threshold") W.filter_threshold = atof(num("--filter-threshold"));
+    else if (a == "--repeat-weight") W.repeat_weight = atof(num("--repeat-weight"));
+    else if (a == "--repeat-idf-scale") W.repeat_idf_scale = atof(num("--repeat-idf-scale"));
+    else if (a == "--no-tf") W.no_tf = 1;
+    else if (a == "--supress-noise") {
+      fprintf(stderr, "mhap: %s: the jar's noise suppression is not implemented\n", a.c_str());
       return 1;
     } else if (a == "--no-self") no_self = true;
     else if (a == "-f") fpath = num("-f");
@@ -235,11 +234,6 @@ int main(int argc, char **argv) {
   if (fasta && !qpath) {
     fprintf(stderr, "mhap: -p needs -q <output directory>\n");
     return usage(argv[0]);
-  }
-  if (!ignored.empty()) {
-    fprintf(stderr, "mhap: WARNING:");
-    for (auto &s : ignored) fprintf(stderr, " %s", s.c_str());
-    fprintf(stderr, " accepted, but the sketch is unweighted (no tf-idf repeat weighting)\n");
   }
   const char *dev = getenv("CANU_MHAP_DEVICE");
   mhap_ctx *ctx = nullptr;
@@ -266,14 +260,15 @@ int main(int argc, char **argv) {
     if (b.n) {
       if (mhap_load_reads(ctx, 1, b.n, bases.data(), off.data(), len.data()) != 0) {
         rc = fail_lib("load");
-      } else if (fpath) {
+      } else {
         std::string kmers;
-        uint64_t nk = 0;
-        if (!read_filter(fpath, P.k, filter_threshold, kmers, nk)) {
+        std::vector<double> fr;
+        if (fpath && !read_filter(fpath, P.k, kmers, fr)) {
           fprintf(stderr, "mhap: cannot read filter '%s'\n", fpath);
           rc = 1;
-        } else if (mhap_set_filter_kmers(ctx, kmers.data(), nk) != 0) {
-          rc = fail_lib("filter");
+        } else if ((fpath || W.repeat_weight >= 0.0) &&
+                   mhap_set_kmer_frequencies(ctx, kmers.data(), fr.data(), fr.size(), &W) != 0) {
+          rc = fail_lib("k-mer frequencies");
         }
       }
       if (!rc && mhap_sketch(ctx, 1, b.n) != 0) rc = fail_lib("sketch");

@@ -8,7 +8,6 @@ from __future__ import annotations
 import ctypes
 import dataclasses
 import os
-import warnings
 
 import numpy as np
 
@@ -24,8 +23,10 @@ EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last
            "mhap_abi_version", "mhap_load_reads", "mhap_load_reads_device",
            "mhap_set_filter_kmers", "mhap_sketch", "mhap_sketch_buffers", "mhap_copy_sketches",
            "mhap_build_index", "mhap_build_index_range", "mhap_compare_all",
-           "mhap_copy_sketches_host",
+           "mhap_copy_sketches_host", "mhap_weighting_init", "mhap_set_kmer_frequencies",
            "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
+
+ABI_VERSION = 3          # MHAP_ABI_VERSION of include/canu_mhap.h
 
 
 class MhapError(RuntimeError):
@@ -39,6 +40,11 @@ class _Params(ctypes.Structure):
                 ("min_matches", ctypes.c_uint32), ("ordered_sketch", ctypes.c_uint32),
                 ("ordered_k", ctypes.c_uint32), ("min_olap", ctypes.c_int32),
                 ("threshold", ctypes.c_double)]
+
+
+class _Weighting(ctypes.Structure):
+    _fields_ = [("repeat_weight", ctypes.c_double), ("repeat_idf_scale", ctypes.c_double),
+                ("filter_threshold", ctypes.c_double), ("no_tf", ctypes.c_int32)]
 
 
 class _Stats(ctypes.Structure):
@@ -59,6 +65,10 @@ def load_library(path: str | None = None):
     if not os.path.exists(path):
         raise MhapError(-1, f"{path} missing: run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
+    # the structs below mirror include/canu_mhap.h of this ABI: refuse a stale library
+    if lib.mhap_abi_version() != ABI_VERSION:
+        raise MhapError(-1, f"{path} has ABI {lib.mhap_abi_version()}, this binding expects "
+                            f"{ABI_VERSION}: rebuild with __graft_entry__.build()")
     P, V, U32, U64 = ctypes.POINTER, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
     lib.mhap_params_init.argtypes = [P(_Params)]
     lib.mhap_ctx_create.argtypes = [P(_Params), ctypes.c_int, P(V)]
@@ -78,6 +88,8 @@ def load_library(path: str | None = None):
     lib.mhap_fetch.argtypes = [V, V, U64, P(U64)]
     lib.mhap_write_text.argtypes = [V, ctypes.c_char_p, U32, U32, U32]
     lib.mhap_get_stats.argtypes = [V, P(_Stats)]
+    lib.mhap_weighting_init.argtypes = [P(_Weighting)]
+    lib.mhap_set_kmer_frequencies.argtypes = [V, ctypes.c_char_p, V, U64, P(_Weighting)]
     _lib = lib
     return lib
 
@@ -92,6 +104,12 @@ class MhapParameters:
     ordered_sketch_size: int = 1536
     ordered_kmer_size: int = 12
     min_olap_length: int = 500
+    # repeat weighting (canu_mhap.h mhap_weighting; canu passes --repeat-weight 0.9
+    # --repeat-idf-scale 10 --filter-threshold, OverlapMhap.pm:382, :390); < 0: unweighted
+    repeat_weight: float = -1.0
+    repeat_idf_scale: float = 10.0
+    filter_threshold: float = 1e-5
+    no_tf: bool = False
 
     @classmethod
     def sensitivity(cls, level: str, tag: str = "cor", nanopore: bool = False,
@@ -121,10 +139,23 @@ class MhapParameters:
         return _Params(self.k, self.num_hashes, self.num_min_matches, self.ordered_sketch_size,
                        self.ordered_kmer_size, self.min_olap_length, self.threshold)
 
+    def weighting_c(self) -> _Weighting:
+        return _Weighting(self.repeat_weight, self.repeat_idf_scale, self.filter_threshold,
+                          1 if self.no_tf else 0)
+
+    def canu_weighting(self, filter_threshold: float = 0.000005) -> "MhapParameters":
+        """The weighting canu always asks the jar for (OverlapMhap.pm:382, :390;
+        mhapFilterThreshold, Defaults.pm:699)."""
+        self.repeat_weight, self.repeat_idf_scale = 0.9, 10.0
+        self.filter_threshold = filter_threshold
+        return self
+
     def as_oracle(self) -> dict:
         return dict(k=self.k, num_hashes=self.num_hashes, min_matches=self.num_min_matches,
                     threshold=self.threshold, ordered_sketch=self.ordered_sketch_size,
-                    ordered_k=self.ordered_kmer_size, min_olap=self.min_olap_length)
+                    ordered_k=self.ordered_kmer_size, min_olap=self.min_olap_length,
+                    repeat_weight=self.repeat_weight, repeat_idf_scale=self.repeat_idf_scale,
+                    filter_threshold=self.filter_threshold, no_tf=bool(self.no_tf))
 
 
 def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
@@ -153,29 +184,43 @@ def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
             p.min_olap_length = int(val); i += 1
         elif a in ("-f", "-p", "-q", "-s", "--num-threads"):
             io[a] = val; i += 1
-        elif a in ("--filter-threshold", "--repeat-weight", "--repeat-idf-scale"):
-            # canu always passes these (OverlapMhap.pm:382, :390).  The jar's tf-idf
-            # repeat weighting is not implemented here (its algorithm ships only as
-            # bytecode, no fixture pins it): the sketch stays unweighted and -f k-mers are
-            # dropped outright.  Say so rather than accept the options silently.
-            io[a] = val; i += 1
-            io.setdefault("ignored", []).append(a)
+        elif a == "--repeat-weight":
+            p.repeat_weight = float(val); i += 1
+        elif a == "--repeat-idf-scale":
+            p.repeat_idf_scale = float(val); i += 1
+        elif a == "--filter-threshold":
+            p.filter_threshold = float(val); i += 1
+        elif a == "--no-tf":
+            p.no_tf = True
         elif a in ("--no-self",):
             io[a] = True
-        elif a in ("--supress-noise", "--no-tf"):
-            raise MhapError(-3, f"{a}: tf-idf weighting options are not implemented")
+        elif a == "--supress-noise":
+            raise MhapError(-3, f"{a}: the jar's low-frequency noise suppression is not "
+                                "implemented (canu passes it only with mhapFilterUnique)")
         else:
             raise MhapError(-2, f"unknown MHAP option '{a}'")
         i += 1
-    if io.get("ignored"):
-        warnings.warn("MHAP options " + ", ".join(io["ignored"]) + " are ignored: the sketch is "
-                      "unweighted (no tf-idf repeat weighting); see DESIGN.md", MhapWeightingWarning,
-                      stacklevel=2)
     return p, io
 
 
-class MhapWeightingWarning(UserWarning):
-    """The jar's repeat-weighting options were given; this build sketches unweighted."""
+def read_frequency_file(path: str, k: int) -> tuple[list[str], np.ndarray]:
+    """The -f file canu writes (Meryl.pm:699-716): optionally gzipped, a first line with
+    the number of k-mer lines, then "kmer<TAB>fraction" lines (both strands)."""
+    import gzip
+    op = gzip.open if path.endswith(".gz") else open
+    kmers, fr = [], []
+    with op(path, "rt") as f:
+        for j, line in enumerate(f):
+            parts = line.split()
+            if not parts:
+                continue
+            if j == 0 and len(parts) == 1:
+                continue                                   # the count line
+            if len(parts[0]) != k:
+                raise MhapError(-4, f"{path}:{j + 1}: k-mer of length {len(parts[0])}, not {k}")
+            kmers.append(parts[0])
+            fr.append(float(parts[1]) if len(parts) > 1 else 1.0)
+    return kmers, np.asarray(fr, dtype=np.float64)
 
 
 class Mhap:
@@ -224,6 +269,16 @@ class Mhap:
     def set_filter_kmers(self, kmers: list[str]) -> None:
         blob = "".join(kmers).encode()
         self._check(self.lib.mhap_set_filter_kmers(self.ctx, blob, len(kmers)))
+
+    def set_kmer_frequencies(self, kmers: list[str], fractions) -> None:
+        """-f with fractions, under this job's weighting options (params.repeat_weight ...):
+        weighted sketches when repeat_weight >= 0 (no k-mers: tf weighting alone)."""
+        blob = "".join(kmers).encode()
+        fr = np.ascontiguousarray(fractions, dtype=np.float64)
+        w = self.params.weighting_c()
+        self._check(self.lib.mhap_set_kmer_frequencies(self.ctx, blob,
+                                                       fr.ctypes.data if fr.size else None,
+                                                       len(kmers), ctypes.byref(w)))
 
     def sketch(self, bgn: int | None = None, end: int | None = None) -> None:
         bgn = self.first_iid if bgn is None else bgn
@@ -280,11 +335,16 @@ class Mhap:
         self._check(self.lib.mhap_get_stats(self.ctx, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in _Stats._fields_}
 
-    def run(self, rs, filter_kmers=None) -> np.ndarray:
-        """One all-vs-all job over rs: every pair (a < b) once, records sorted by (a, b)."""
+    def run(self, rs, filter_kmers=None, frequencies=None) -> np.ndarray:
+        """One all-vs-all job over rs: every pair (a < b) once, records sorted by (a, b).
+        frequencies = (k-mers, fractions) of a -f file; with params.repeat_weight >= 0 the
+        sketches are weighted (tf weighting alone when no frequencies are given)."""
         self.load_reads(rs)
         if filter_kmers:
             self.set_filter_kmers(filter_kmers)
+        if frequencies is not None or self.params.repeat_weight >= 0:
+            km, fr = frequencies if frequencies is not None else ([], np.zeros(0))
+            self.set_kmer_frequencies(list(km), fr)
         self.sketch()
         self.build_index()
         self.compare()

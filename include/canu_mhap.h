@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHAP_ABI_VERSION 2
+#define MHAP_ABI_VERSION 3
 
 typedef struct {
   uint32_t k;               /* -k                      MinHash k-mer size, 1..32        */
@@ -93,6 +93,35 @@ int         mhap_load_reads_device(mhap_ctx *ctx, uint32_t first_iid, uint32_t n
 
 /* -f: k-mers (n * k ACGT bytes, back to back) that never enter a MinHash sketch. */
 int         mhap_set_filter_kmers(mhap_ctx *ctx, const char *kmers, uint64_t n);
+
+/* The jar's repeat weighting (MHAP 2.x tf-idf; options canu always passes,
+ * OverlapMhap.pm:382, :390).  Restated from the published algorithm -- parity with the jar
+ * is unpinned: each distinct k-mer c of a read enters the MinHash sketch with
+ * an integer weight w(c) >= 1, i.e. w(c) consecutive draws of its xorshift64 chain per
+ * hash function instead of one:
+ *   tf(c)   occurrences of c in the read (1 with no_tf)
+ *   idf(c)  ln(1 / fraction(c)) for -f k-mers with fraction >= filter_threshold, else
+ *           ln(1 / filter_threshold); scaled linearly onto [1, repeat_idf_scale] between
+ *           the most frequent -f k-mer (1) and ln(1 / filter_threshold) (repeat_idf_scale)
+ *   w(c)    max(1, floor(tf(c) * m(c) + 0.5)), m(c) = r + (1 - r) * scaled idf(c), where
+ *           r = repeat_weight; r >= 1 or no -f k-mers: m = 1 (tf only)
+ * repeat_weight < 0 is MHAP 1.x's unweighted sketch: -f k-mers with a fraction >=
+ * filter_threshold are dropped, every other k-mer counts once. */
+typedef struct {
+  double  repeat_weight;      /* --repeat-weight     (canu: 0.9; < 0 unweighted)         */
+  double  repeat_idf_scale;   /* --repeat-idf-scale  (canu: 10)                          */
+  double  filter_threshold;   /* --filter-threshold  (canu: mhapFilterThreshold 5e-6)    */
+  int32_t no_tf;              /* --no-tf                                                 */
+} mhap_weighting;
+
+/* Unweighted defaults: repeat_weight -1, repeat_idf_scale 10, filter_threshold 1e-5, tf on. */
+void        mhap_weighting_init(mhap_weighting *w);
+
+/* -f with its second column: n k-mers (n * k bytes) and the fraction of all k-mers each
+ * one is (Meryl.pm:699-716 writes "kmer<TAB>fraction" lines, both strands), with the
+ * weighting options.  n = 0 sets the weighting alone (tf weighting, no idf). */
+int         mhap_set_kmer_frequencies(mhap_ctx *ctx, const char *kmers, const double *fractions,
+                                      uint64_t n, const mhap_weighting *w);
 
 /* Sketch reads bgn_iid..end_iid (inclusive): MinHash sketch + ordered sketch. */
 int         mhap_sketch(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);

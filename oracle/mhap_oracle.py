@@ -69,7 +69,8 @@ for _c, _v in zip(b"ACGTacgt", (0, 1, 2, 3, 0, 1, 2, 3)):
 def default_params(**kw) -> dict:
     """canu's 'normal' sensitivity for correction (OverlapMhap.pm:116-121, Defaults.pm)."""
     p = dict(k=16, num_hashes=512, min_matches=3, threshold=0.78, ordered_sketch=1536,
-             ordered_k=12, min_olap=500)
+             ordered_k=12, min_olap=500, repeat_weight=-1.0, repeat_idf_scale=10.0,
+             filter_threshold=1e-5, no_tf=False)
     p.update(kw)
     return p
 
@@ -126,6 +127,88 @@ def sketch(rs, p: dict, skip: np.ndarray | None = None) -> np.ndarray:
                 x ^= x >> U64(35)
                 x ^= x << U64(4)
                 out[i, j] = (x & U64(0xFFFFFFFF)).astype(np.uint32).view(np.int32).min()
+    return out
+
+
+def kmer_multipliers(freq_kmers, fractions, p: dict):
+    """The -f table of the weighted sketch (canu_amd mhap_set_kmer_frequencies, restated from
+    MHAP 2.x's tf-idf; parity with the jar unpinned): canonical codes of the -f k-mers with
+    a fraction >= filter_threshold (largest fraction per code), their multipliers
+      m = r + (1 - r) * (1 + (X - 1) * (idf - idf_min) / (idf_max - idf_min)),
+      idf = ln(1 / fraction), idf_max = ln(1 / filter_threshold), idf_min over the table,
+    r = repeat_weight, X = repeat_idf_scale (m = 1 when r >= 1 or the table is empty), and
+    the multiplier of every other k-mer (idf = idf_max).  Logs and arithmetic in Python
+    floats (C doubles, libm log), in the library's order of operations."""
+    import math
+    k, thr = p["k"], p["filter_threshold"]
+    r, X = p["repeat_weight"], p["repeat_idf_scale"]
+    best = {}
+    for km, f in zip(freq_kmers, fractions):
+        f = float(f)
+        c = _CODE[np.frombuffer(km.encode() if isinstance(km, str) else km, dtype=np.uint8)]
+        if c.shape[0] != k or (c == 255).any() or not (f >= thr):
+            continue
+        _, can, _ = kmers(c, k)
+        cc = int(can[0])
+        best[cc] = max(best.get(cc, f), f)
+    codes = sorted(best)
+    idf_max = math.log(1.0 / thr)
+    idf = [math.log(1.0 / best[c]) for c in codes]
+    idf_min = min([idf_max] + idf)
+
+    def mult(v):
+        if r >= 1.0 or not codes:
+            return 1.0
+        sc = 1.0 + (X - 1.0) * (v - idf_min) / (idf_max - idf_min) if idf_max > idf_min else X
+        return r + (1.0 - r) * sc
+
+    return (np.array(codes, dtype=U64), np.array([mult(v) for v in idf], dtype=np.float64),
+            mult(idf_max))
+
+
+def sketch_weighted(rs, p: dict, freq=None) -> np.ndarray:
+    """Stage 1 with repeat weighting (p["repeat_weight"] >= 0): every DISTINCT canonical
+    k-mer c of a read, with tf = its occurrences (1 with no_tf) and multiplier m (the -f
+    table, kmer_multipliers; m = 1 without one), has weight w = max(1, floor(tf * m + 0.5))
+    and takes w consecutive steps of its xorshift64 chain (seeded by splitmix64(c)) per
+    hash function j; sketch[j] = min over the read's k-mers and their w values of
+    int32(low 32 bits).  With w = 1 everywhere this is sketch() exactly."""
+    import math
+    H, k = p["num_hashes"], p["k"]
+    if freq is not None:
+        fcodes, fmult, dmult = kmer_multipliers(freq[0], freq[1], p)
+    else:
+        fcodes, fmult, dmult = np.zeros(0, dtype=U64), np.zeros(0), 1.0
+    out = np.full((rs.nreads, H), INT32_MAX, dtype=np.int32)
+    for i in range(rs.nreads):
+        _, c, _ = kmers(read_codes(rs, i), k)
+        if c.size == 0:
+            continue
+        u, tf = np.unique(c, return_counts=True)
+        if p.get("no_tf"):
+            tf = np.ones_like(tf)
+        m = np.full(u.shape[0], dmult, dtype=np.float64)
+        if fcodes.size:
+            q = np.searchsorted(fcodes, u)
+            hit = (q < fcodes.size) & (fcodes[np.minimum(q, fcodes.size - 1)] == u)
+            m[hit] = fmult[q[hit]]
+        w = np.array([max(1, int(math.floor(float(t) * float(mm) + 0.5)))
+                      for t, mm in zip(tf.tolist(), m.tolist())], dtype=np.int64)
+        x = splitmix64(u)
+        wmax = int(w.max())
+        with np.errstate(over="ignore"):
+            for j in range(H):
+                best = np.full(u.shape[0], INT32_MAX, dtype=np.int32)
+                for t in range(wmax):
+                    act = t < w
+                    xa = x[act]
+                    xa ^= xa << U64(21)
+                    xa ^= xa >> U64(35)
+                    xa ^= xa << U64(4)
+                    x[act] = xa
+                    v = (xa & U64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+                    best[act] = np.minimum(best[act], v)
+                out[i, j] = best.min()
     return out
 
 
@@ -210,10 +293,12 @@ def compare(A, B, la: int, lb: int, p: dict):
     return (min(D, 1.0), a_bgn, a_end, o, b_bgn, b_end)
 
 
-def run(rs, p: dict, q_range=None, skip_kmers=None, t_range=None) -> np.ndarray:
+def run(rs, p: dict, q_range=None, skip_kmers=None, t_range=None, freq=None) -> np.ndarray:
     """All-vs-all over rs (queries in q_range, 0-based [lo, hi)): MHAP_DTYPE records with
     1-based read IDs (rs.first_iid based), sorted by (a, b).  t_range (0-based [lo, hi)):
-    the targets are the reads in it (every one but the query), not the later reads."""
+    the targets are the reads in it (every one but the query), not the later reads.
+    p["repeat_weight"] >= 0: weighted sketches (sketch_weighted, -f table freq =
+    (k-mers, fractions) or none)."""
     skip = None
     if skip_kmers:
         codes = []
@@ -223,7 +308,10 @@ def run(rs, p: dict, q_range=None, skip_kmers=None, t_range=None) -> np.ndarray:
             codes.extend(can.tolist())
         skip = np.unique(np.array(codes, dtype=U64))
     q_range = q_range or (0, rs.nreads)
-    sk = sketch(rs, p, skip)
+    if p.get("repeat_weight", -1.0) >= 0:
+        sk = sketch_weighted(rs, p, freq)
+    else:
+        sk = sketch(rs, p, skip)
     cands = candidates(sk, q_range, p["min_matches"], t_range)
     cache = {}
 

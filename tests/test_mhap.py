@@ -48,7 +48,7 @@ def test_header_declares_the_python_exports():
 def test_library_exports_every_declared_symbol(built):
     lib = mhap.load_library()
     assert [f for f in mhap.EXPORTS if not hasattr(lib, f)] == []
-    assert lib.mhap_abi_version() == 2
+    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 3
 
 
 def test_params_init_is_canu_normal(built):
@@ -76,20 +76,77 @@ def test_sensitivity_presets():
 
 
 def test_parse_canu_command_line():
+    """The jar's options as canu writes them (OverlapMhap.pm:380-395), weighting included."""
     argv = ("--repeat-weight 0.9 --repeat-idf-scale 10 -k 16 --num-hashes 768 "
             "--num-min-matches 2 --threshold 0.73 --filter-threshold 0.000005 "
             "--ordered-sketch-size 1536 --ordered-kmer-size 12 --min-olap-length 500 "
             "--num-threads 8 -s ./blocks/000001.dat -q queries/000001").split()
-    with pytest.warns(mhap.MhapWeightingWarning, match="repeat-weight"):
-        p, io = mhap.parse_mhap_args(argv)
-    assert io["ignored"] == ["--repeat-weight", "--repeat-idf-scale", "--filter-threshold"]
+    p, io = mhap.parse_mhap_args(argv)
     assert (p.k, p.num_hashes, p.num_min_matches, p.ordered_sketch_size) == (16, 768, 2, 1536)
     assert abs(p.threshold - 0.73) < 1e-12 and p.min_olap_length == 500
+    assert (p.repeat_weight, p.repeat_idf_scale, p.filter_threshold) == (0.9, 10.0, 0.000005)
+    assert not p.no_tf
     assert io["-s"] == "./blocks/000001.dat" and io["--num-threads"] == "8"
+    assert mhap.parse_mhap_args(["--no-tf"])[0].no_tf
     with pytest.raises(mhap.MhapError):
-        mhap.parse_mhap_args(["--no-tf"])
+        mhap.parse_mhap_args(["--supress-noise", "2"])
     with pytest.raises(mhap.MhapError):
         mhap.parse_mhap_args(["--bogus"])
+
+
+def test_frequency_file(tmp_path):
+    """The -f file canu writes (Meryl.pm:699-716): gzip, a count line, kmer<TAB>fraction."""
+    import gzip
+    path = str(tmp_path / "f.ignore.gz")
+    with gzip.open(path, "wt") as f:
+        f.write("4\nACGTACGTACGTACGT\t1.000000e-03\nACGTACGTACGTACGT\t1.000000e-03\n"
+                "AAAAAAAAAAAAAAAA\t5.000000e-06\nTTTTTTTTTTTTTTTT\t5.000000e-06\n")
+    km, fr = mhap.read_frequency_file(path, 16)
+    assert km[0] == "ACGTACGTACGTACGT" and len(km) == 4 and fr[2] == 5e-6
+
+
+def _weighted_params(**kw):
+    p = M.default_params(num_hashes=96)
+    p.update(repeat_weight=0.9, repeat_idf_scale=10.0, filter_threshold=5e-6)
+    p.update(kw)
+    return p
+
+
+def _freq_for(rs, every=11):
+    """-f entries for a read set: some of read 0's 16-mers at graded fractions, both
+    strands written as canu does."""
+    r0 = rs.read(0).decode()
+    comp = str.maketrans("ACGT", "TGCA")
+    km, fr = [], []
+    for j, i in enumerate(range(0, 2400, every)):
+        m = r0[i:i + 16]
+        f = 5e-6 * (1.5 ** (j % 12))
+        km += [m, m.translate(comp)[::-1]]
+        fr += [f, f]
+    return km, np.array(fr)
+
+
+def test_oracle_weighting_properties():
+    """The restated weighting (canu_mhap.h): with weight 1 everywhere the weighted sketch
+    IS the unweighted one; tf weighting changes only reads with repeated k-mers; the -f
+    table lowers the weight of listed (frequent) k-mers relative to the rest."""
+    rs = _reads(n=6, L=3000, cov=10, seed=17)
+    base = M.sketch(rs, M.default_params(num_hashes=96))
+    # no -f, no tf: every weight is 1
+    w1 = M.sketch_weighted(rs, _weighted_params(no_tf=True), None)
+    assert np.array_equal(w1, base)
+    # r >= 1: m = 1 for every k-mer (tf only); a read with no repeated k-mer is unchanged
+    tfo = M.sketch_weighted(rs, _weighted_params(repeat_weight=1.0), _freq_for(rs))
+    assert np.array_equal(tfo, M.sketch_weighted(rs, _weighted_params(repeat_weight=1.0)))
+    # the multipliers: frequent k-mers get the smallest, unlisted ones the largest
+    km, fr = _freq_for(rs)
+    codes, mult, dm = M.kmer_multipliers(km, fr, _weighted_params())
+    assert codes.size == np.unique(codes).size and mult.min() >= 1.0 - 1e-12
+    assert abs(dm - (0.9 + 0.1 * 10.0)) < 1e-12 and mult.max() <= dm
+    assert abs(mult.min() - 1.0) < 1e-12                 # the most frequent: scaled idf 1
+    # a read whose k-mers are all listed at one fraction gets a sketch unlike the tf one
+    full = M.sketch_weighted(rs, _weighted_params(), (km, fr))
+    assert not np.array_equal(full, tfo)
 
 
 def test_oracle_kmer_codes():
@@ -257,3 +314,50 @@ def test_gpu_sketch_rows_match_oracle(built, small):
         key = (h.astype(np.uint64) << np.uint64(32)) | (pos.astype(np.uint64) << np.uint64(1)) \
             | s.astype(np.uint64)
         assert np.array_equal(od[i, :oc[i]], key), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "repeat_read"])
+def test_gpu_weighted_sketch_rows_match_oracle(built, variant):
+    """The weighted MinHash rows in HBM (distinct k-mers by a radix sort, tf as run lengths,
+    the -f multipliers) equal the restatement's, bit for bit."""
+    import ctypes
+    kw = dict(n=40, L=3000, cov=12, seed=19)
+    if variant == "repeat_read":
+        kw.update(n_repeats=6, repeat_len=400)        # tf > 1 inside reads
+    rs = _reads(**kw)
+    P = mhap.MhapParameters(num_hashes=128, ordered_sketch_size=600, ordered_kmer_size=14,
+                            min_olap_length=300).canu_weighting()
+    freq = _freq_for(rs)
+    if variant == "no_tf":
+        P.no_tf = True
+    if variant == "tf_only":
+        P.repeat_weight = 1.0
+    m = mhap.Mhap(P, device=0)
+    m.load_reads(rs)
+    m.set_kmer_frequencies(*freq)
+    m.sketch()
+    pmh, _, _ = m.sketch_buffers()
+    mh = np.zeros((rs.nreads, P.num_hashes), dtype=np.int32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(mh.ctypes.data, pmh, mh.nbytes, 2) == 0
+    m.close()
+    want = M.sketch_weighted(rs, P.as_oracle(), freq)
+    assert np.array_equal(mh, want)
+
+
+@pytest.mark.gpu
+def test_gpu_weighted_job_matches_oracle(built):
+    """canu's weighting end to end: records of the weighted all-vs-all equal the
+    restatement's (integers bit-exact, erate within 1e-6)."""
+    rs = _reads(n=70, L=4000, cov=14, seed=23)
+    P = mhap.MhapParameters(num_hashes=256, ordered_sketch_size=1000,
+                            min_olap_length=400).canu_weighting()
+    freq = _freq_for(rs, every=5)
+    m = mhap.Mhap(P, device=0)
+    got = m.run(rs, frequencies=freq)
+    m.close()
+    want = M.run(rs, P.as_oracle(), freq=freq)
+    assert len(want) > 20
+    _same(got, want)

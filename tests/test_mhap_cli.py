@@ -40,7 +40,7 @@ def _run(cli, args, cwd=None):
 
 def test_cli_usage_errors(cli):
     for args in ([], ["-p", "x.fasta"], ["-p", "x.fasta", "-s", "y.dat", "-q", "."],
-                 ["--bogus"], ["-k"], ["--no-tf", "-s", "y.dat"],
+                 ["--bogus"], ["-k"], ["--no-tf", "-s", "missing.dat"],
                  ["--supress-noise", "2", "-s", "y.dat"]):
         cp = _run(cli, args)
         assert cp.returncode == 1, (args, cp.stderr)
@@ -86,20 +86,38 @@ def _same(got, want):
 
 @pytest.mark.gpu
 def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
+    import gzip
     rs = _reads()
     blocks = [_block(rs, i, i + BLOCK) for i in range(0, N, BLOCK)]
     bdir = tmp_path / "blocks"
     bdir.mkdir()
+    # the -f file canu writes (Meryl.pm:699-716): a count line, kmer<TAB>fraction, both
+    # strands; some of read 1's 16-mers at graded fractions
+    r0 = rs.read(0).decode()
+    comp = str.maketrans("ACGT", "TGCA")
+    km, fr = [], []
+    for j, i0 in enumerate(range(0, 3000, 9)):
+        m = r0[i0:i0 + 16]
+        km += [m, m.translate(comp)[::-1]]
+        fr += [5e-6 * 1.4 ** (j % 15)] * 2
+    fpath = tmp_path / "asm.ms16.frequentMers.ignore.gz"
+    with gzip.open(fpath, "wt") as f:
+        f.write(f"{len(km)}\n")
+        for m, x in zip(km, fr):
+            f.write(f"{m}\t{x:e}\n")
+    fr_read = [float(f"{x:e}") for x in fr]          # the fractions as the file holds them
     for i, b in enumerate(blocks, start=1):
         fa = bdir / f"{i:06d}.input.fasta"
         with open(fa, "w") as f:
             for r in range(b.nreads):
                 f.write(f">{BLOCK * (i - 1) + r + 1}\n{b.read(r).decode()}\n")
-        cp = _run(cli, [*OPTS, *CANU_EXTRA, "-p", f"./{fa.name}", "-q", "."], cwd=bdir)
+        cp = _run(cli, [*OPTS, *CANU_EXTRA, "-f", str(fpath), "-p", f"./{fa.name}", "-q", "."],
+                  cwd=bdir)
         assert cp.returncode == 0, cp.stderr
-        assert "unweighted" in cp.stderr
         os.replace(bdir / f"{i:06d}.input.dat", bdir / f"{i:06d}.dat")
-    P = mhap.MhapParameters().as_oracle()
+    # the sketches are canu's weighted ones (restated tf-idf, canu_mhap.h)
+    P = mhap.MhapParameters().canu_weighting(0.000005).as_oracle()
+    freq = (km, np.array(fr_read))
 
     # job 1: block 1 against itself and blocks 2-3 (OverlapMhap.pm's "(and self)" case)
     q1 = tmp_path / "queries" / "000001"
@@ -109,8 +127,8 @@ def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
     cp = _run(cli, [*OPTS, "-s", "./blocks/000001.dat", "-q", "queries/000001"], cwd=tmp_path)
     assert cp.returncode == 0, cp.stderr
     got = _parse(cp.stdout)
-    self_want = M.run(blocks[0], P)
-    cross_want = M.run(_concat(blocks), P, q_range=(BLOCK, N), t_range=(0, BLOCK))
+    self_want = M.run(blocks[0], P, freq=freq)
+    cross_want = M.run(_concat(blocks), P, q_range=(BLOCK, N), t_range=(0, BLOCK), freq=freq)
     assert len(self_want) > 5 and len(cross_want) > 5
     _same(got[:len(self_want)], self_want)
     _same(got[len(self_want):], cross_want)
@@ -125,7 +143,8 @@ def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
                     "./blocks/000003.dat"], cwd=tmp_path)
     assert cp.returncode == 0, cp.stderr
     got2 = _parse(cp.stdout)
-    want2 = M.run(_concat(blocks[1:]), P, q_range=(BLOCK, 2 * BLOCK), t_range=(0, BLOCK))
+    want2 = M.run(_concat(blocks[1:]), P, q_range=(BLOCK, 2 * BLOCK), t_range=(0, BLOCK),
+                  freq=freq)
     _same(got2, want2)
 
     # a sketch file made with other options is refused
