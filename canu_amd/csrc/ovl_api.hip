@@ -221,6 +221,15 @@ struct ovl_ctx {
   uint32_t stats_ext_waves = 0, stats_gen_waves = 0;
   uint64_t index_records = 0;    // records of the current index (windows + skip markers)
 
+  // pending extension work (see find_impl): chains of several probe chunks -- and of the
+  // driver's hash batches -- are appended here and extended together in one launch
+  struct {
+    DBuf<Unit> units;
+    DBuf<Node> pnodes;
+    DBuf<PairRec> pairs;
+    uint64_t nu = 0, nn = 0, np = 0;
+  } acc;
+
   // results
   DBuf<Rec> d_out;
   uint64_t nout = 0;
@@ -440,6 +449,18 @@ __global__ void k_olim_keys(const PairRec *pairs, const Node *pnodes, uint32_t n
 __global__ void k_gather_u64(const uint64_t *src, const uint32_t *idx, uint32_t n, uint64_t *dst) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
     dst[i] = src[idx[i]];
+}
+
+// A chunk's pairs appended to the pending-extension accumulator: their unit and node indices
+// move by where the chunk's units and nodes land there.
+__global__ void k_append_pairs(const PairRec *src, uint32_t n, uint32_t unit_base,
+                               uint32_t node_base, PairRec *dst) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    PairRec p = src[i];
+    p.unit += unit_base;
+    p.node_off += node_base;
+    dst[i] = p;
+  }
 }
 
 __global__ void k_gather_unit(const PairRec *pairs, const uint32_t *idx, uint32_t n, uint32_t *dst) {
@@ -1056,7 +1077,7 @@ IndexDev index_dev(const ovl_ctx *c) {
 // libraries [lib_lo, lib_hi] against the current index.  append: keep the records and
 // counters already held (the driver's later hash batches).
 static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, uint32_t lib_hi,
-                     bool append, uint64_t *n_out) {
+                     bool append, uint64_t *n_out, bool flush = true) {
   if (!c) return fail(OVL_ERR_STATE, "null context");
   if (!c->have_index) return fail(OVL_ERR_STATE, "ovl_build_hash_index() first");
   HIPC(hipSetDevice(c->device));
@@ -1086,6 +1107,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     uwin.push_back((uint64_t)(L - (int32_t)k + 1));
   }
   if (!append) {
+    c->acc.nu = c->acc.nn = c->acc.np = 0;          // a new job: nothing pending
     ovl_stats keep_idx = c->stats;
     memset(&c->stats, 0, sizeof(c->stats));
     c->stats.ms_index = keep_idx.ms_index;
@@ -1345,6 +1367,271 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     generic_pairs += left;
     return OVL_OK;
   };
+  // One chunk's (or the accumulator's) pairs through the extension kernels on xs, the host
+  // not waiting: work order, the staged classes, the generic kernel; collect(slot) reads
+  // its counters back.
+  auto launch_ext = [&](int slot, const Unit *ext_units, PairRec *ext_pairs, Node *ext_pnodes,
+                        uint32_t npairs, uint32_t nc) -> int {
+    auto &x_ctr = c->fb.xctr[slot];
+      nout_ub += 3ull * npairs;
+      if (int rc = ensure_out(nout_ub)) return rc;
+      ExtendArgs EA;
+      EA.R = c->reads();
+      EA.units = ext_units;
+      EA.pairs = ext_pairs;
+      EA.npairs = npairs;
+      EA.npairs_dev = nullptr;
+      EA.restore = 0;
+      EA.pnodes = ext_pnodes;
+      EA.pair_next = x_ctr.p + 5;
+      EA.error_bound = c->d_error_bound.p;
+      EA.match_limit = c->d_match_limit.p;
+      EA.max_errors = c->max_errors;
+      EA.branch_match_value = c->branch_match_value;
+      EA.min_branch_tail_slope = c->min_branch_tail_slope;
+      EA.min_branch_end_dist = 20;
+      EA.partial = c->P.partial;
+      EA.unique = c->P.unique_olap_per_pair;
+      EA.min_olap_len = c->P.min_olap_len;
+      EA.use_hopeless = c->P.use_hopeless_check;
+      EA.k = (int32_t)k;
+      EA.filter_by_kmer_count = c->P.filter_by_kmer_count;
+      EA.minkmer_exp = exp(-1.0 * (double)k * c->P.max_erate);
+      EA.rows = d_rows.p;
+      EA.rowdir = d_rowdir.p;
+      EA.deltas = d_deltas.p;
+      EA.out = c->d_out.p;
+      EA.nout = c->fb.xnout.p;
+      EA.out_cap = (uint32_t)std::min<uint64_t>(c->d_out.n, 0xFFFFFFF0ull);
+      EA.stats = d_stats.p;
+      EA.window = window ? 1 : 0;
+      EA.overflow = x_ctr.p + 7;
+      EA.dbg = nullptr;
+      if (getenv("OVL_DEBUG")) {
+        if (!c->dbg.p) {
+          HIPC(hipStreamSynchronize(xs));
+          if (c->dbg.alloc(32)) return fail(OVL_ERR_OOM, "debug counters");
+          HIPC(hipMemsetAsync(c->dbg.p, 0, 256, xs));
+        }
+        EA.dbg = c->dbg.p;
+      }
+      EA.list = nullptr;
+      EA.defer = nullptr;
+      EA.ndefer = nullptr;
+      EA.olim = c->P.frag_olap_limit;
+      EA.nunits = nc;
+      EA.useg = nullptr;
+      EA.ord_slot = nullptr;
+      EA.ord_diag = nullptr;
+      EA.dkey = nullptr;
+      slot_pairs[slot] = npairs;
+      HIPC(hipMemsetAsync(x_ctr.p, 0, 64, xs));
+      if (npairs && ordered) {
+        // the reference's two pair orders per unit (see k_olim_keys): String_Olap_Space
+        // order and By_Diag_Sum order, by stable radix sorts
+        auto &fb = c->fb;
+        const int n = (int)npairs;
+        size_t t1 = 0, t2 = 0, t3 = 0;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, fb.okey.p, fb.okey2.p, fb.oa.p,
+                                                fb.ob.p, n, 0, 32, xs));
+        HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, fb.ok64a.p, fb.ok64b.p, fb.oa.p,
+                                                fb.ob.p, n, 0, 64, xs));
+        HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, fb.ucnt.p, fb.useg.p, (int)nc + 1, xs));
+        const size_t tmp = std::max(std::max(t1, t2), t3);
+        HIPC(hipStreamSynchronize(xs));
+        if (fb.okey.grow(npairs) || fb.okey2.grow(npairs) || fb.oa.grow(npairs) ||
+            fb.ob.grow(npairs) || fb.oidx.grow(npairs) || fb.oidx2.grow(npairs) ||
+            fb.ok64a.grow(npairs) || fb.ok64b.grow(npairs) || fb.dkey.grow(npairs) ||
+            fb.ucnt.grow((size_t)nc + 1) || fb.useg.grow((size_t)nc + 1) ||
+            fb.otmp.grow(std::max<size_t>(tmp, 1)))
+          return fail(OVL_ERR_OOM, "-l pair orders");
+        const dim3 grid(std::min<uint32_t>((npairs + 255) / 256, 4096)), blk(256);
+        HIPC(hipMemsetAsync(fb.ucnt.p, 0, 4ull * (nc + 1), xs));
+        // first-hit order: by ~tgt, then (stably) by (unit, diag_bgn)
+        hipLaunchKernelGGL(k_olim_keys, grid, blk, 0, xs, ext_pairs, ext_pnodes, npairs, (int32_t)k,
+                           fb.okey.p, fb.ok64a.p, fb.oa.p, fb.dkey.p, fb.ucnt.p);
+        HIPC(hipGetLastError());
+        HIPC(hipcub::DeviceScan::ExclusiveSum(fb.otmp.p, t3, fb.ucnt.p, fb.useg.p, (int)nc + 1, xs));
+        size_t tt = t1;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.okey.p, fb.okey2.p, fb.oa.p,
+                                                fb.ob.p, n, 0, 32, xs));
+        hipLaunchKernelGGL(k_gather_u64, grid, blk, 0, xs, fb.ok64a.p, fb.ob.p, npairs, fb.ok64b.p);
+        tt = t2;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64b.p, fb.ok64a.p, fb.ob.p,
+                                                fb.oa.p, n, 0, 64, xs));
+        // String_Olap_Space indices, then the order by (unit, index)
+        hipLaunchKernelGGL(k_olim_slots, dim3(std::min<uint32_t>((nc + 3) / 4, 8192)), blk, 0, xs,
+                           ext_pairs, fb.oa.p, fb.useg.p, nc,
+                           c->first_iid - c->hash_bgn_iid, fb.ok64b.p, fb.ob.p);
+        HIPC(hipGetLastError());
+        tt = t2;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64b.p, fb.ok64a.p, fb.ob.p,
+                                                fb.oidx.p, n, 0, 64, xs));       // oidx: ord_slot
+        // By_Diag_Sum: stably by the diagonal key, then stably by unit
+        hipLaunchKernelGGL(k_gather_u64, grid, blk, 0, xs, fb.dkey.p, fb.oidx.p, npairs, fb.ok64a.p);
+        tt = t2;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64a.p, fb.ok64b.p, fb.oidx.p,
+                                                fb.oa.p, n, 0, 64, xs));
+        hipLaunchKernelGGL(k_gather_unit, grid, blk, 0, xs, ext_pairs, fb.oa.p, npairs, fb.okey.p);
+        tt = t1;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.okey.p, fb.okey2.p, fb.oa.p,
+                                                fb.oidx2.p, n, 0, 32, xs));      // oidx2: ord_diag
+        HIPC(hipGetLastError());
+        EA.useg = fb.useg.p;
+        EA.ord_slot = fb.oidx.p;
+        EA.ord_diag = fb.oidx2.p;
+        EA.dkey = fb.dkey.p;
+      }
+      if (npairs && !ordered) {
+        // the extension-only buffers are shared by the slots: regrowing one waits for xs
+        auto &fb = c->fb;
+        size_t tmp = 0;
+        HIPC(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, fb.okey.p, fb.okey2.p,
+                                                          fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
+                                                          32, xs));
+        if (fb.okey.n < npairs || fb.oidx.n < npairs || fb.okey2.n < npairs || fb.oidx2.n < npairs ||
+            d_defer.n < npairs || fb.defer2.n < npairs || fb.otmp.n < tmp || !fb.otmp.p) {
+          HIPC(hipStreamSynchronize(xs));
+          if (fb.okey.grow(npairs) || fb.oidx.grow(npairs) || fb.okey2.grow(npairs) ||
+              fb.oidx2.grow(npairs) || d_defer.grow(npairs) || fb.defer2.grow(npairs) ||
+              fb.otmp.grow(std::max<size_t>(tmp, 1)))
+            return fail(OVL_ERR_OOM, "work order");
+        }
+        if (npairs > 1) {
+          // longest-first work order (node count descending; ties keep pair order)
+          hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
+                             dim3(256), 0, xs, ext_pairs, npairs, fb.okey.p, fb.oidx.p);
+          HIPC(hipGetLastError());
+          HIPC(hipcub::DeviceRadixSort::SortPairsDescending(fb.otmp.p, tmp, fb.okey.p, fb.okey2.p,
+                                                            fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
+                                                            32, xs));
+          EA.list = fb.oidx2.p;
+        }
+      }
+      HIPC(hipEventRecord(c->xev[slot], xs));
+      if (npairs && ordered) {
+        EA.e_cap = gen.ecap;
+        EA.rows_cap = gen.stride;
+        EA.sw_words = 0;
+        EA.stage_len = 0;
+        EA.pair_next = x_ctr.p + 9;
+        n_ext_launch++;
+        if (gen.l16)
+          hipLaunchKernelGGL((k_extend<false, true, true>), dim3(gen.waves / gen.wpb),
+                             dim3(64 * gen.wpb), gen.lds, xs, EA);
+        else
+          hipLaunchKernelGGL((k_extend<false, false, true>), dim3(gen.waves / gen.wpb),
+                             dim3(64 * gen.wpb), gen.lds, xs, EA);
+        HIPC(hipGetLastError());
+      } else if (npairs) {
+        // the staged classes in turn, each deferring what it cannot take to the next list
+        // (whose length the next launch reads from the device counter); the generic kernel
+        // takes the last list, or every pair when no class exists
+        uint32_t *defer_buf[2] = {d_defer.p, c->fb.defer2.p};
+        for (size_t ci = 0; ci < ext_stage.size(); ci++) {
+          const ExtClass &g = ext_stage[ci];
+          EA.e_cap = g.ecap;
+          EA.rows_cap = g.stride;
+          EA.sw_words = g.sw;
+          EA.stage_len = (int32_t)g.len;
+          EA.pair_next = x_ctr.p + ctr_next[ci];
+          EA.defer = defer_buf[ci & 1];
+          EA.ndefer = x_ctr.p + ctr_defer[ci];
+          n_ext_launch++;
+          if (g.l16)
+            hipLaunchKernelGGL((k_extend<true, true>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
+          else
+            hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
+          HIPC(hipGetLastError());
+          EA.list = defer_buf[ci & 1];
+          EA.npairs_dev = x_ctr.p + ctr_defer[ci];
+          EA.restore = 1;          // a deferred pair may have had nodes removed (~Len)
+        }
+        EA.e_cap = gen.ecap;
+        EA.rows_cap = gen.stride;
+        EA.sw_words = 0;
+        EA.stage_len = 0;
+        EA.pair_next = x_ctr.p + 9;
+        EA.defer = nullptr;
+        EA.ndefer = nullptr;
+        // without the pipeline the host waits for this chunk next anyway: read the last
+        // class's defer count and skip an empty generic launch
+        bool gen_needed = true;
+        if (!pipe && !ext_stage.empty()) {
+          uint32_t nd = 0;
+          HIPC(hipMemcpyAsync(&nd, x_ctr.p + ctr_defer[ext_stage.size() - 1], 4,
+                              hipMemcpyDeviceToHost, xs));
+          HIPC(hipStreamSynchronize(xs));
+          gen_needed = nd > 0;
+        }
+        if (gen_needed) {
+          n_ext_launch++;
+          if (gen.l16)
+            hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                               gen.lds, xs, EA);
+          else
+            hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
+                               gen.lds, xs, EA);
+          HIPC(hipGetLastError());
+        }
+      }
+    HIPC(hipEventRecord(c->xev[2 + slot], xs));
+    pending[slot] = true;
+    return OVL_OK;
+  };
+  // Append a chunk's units, list nodes and pairs to the accumulator (device copies on s,
+  // which the extension also runs on without OVL_PIPELINE: nothing is overwritten early).
+  const uint64_t ACC_PAIRS = 4ull << 20, ACC_NODES = 1ull << 30;
+  auto acc_append = [&](const Unit *u, uint32_t nu_c, const Node *nodes, uint64_t nn_c,
+                        const PairRec *pairs, uint32_t np_c) -> int {
+    auto &A = c->acc;
+    if (A.nu + nu_c >= 0xFFFFFFF0ull || A.nn + nn_c >= 0xFFFFFFF0ull)
+      return fail(OVL_ERR_UNSUPPORTED, "extension accumulator past 2^32 entries");
+    if (A.units.n < A.nu + nu_c || A.pnodes.n < A.nn + nn_c || A.pairs.n < A.np + np_c) {
+      // growing moves the buffers: the pending extension (which reads them) must be done,
+      // and what the accumulator holds is carried over
+      HIPC(hipStreamSynchronize(xs));
+      HIPC(hipStreamSynchronize(s));
+      auto regrow = [&](auto &buf, uint64_t used, uint64_t need) -> int {
+        if (buf.n >= need && buf.p) return OVL_OK;
+        typename std::remove_reference<decltype(buf)>::type bigger;
+        if (bigger.alloc(std::max<uint64_t>(need, buf.n + buf.n / 2))) return -1;
+        if (used) HIPC(hipMemcpy(bigger.p, buf.p, used * sizeof(*buf.p), hipMemcpyDeviceToDevice));
+        std::swap(bigger.p, buf.p);
+        std::swap(bigger.n, buf.n);
+        return OVL_OK;
+      };
+      if (regrow(A.units, A.nu, A.nu + nu_c) || regrow(A.pnodes, A.nn, A.nn + nn_c) ||
+          regrow(A.pairs, A.np, A.np + np_c))
+        return fail(OVL_ERR_OOM, "extension accumulator (%llu nodes)",
+                    (unsigned long long)(A.nn + nn_c));
+    }
+    if (nu_c)
+      HIPC(hipMemcpyAsync(A.units.p + A.nu, u, sizeof(Unit) * nu_c, hipMemcpyDeviceToDevice, s));
+    if (nn_c)
+      HIPC(hipMemcpyAsync(A.pnodes.p + A.nn, nodes, sizeof(Node) * nn_c, hipMemcpyDeviceToDevice, s));
+    if (np_c) {
+      hipLaunchKernelGGL(k_append_pairs, dim3(std::min<uint32_t>((np_c + 255) / 256, 4096)),
+                         dim3(256), 0, s, pairs, np_c, (uint32_t)A.nu, (uint32_t)A.nn,
+                         A.pairs.p + A.np);
+      HIPC(hipGetLastError());
+    }
+    A.nu += nu_c;
+    A.nn += nn_c;
+    A.np += np_c;
+    return OVL_OK;
+  };
+  // Extend everything the accumulator holds; it is empty again for the next chunk (the
+  // stream orders the next appends after this launch's reads).
+  auto flush_acc = [&]() -> int {
+    if (int rc = collect(0)) return rc;
+    auto &A = c->acc;
+    const uint32_t np = (uint32_t)A.np;
+    slot_pairs[0] = np;
+    int rc = launch_ext(0, A.units.p, A.pairs.p, A.pnodes.p, np, (uint32_t)A.nu);
+    A.nu = A.nn = A.np = 0;
+    return rc;
+  };
   uint64_t chunk = 0;
   while (u0 < nu) {
     const int slot = pipe ? (int)(chunk & 1) : 0;
@@ -1353,7 +1640,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     auto &d_units = c->fb.units[slot];
     auto &d_pnodes = c->fb.pnodes[slot];
     auto &d_pairs = c->fb.pairs[slot];
-    auto &x_ctr = c->fb.xctr[slot];
     // batch by probe slots
     uint32_t u1 = u0;
     uint64_t wsum = 0;
@@ -1544,214 +1830,25 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     npairs_tot += npairs;
     nodes_tot += hc[2];                                  // pnodes_next: the lists' nodes
 
-    // ---- the extension of this chunk, queued on xs (the host does not wait for it) ----
-    nout_ub += 3ull * npairs;
-    if (int rc = ensure_out(nout_ub)) return rc;
-    ExtendArgs EA;
-    EA.R = c->reads();
-    EA.units = d_units.p;
-    EA.pairs = d_pairs.p;
-    EA.npairs = npairs;
-    EA.npairs_dev = nullptr;
-    EA.restore = 0;
-    EA.pnodes = d_pnodes.p;
-    EA.pair_next = x_ctr.p + 5;
-    EA.error_bound = c->d_error_bound.p;
-    EA.match_limit = c->d_match_limit.p;
-    EA.max_errors = c->max_errors;
-    EA.branch_match_value = c->branch_match_value;
-    EA.min_branch_tail_slope = c->min_branch_tail_slope;
-    EA.min_branch_end_dist = 20;
-    EA.partial = c->P.partial;
-    EA.unique = c->P.unique_olap_per_pair;
-    EA.min_olap_len = c->P.min_olap_len;
-    EA.use_hopeless = c->P.use_hopeless_check;
-    EA.k = (int32_t)k;
-    EA.filter_by_kmer_count = c->P.filter_by_kmer_count;
-    EA.minkmer_exp = exp(-1.0 * (double)k * c->P.max_erate);
-    EA.rows = d_rows.p;
-    EA.rowdir = d_rowdir.p;
-    EA.deltas = d_deltas.p;
-    EA.out = c->d_out.p;
-    EA.nout = c->fb.xnout.p;
-    EA.out_cap = (uint32_t)std::min<uint64_t>(c->d_out.n, 0xFFFFFFF0ull);
-    EA.stats = d_stats.p;
-    EA.window = window ? 1 : 0;
-    EA.overflow = x_ctr.p + 7;
-    EA.dbg = nullptr;
-    if (getenv("OVL_DEBUG")) {
-      if (!c->dbg.p) {
-        HIPC(hipStreamSynchronize(xs));
-        if (c->dbg.alloc(32)) return fail(OVL_ERR_OOM, "debug counters");
-        HIPC(hipMemsetAsync(c->dbg.p, 0, 256, xs));
-      }
-      EA.dbg = c->dbg.p;
+    // ---- the extension ----------------------------------------------------------------
+    // Default path: the chunk's chains go to the accumulator (c->acc) and are extended
+    // together once ACC_PAIRS pairs have gathered or the job ends, so a launch's tail (its
+    // last, longest pairs on few waves) is paid once per job rather than once per probe
+    // chunk and per hash batch (canu's small --hashbits batches made that tail most of a
+    // configs[4] rank's extension time).  -l (a unit's pairs in the reference's order) and
+    // OVL_PIPELINE extend each chunk as it comes, from the slot's own buffers.
+    if (!ordered && !pipe) {
+      if (int rc = acc_append(d_units.p, nc, d_pnodes.p, hc[2], d_pairs.p, npairs)) return rc;
+      if (c->acc.np >= ACC_PAIRS || c->acc.nn >= ACC_NODES)
+        if (int rc = flush_acc()) return rc;
+    } else {
+      if (int rc = launch_ext(slot, d_units.p, d_pairs.p, d_pnodes.p, npairs, nc)) return rc;
     }
-    EA.list = nullptr;
-    EA.defer = nullptr;
-    EA.ndefer = nullptr;
-    EA.olim = c->P.frag_olap_limit;
-    EA.nunits = nc;
-    EA.useg = nullptr;
-    EA.ord_slot = nullptr;
-    EA.ord_diag = nullptr;
-    EA.dkey = nullptr;
-    slot_pairs[slot] = npairs;
-    HIPC(hipMemsetAsync(x_ctr.p, 0, 64, xs));
-    if (npairs && ordered) {
-      // the reference's two pair orders per unit (see k_olim_keys): String_Olap_Space
-      // order and By_Diag_Sum order, by stable radix sorts
-      auto &fb = c->fb;
-      const int n = (int)npairs;
-      size_t t1 = 0, t2 = 0, t3 = 0;
-      HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, fb.okey.p, fb.okey2.p, fb.oa.p,
-                                              fb.ob.p, n, 0, 32, xs));
-      HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, fb.ok64a.p, fb.ok64b.p, fb.oa.p,
-                                              fb.ob.p, n, 0, 64, xs));
-      HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, fb.ucnt.p, fb.useg.p, (int)nc + 1, xs));
-      const size_t tmp = std::max(std::max(t1, t2), t3);
-      HIPC(hipStreamSynchronize(xs));
-      if (fb.okey.grow(npairs) || fb.okey2.grow(npairs) || fb.oa.grow(npairs) ||
-          fb.ob.grow(npairs) || fb.oidx.grow(npairs) || fb.oidx2.grow(npairs) ||
-          fb.ok64a.grow(npairs) || fb.ok64b.grow(npairs) || fb.dkey.grow(npairs) ||
-          fb.ucnt.grow((size_t)nc + 1) || fb.useg.grow((size_t)nc + 1) ||
-          fb.otmp.grow(std::max<size_t>(tmp, 1)))
-        return fail(OVL_ERR_OOM, "-l pair orders");
-      const dim3 grid(std::min<uint32_t>((npairs + 255) / 256, 4096)), blk(256);
-      HIPC(hipMemsetAsync(fb.ucnt.p, 0, 4ull * (nc + 1), xs));
-      // first-hit order: by ~tgt, then (stably) by (unit, diag_bgn)
-      hipLaunchKernelGGL(k_olim_keys, grid, blk, 0, xs, d_pairs.p, d_pnodes.p, npairs, (int32_t)k,
-                         fb.okey.p, fb.ok64a.p, fb.oa.p, fb.dkey.p, fb.ucnt.p);
-      HIPC(hipGetLastError());
-      HIPC(hipcub::DeviceScan::ExclusiveSum(fb.otmp.p, t3, fb.ucnt.p, fb.useg.p, (int)nc + 1, xs));
-      size_t tt = t1;
-      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.okey.p, fb.okey2.p, fb.oa.p,
-                                              fb.ob.p, n, 0, 32, xs));
-      hipLaunchKernelGGL(k_gather_u64, grid, blk, 0, xs, fb.ok64a.p, fb.ob.p, npairs, fb.ok64b.p);
-      tt = t2;
-      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64b.p, fb.ok64a.p, fb.ob.p,
-                                              fb.oa.p, n, 0, 64, xs));
-      // String_Olap_Space indices, then the order by (unit, index)
-      hipLaunchKernelGGL(k_olim_slots, dim3(std::min<uint32_t>((nc + 3) / 4, 8192)), blk, 0, xs,
-                         d_pairs.p, fb.oa.p, fb.useg.p, nc,
-                         c->first_iid - c->hash_bgn_iid, fb.ok64b.p, fb.ob.p);
-      HIPC(hipGetLastError());
-      tt = t2;
-      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64b.p, fb.ok64a.p, fb.ob.p,
-                                              fb.oidx.p, n, 0, 64, xs));       // oidx: ord_slot
-      // By_Diag_Sum: stably by the diagonal key, then stably by unit
-      hipLaunchKernelGGL(k_gather_u64, grid, blk, 0, xs, fb.dkey.p, fb.oidx.p, npairs, fb.ok64a.p);
-      tt = t2;
-      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.ok64a.p, fb.ok64b.p, fb.oidx.p,
-                                              fb.oa.p, n, 0, 64, xs));
-      hipLaunchKernelGGL(k_gather_unit, grid, blk, 0, xs, d_pairs.p, fb.oa.p, npairs, fb.okey.p);
-      tt = t1;
-      HIPC(hipcub::DeviceRadixSort::SortPairs(fb.otmp.p, tt, fb.okey.p, fb.okey2.p, fb.oa.p,
-                                              fb.oidx2.p, n, 0, 32, xs));      // oidx2: ord_diag
-      HIPC(hipGetLastError());
-      EA.useg = fb.useg.p;
-      EA.ord_slot = fb.oidx.p;
-      EA.ord_diag = fb.oidx2.p;
-      EA.dkey = fb.dkey.p;
-    }
-    if (npairs && !ordered) {
-      // the extension-only buffers are shared by the slots: regrowing one waits for xs
-      auto &fb = c->fb;
-      size_t tmp = 0;
-      HIPC(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, fb.okey.p, fb.okey2.p,
-                                                        fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
-                                                        32, xs));
-      if (fb.okey.n < npairs || fb.oidx.n < npairs || fb.okey2.n < npairs || fb.oidx2.n < npairs ||
-          d_defer.n < npairs || fb.defer2.n < npairs || fb.otmp.n < tmp || !fb.otmp.p) {
-        HIPC(hipStreamSynchronize(xs));
-        if (fb.okey.grow(npairs) || fb.oidx.grow(npairs) || fb.okey2.grow(npairs) ||
-            fb.oidx2.grow(npairs) || d_defer.grow(npairs) || fb.defer2.grow(npairs) ||
-            fb.otmp.grow(std::max<size_t>(tmp, 1)))
-          return fail(OVL_ERR_OOM, "work order");
-      }
-      if (npairs > 1) {
-        // longest-first work order (node count descending; ties keep pair order)
-        hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
-                           dim3(256), 0, xs, d_pairs.p, npairs, fb.okey.p, fb.oidx.p);
-        HIPC(hipGetLastError());
-        HIPC(hipcub::DeviceRadixSort::SortPairsDescending(fb.otmp.p, tmp, fb.okey.p, fb.okey2.p,
-                                                          fb.oidx.p, fb.oidx2.p, (int)npairs, 0,
-                                                          32, xs));
-        EA.list = fb.oidx2.p;
-      }
-    }
-    HIPC(hipEventRecord(c->xev[slot], xs));
-    if (npairs && ordered) {
-      EA.e_cap = gen.ecap;
-      EA.rows_cap = gen.stride;
-      EA.sw_words = 0;
-      EA.stage_len = 0;
-      EA.pair_next = x_ctr.p + 9;
-      n_ext_launch++;
-      if (gen.l16)
-        hipLaunchKernelGGL((k_extend<false, true, true>), dim3(gen.waves / gen.wpb),
-                           dim3(64 * gen.wpb), gen.lds, xs, EA);
-      else
-        hipLaunchKernelGGL((k_extend<false, false, true>), dim3(gen.waves / gen.wpb),
-                           dim3(64 * gen.wpb), gen.lds, xs, EA);
-      HIPC(hipGetLastError());
-    } else if (npairs) {
-      // the staged classes in turn, each deferring what it cannot take to the next list
-      // (whose length the next launch reads from the device counter); the generic kernel
-      // takes the last list, or every pair when no class exists
-      uint32_t *defer_buf[2] = {d_defer.p, c->fb.defer2.p};
-      for (size_t ci = 0; ci < ext_stage.size(); ci++) {
-        const ExtClass &g = ext_stage[ci];
-        EA.e_cap = g.ecap;
-        EA.rows_cap = g.stride;
-        EA.sw_words = g.sw;
-        EA.stage_len = (int32_t)g.len;
-        EA.pair_next = x_ctr.p + ctr_next[ci];
-        EA.defer = defer_buf[ci & 1];
-        EA.ndefer = x_ctr.p + ctr_defer[ci];
-        n_ext_launch++;
-        if (g.l16)
-          hipLaunchKernelGGL((k_extend<true, true>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
-        else
-          hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
-        HIPC(hipGetLastError());
-        EA.list = defer_buf[ci & 1];
-        EA.npairs_dev = x_ctr.p + ctr_defer[ci];
-        EA.restore = 1;          // a deferred pair may have had nodes removed (~Len)
-      }
-      EA.e_cap = gen.ecap;
-      EA.rows_cap = gen.stride;
-      EA.sw_words = 0;
-      EA.stage_len = 0;
-      EA.pair_next = x_ctr.p + 9;
-      EA.defer = nullptr;
-      EA.ndefer = nullptr;
-      // without the pipeline the host waits for this chunk next anyway: read the last
-      // class's defer count and skip an empty generic launch
-      bool gen_needed = true;
-      if (!pipe && !ext_stage.empty()) {
-        uint32_t nd = 0;
-        HIPC(hipMemcpyAsync(&nd, x_ctr.p + ctr_defer[ext_stage.size() - 1], 4,
-                            hipMemcpyDeviceToHost, xs));
-        HIPC(hipStreamSynchronize(xs));
-        gen_needed = nd > 0;
-      }
-      if (gen_needed) {
-        n_ext_launch++;
-        if (gen.l16)
-          hipLaunchKernelGGL((k_extend<false, true>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
-                             gen.lds, xs, EA);
-        else
-          hipLaunchKernelGGL((k_extend<false, false>), dim3(gen.waves / gen.wpb), dim3(64 * gen.wpb),
-                             gen.lds, xs, EA);
-        HIPC(hipGetLastError());
-      }
-    }
-    HIPC(hipEventRecord(c->xev[2 + slot], xs));
-    pending[slot] = true;
     chunk++;
     u0 += nc;
   }
+  if (flush && c->acc.np)
+    if (int rc = flush_acc()) return rc;
   for (int sl = 0; sl < 2; sl++)
     if (int rc = collect(sl)) return rc;
   {
@@ -1966,6 +2063,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   }
   memset(&c->stats, 0, sizeof(c->stats));
   c->nout = 0;
+  c->acc.nu = c->acc.nn = c->acc.np = 0;
   uint32_t bgn = g_bgn_hash;
   uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
   uint64_t batches = 0;
@@ -1979,8 +2077,11 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     end = loaded;
     batches++;
     if (any_ref) {
+      // the batches' pairs are extended together: the last batch flushes what is pending
       uint64_t n = 0;
-      if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n)))
+      const bool last_batch = !(end + 1 < g_end_hash);
+      if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n,
+                          last_batch)))
         return rc;
     }
     if (getenv("OVL_TIMING")) {
