@@ -246,18 +246,23 @@ struct KeyArgs {
   int32_t k;
   const uint64_t *koff;         // per read of the batch: its first key
   uint64_t sentinel;            // key of an invalid position (sorts after every real key)
-  uint64_t *keys;
+  void *keys;                   // K[]
+  uint32_t *vcnt;               // 32-bit keys: valid k-mers per read
   unsigned long long *kmers;
 };
 
+// K = uint32_t (2k <= 32): each read's keys are its codes, sorted per read (segmented
+// sort); K = uint64_t: read index << 2k | code, one sort over the batch.  4^k - 1 (all T)
+// is never a canonical code, so it can mark an invalid position in the 32-bit form.
+template <typename K>
 __global__ void __launch_bounds__(256) k_mh_kmer_keys(KeyArgs A) {
   const uint32_t ri = blockIdx.x, r = A.r0 + ri;
   const int32_t k = A.k;
   const uint8_t *s = A.bases + A.off[r];
   const int32_t L = (int32_t)A.len[r];
   const int32_t npos = L - k + 1;
-  uint64_t *out = A.keys + A.koff[ri];
-  const uint64_t hi = (uint64_t)ri << (2 * k);
+  K *out = (K *)A.keys + A.koff[ri];
+  const uint64_t hi = sizeof(K) == 8 ? ((uint64_t)ri << (2 * k)) : 0;
   unsigned long long nk = 0;
   for (int32_t base = 0; base < npos; base += 256 * RKK) {
     const int32_t p0 = base + (int32_t)threadIdx.x * RKK;
@@ -269,25 +274,36 @@ __global__ void __launch_bounds__(256) k_mh_kmer_keys(KeyArgs A) {
       const int32_t p = p0 + i;
       if (p < npos) {
         const bool ok = R.push(base_code(s[p + k - 1]));
-        out[p] = ok ? (hi | R.canon()) : A.sentinel;
+        out[p] = ok ? (K)(hi | R.canon()) : (K)A.sentinel;
         nk += ok;
       }
     }
   }
-  if (A.kmers) {
-    for (int s2 = 32; s2 > 0; s2 >>= 1) nk += __shfl_xor(nk, s2);
-    if ((threadIdx.x & 63) == 0 && nk) atomicAdd(A.kmers, nk);
+  for (int s2 = 32; s2 > 0; s2 >>= 1) nk += __shfl_xor(nk, s2);
+  if ((threadIdx.x & 63) == 0 && nk) {
+    if (A.kmers) atomicAdd(A.kmers, nk);
+    if (sizeof(K) == 4) atomicAdd(&A.vcnt[ri], (uint32_t)nk);
   }
 }
 
+// The -f multipliers as an open-addressing table (a binary search over the sorted codes
+// cost ~17 dependent loads per distinct k-mer): slot = splitmix64(code) & mask, linear
+// probing, empty slots hold FEMPTY (no 2k-bit code reaches it).
+constexpr uint64_t FEMPTY = ~0ull;
+struct FreqSlot {
+  uint64_t code;
+  double mult;
+};
+
 struct WSketchArgs {
-  const uint64_t *keys;         // sorted
+  const void *keys;             // K[], sorted (per read, or over the batch)
   uint64_t nkeys;
+  const uint64_t *koff;         // 32-bit keys: per read its first key ...
+  const uint32_t *vcnt;         // ... and its valid ones
   uint32_t r0, nreads;
   int32_t k, H;
-  const uint64_t *fcodes;       // -f k-mers (canonical, sorted) ...
-  const double *fmult;          // ... and their multipliers m(c)
-  uint32_t nf;
+  const FreqSlot *ftab;         // -f k-mers and their multipliers m(c), or null
+  uint64_t fmask;               // table slots - 1
   double dmult;                 // m(c) of every other k-mer
   int32_t no_tf;
   int32_t *minhash;             // [read][H]
@@ -304,7 +320,9 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t 
 }
 
 // Stage 1, weighted (oracle: mhap_oracle.sketch_weighted)
+template <typename K>
 __global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
+  const K *keys = (const K *)A.keys;
   extern __shared__ int32_t s_min[];               // [4 waves][H]
   __shared__ uint64_t s_rng[2];
   const uint32_t ri = blockIdx.x, r = A.r0 + ri;
@@ -313,8 +331,13 @@ __global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
   const uint64_t cmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1);
   for (int32_t j = tid; j < 4 * H; j += 256) s_min[j] = I32MAX;
   if (tid == 0) {
-    s_rng[0] = lower_bound_u64(A.keys, A.nkeys, (uint64_t)ri << (2 * k));
-    s_rng[1] = lower_bound_u64(A.keys, A.nkeys, (uint64_t)(ri + 1) << (2 * k));
+    if (sizeof(K) == 4) {
+      s_rng[0] = A.koff[ri];
+      s_rng[1] = A.koff[ri] + A.vcnt[ri];
+    } else {
+      s_rng[0] = lower_bound_u64((const uint64_t *)keys, A.nkeys, (uint64_t)ri << (2 * k));
+      s_rng[1] = lower_bound_u64((const uint64_t *)keys, A.nkeys, (uint64_t)(ri + 1) << (2 * k));
+    }
   }
   __syncthreads();
   const uint64_t s0 = s_rng[0], s1 = s_rng[1];
@@ -330,15 +353,18 @@ __global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
       W[i] = 0;
       const uint64_t p = p0 + i;
       if (p < s1) {
-        const uint64_t key = A.keys[p];
-        if (p == s0 || A.keys[p - 1] != key) {           // a run start: a distinct k-mer
+        const K key = keys[p];
+        if (p == s0 || keys[p - 1] != key) {             // a run start: a distinct k-mer
           uint64_t e = p + 1;
-          while (e < s1 && A.keys[e] == key) e++;
-          const uint64_t c = key & cmask;
+          while (e < s1 && keys[e] == key) e++;
+          const uint64_t c = (uint64_t)key & cmask;
           double m = A.dmult;
-          if (A.nf) {
-            const uint64_t q = lower_bound_u64(A.fcodes, A.nf, c);
-            if (q < A.nf && A.fcodes[q] == c) m = A.fmult[q];
+          if (A.ftab) {
+            for (uint64_t h = splitmix64(c) & A.fmask;; h = (h + 1) & A.fmask) {
+              const FreqSlot fs = A.ftab[h];
+              if (fs.code == c) { m = fs.mult; break; }
+              if (fs.code == FEMPTY) break;
+            }
           }
           const double tf = A.no_tf ? 1.0 : (double)(e - p);
           const double wf = floor(tf * m + 0.5);
@@ -854,8 +880,9 @@ struct mhap_ctx {
   // repeat weighting (mhap_set_kmer_frequencies): weighted sketch when repeat_weight >= 0
   mhap_weighting W{-1.0, 10.0, 1e-5, 0};
   bool weighted = false;
-  MBuf<uint64_t> fcodes, wkeys, wkeys2;
-  MBuf<double> fmult;
+  MBuf<uint64_t> wkeys, wkeys2;
+  MBuf<FreqSlot> ftab;
+  uint64_t fmask = 0;
   uint32_t nf = 0;
   double dmult = 1.0;
   MBuf<uint8_t> wsort_tmp;
@@ -1098,12 +1125,18 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   std::vector<double> m(codes.size());
   for (size_t i = 0; i < codes.size(); i++) m[i] = mult(idf[i]);
   c->dmult = mult(idf_max);
-  if (c->fcodes.alloc(codes.size()) || c->fmult.alloc(codes.size()))
-    return mfail(M_OOM, "k-mer frequency table");
-  if (!codes.empty()) {
-    MHC(hipMemcpy(c->fcodes.p, codes.data(), 8 * codes.size(), hipMemcpyHostToDevice));
-    MHC(hipMemcpy(c->fmult.p, m.data(), 8 * m.size(), hipMemcpyHostToDevice));
+  // open addressing at load <= 1/2
+  uint64_t slots = 16;
+  while (slots < 2 * codes.size() + 1) slots <<= 1;
+  std::vector<FreqSlot> tab(slots, FreqSlot{FEMPTY, 0.0});
+  for (size_t i = 0; i < codes.size(); i++) {
+    uint64_t h = splitmix64(codes[i]) & (slots - 1);
+    while (tab[h].code != FEMPTY) h = (h + 1) & (slots - 1);
+    tab[h] = FreqSlot{codes[i], m[i]};
   }
+  if (c->ftab.alloc(slots)) return mfail(M_OOM, "k-mer frequency table");
+  MHC(hipMemcpy(c->ftab.p, tab.data(), sizeof(FreqSlot) * slots, hipMemcpyHostToDevice));
+  c->fmask = slots - 1;
   c->nf = (uint32_t)codes.size();
   return M_OK;
 }
@@ -1113,9 +1146,13 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
 static int sketch_weighted(mhap_ctx *c, uint32_t r0, uint32_t nr) {
   hipStream_t s = c->stream;
   const uint32_t k = c->P.k;
-  const uint64_t WKEY_BUDGET = 1ull << 30;                  // 8 GB of keys per buffer
+  // k <= 16: 32-bit codes sorted per read (a segmented sort, 4 B per key); longer k-mers:
+  // 64-bit (read index, code) keys in one sort over the batch
+  const bool k32 = 2 * k <= 32;
+  const uint64_t WKEY_BUDGET = 1ull << 30;                  // keys per batch
   const uint32_t idx_bits = 64 - 2 * k;
-  const uint64_t max_reads = idx_bits >= 32 ? 0xFFFFFFF0ull : (1ull << idx_bits) - 2;
+  const uint64_t max_reads = k32 ? (1u << 20)
+                                 : (idx_bits >= 32 ? 0xFFFFFFF0ull : (1ull << idx_bits) - 2);
   for (uint32_t a = 0; a < nr;) {
     std::vector<uint64_t> koff;
     uint64_t tot = 0;
@@ -1128,31 +1165,56 @@ static int sketch_weighted(mhap_ctx *c, uint32_t r0, uint32_t nr) {
       tot += add;
       b++;
     }
+    koff.push_back(tot);                                    // the segments' end offsets
     const uint32_t nb = b - a;
-    const uint32_t end_bit = 2 * k + (uint32_t)std::max<int>(1, 64 - __builtin_clzll((uint64_t)nb + 1));
-    const uint64_t sentinel = end_bit >= 64 ? ~0ull : ((1ull << end_bit) - 1);
+    uint32_t end_bit;
+    uint64_t sentinel;
+    if (k32) {
+      end_bit = 2 * k;
+      sentinel = (1ull << (2 * k)) - 1;                     // never a canonical code
+    } else {
+      end_bit = 2 * k + (uint32_t)std::max<int>(1, 64 - __builtin_clzll((uint64_t)nb + 1));
+      sentinel = end_bit >= 64 ? ~0ull : ((1ull << end_bit) - 1);
+    }
+    const size_t ksz = k32 ? 4 : 8;
     MBuf<uint64_t> d_koff;
-    if (d_koff.alloc(nb) || c->wkeys.alloc(std::max<uint64_t>(tot, 1)) ||
-        c->wkeys2.alloc(std::max<uint64_t>(tot, 1)))
+    MBuf<uint32_t> d_vcnt;
+    const uint64_t kwords = (std::max<uint64_t>(tot, 1) * ksz + 7) / 8;
+    if (d_koff.alloc(nb + 1) || d_vcnt.alloc(nb) || c->wkeys.alloc(kwords) ||
+        c->wkeys2.alloc(kwords))
       return mfail(M_OOM, "weighted-sketch keys (%llu)", (unsigned long long)tot);
-    MHC(hipMemcpyAsync(d_koff.p, koff.data(), 8ull * nb, hipMemcpyHostToDevice, s));
+    MHC(hipMemcpyAsync(d_koff.p, koff.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
+    MHC(hipMemsetAsync(d_vcnt.p, 0, 4ull * nb, s));
     KeyArgs KA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)k, d_koff.p, sentinel,
-               c->wkeys.p, c->kctr.p};
-    hipLaunchKernelGGL(k_mh_kmer_keys, dim3(nb), dim3(256), 0, s, KA);
+               c->wkeys.p, d_vcnt.p, c->kctr.p};
+    if (k32) hipLaunchKernelGGL(k_mh_kmer_keys<uint32_t>, dim3(nb), dim3(256), 0, s, KA);
+    else     hipLaunchKernelGGL(k_mh_kmer_keys<uint64_t>, dim3(nb), dim3(256), 0, s, KA);
     MHC(hipGetLastError());
     size_t tb = 0;
-    // key counts can pass 2^31: the 64-bit-count form of the sort
-    MHC(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
-                                          (int)end_bit, s));
-    if (c->wsort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
-    MHC(hipcub::DeviceRadixSort::SortKeys(c->wsort_tmp.p, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
-                                          (int)end_bit, s));
-    WSketchArgs WA{c->wkeys2.p, tot, r0 + a, nb, (int32_t)k, (int32_t)c->P.num_hashes,
-                   c->nf ? c->fcodes.p : nullptr, c->nf ? c->fmult.p : nullptr, c->nf,
-                   c->dmult, c->W.no_tf, c->minhash.p};
-    hipLaunchKernelGGL(k_mh_sketch_w, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
+    if (k32) {
+      uint32_t *ki = (uint32_t *)c->wkeys.p, *ko = (uint32_t *)c->wkeys2.p;
+      MHC(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, ki, ko, (int)tot, (int)nb,
+                                                     d_koff.p, d_koff.p + 1, 0, (int)end_bit, s));
+      if (c->wsort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
+      MHC(hipcub::DeviceSegmentedRadixSort::SortKeys(c->wsort_tmp.p, tb, ki, ko, (int)tot, (int)nb,
+                                                     d_koff.p, d_koff.p + 1, 0, (int)end_bit, s));
+    } else {
+      // key counts can pass 2^31: the 64-bit-count form of the sort
+      MHC(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
+                                            (int)end_bit, s));
+      if (c->wsort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
+      MHC(hipcub::DeviceRadixSort::SortKeys(c->wsort_tmp.p, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
+                                            (int)end_bit, s));
+    }
+    WSketchArgs WA{c->wkeys2.p, tot, d_koff.p, d_vcnt.p, r0 + a, nb, (int32_t)k,
+                   (int32_t)c->P.num_hashes, c->nf ? c->ftab.p : nullptr, c->fmask, c->dmult,
+                   c->W.no_tf, c->minhash.p};
+    if (k32)
+      hipLaunchKernelGGL(k_mh_sketch_w<uint32_t>, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
+    else
+      hipLaunchKernelGGL(k_mh_sketch_w<uint64_t>, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
     MHC(hipGetLastError());
-    MHC(hipStreamSynchronize(s));                           // d_koff is freed here
+    MHC(hipStreamSynchronize(s));                           // d_koff / d_vcnt are freed here
     a = b;
   }
   return M_OK;

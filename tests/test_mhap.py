@@ -317,7 +317,7 @@ def test_gpu_sketch_rows_match_oracle(built, small):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "repeat_read"])
+@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "repeat_read", "k20"])
 def test_gpu_weighted_sketch_rows_match_oracle(built, variant):
     """The weighted MinHash rows in HBM (distinct k-mers by a radix sort, tf as run lengths,
     the -f multipliers) equal the restatement's, bit for bit."""
@@ -333,6 +333,9 @@ def test_gpu_weighted_sketch_rows_match_oracle(built, variant):
         P.no_tf = True
     if variant == "tf_only":
         P.repeat_weight = 1.0
+    if variant == "k20":                 # 64-bit (read, code) keys: one sort per batch
+        P.k = 20
+        freq = ([x + "ACGT" for x in freq[0]], freq[1])
     m = mhap.Mhap(P, device=0)
     m.load_reads(rs)
     m.set_kmer_frequencies(*freq)
