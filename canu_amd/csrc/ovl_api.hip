@@ -189,9 +189,7 @@ struct ovl_ctx {
   DBuf<uint64_t> d_occ, d_tmpM2;
   DBuf<Rec2> d_tmpR, d_midR;     // build scratch: coarse- and fine-bucketed records
   DBuf<TabEntry> d_tab;
-  DBuf<uint2> d_slice;           // per fine bucket: {first slot, slots}
-  uint32_t fine_bits = 0;
-  uint64_t tab_slots = 0;
+  uint32_t tab_bits = 0, slice_bits = 0;
 
   // find_overlaps working buffers: kept across calls (grow-only), hipMalloc of tens of
   // GB per call would cost seconds
@@ -784,63 +782,37 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
     HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
   }
-  // Table slices sized to their own fine bucket: 2 x its distinct k-mers + 1 slots (load
-  // <= 1/2).  Round 2 sized every slice as a power of two >= 2 x the LARGEST bucket's
-  // distinct k-mers: ~17 % load, 16 GiB at 50k x 10 kb, where random 16-B lookups run
-  // slower than over a smaller table (profiles/r02w_rand_ceiling.log); 2x the own bucket
-  // keeps the probe sequences as short as before while the table shrinks ~2.7x.
-  DBuf<uint32_t> ssize;
-  DBuf<uint64_t> sbase;
-  if (ssize.alloc(nfine) || sbase.alloc(nfine) || c->d_slice.alloc(nfine))
-    return fail(OVL_ERR_OOM, "table slices");
-  HIPC(hipMemsetAsync(misc.p + 3, 0, 4, s));
-  hipLaunchKernelGGL(k_slice_sizes, dim3((nfine + 3) / 4), dim3(256), 0, s, c->d_tmpM2.p,
-                     fstart.p, fcnt.p, nfine, ssize.p, misc.p + 3);
-  HIPC(hipGetLastError());
-  {
-    size_t tb = 0;
-    HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ssize.p, sbase.p, (int)nfine, s));
-    DBuf<uint8_t> tmp;
-    if (tmp.alloc(std::max<size_t>(tb, 1))) return fail(OVL_ERR_OOM, "slice scan");
-    HIPC(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ssize.p, sbase.p, (int)nfine, s));
-    uint64_t last_base = 0;
-    uint32_t last_size = 0;
-    HIPC(hipMemcpyAsync(&last_base, sbase.p + nfine - 1, 8, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(&last_size, ssize.p + nfine - 1, 4, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    c->tab_slots = last_base + last_size;
-  }
-  // slot indices are 32-bit (the slices' first slots)
-  if (c->tab_slots >= 0xFFFFFFF0ull)
-    return fail(OVL_ERR_UNSUPPORTED, "k-mer table of %llu slots, past 2^32; use a smaller -h range",
-                (unsigned long long)c->tab_slots);
-  const uint32_t smax = std::max<uint32_t>(hm[3], 1);
-  c->fine_bits = cb + fb;
-  if (c->d_tab.alloc(c->tab_slots)) return fail(OVL_ERR_OOM, "table (%llu slots)",
-                                                (unsigned long long)c->tab_slots);
-  hipLaunchKernelGGL(k_slice_meta, dim3(std::min<uint32_t>((nfine + 255) / 256, 8192)), dim3(256),
-                     0, s, ssize.p, sbase.p, nfine, c->d_slice.p);
+  uint32_t maxd = std::max<uint32_t>(hm[2], 1);
+#ifndef OVL_SLICE_Q
+#define OVL_SLICE_Q 8
+#endif
+  // slots per slice >= OVL_SLICE_Q / 4 x the largest fine bucket's distinct k-mers (and
+  // always more than it, so every probe sequence meets an empty slot).  2x: a denser table
+  // (1.25x / 1.5x: 16 -> 8 GB at 50k x 10 kb) builds 1.5 ms faster but lengthens the probe
+  // sequences, +2.7 ms in k_probe.  Slices sized to their OWN bucket (2 x distinct + 1,
+  // ~6 GB) were measured in round 3 too: k_probe 12.4 -> 22.2 ms per launch, since the
+  // per-slice {base, size} lookup is a second dependent random access per window
+  // (profiles/r03d_bench_perslice.json); not kept
+  c->slice_bits = std::max<uint32_t>(1, ceil_log2((uint64_t)OVL_SLICE_Q * maxd / 4 + 1));
+  c->tab_bits = cb + fb + c->slice_bits;
+  if (c->d_tab.alloc(1ull << c->tab_bits)) return fail(OVL_ERR_OOM, "table 2^%u", c->tab_bits);
   TableArgs T;
   T.M = c->d_tmpM2.p;
   T.P = c->d_occ.p;
   T.fstart = fstart.p;
   T.fcnt = fcnt.p;
   T.tab = c->d_tab.p;
-  T.slice = c->d_slice.p;
   T.nfine = nfine;
-  T.fine_bits = c->fine_bits;
-  T.smax = smax;
+  T.slice_bits = c->slice_bits;
+  T.tab_bits = c->tab_bits;
   T.len = c->d_len.p;
   T.rflags = c->d_flags.p;
   T.first_iid = c->first_iid;
   T.k = k;
-  uint32_t wpb = std::max<uint32_t>(1, std::min<uint32_t>(4, 65536u / (16u * smax)));
-  size_t lds = (size_t)wpb * 16u * smax;
-  if (lds > 160 * 1024) return fail(OVL_ERR_UNSUPPORTED, "k-mer slice too large (%u)", smax);
-  if (lds > 65536)
-    HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_table),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  uint32_t S = 1u << c->slice_bits;
+  uint32_t wpb = std::max<uint32_t>(1, std::min<uint32_t>(4, 65536u / (16u * S)));
+  size_t lds = (size_t)wpb * 16u * S;
+  if (lds > 65536) return fail(OVL_ERR_UNSUPPORTED, "k-mer slice too large (%u)", S);
   hipLaunchKernelGGL(k_table, dim3((nfine + wpb - 1) / wpb), dim3(64 * wpb), lds, s, T);
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(c->ev[1], s));
@@ -1096,9 +1068,9 @@ int ovl_build_hash_batch(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_hash_
 IndexDev index_dev(const ovl_ctx *c) {
   IndexDev X;
   X.tab = c->d_tab.p;
-  X.slice = c->d_slice.p;
   X.occ = c->d_occ.p;
-  X.fine_bits = c->fine_bits;
+  X.tab_bits = c->tab_bits;
+  X.slice_bits = c->slice_bits;
   X.k = c->P.kmer_len;
   X.kmask = (1ull << (2 * c->P.kmer_len)) - 1;
   return X;

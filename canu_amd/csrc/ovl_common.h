@@ -206,32 +206,24 @@ struct TabEntry {
 
 struct IndexDev {
   const TabEntry *tab;
-  const uint2    *slice;     // per fine bucket: {first slot, slots} of its table slice
   const uint64_t *occ;       // occurrence lists
-  uint32_t        fine_bits; // log2(fine buckets): the top bits of mix(kmer) pick the slice
+  uint32_t        tab_bits;  // log2(table size)
+  uint32_t        slice_bits;// log2(slots per slice)
   uint32_t        k;
   uint64_t        kmask;
 };
 
-// The home slot of key M in its slice of S slots: the 32 bits of M below the fine-bucket
-// bits, scaled onto [0, S) (slices are sized to their own k-mers, not a power of two).
-__device__ __forceinline__ uint32_t slice_home(uint64_t M, uint32_t fine_bits, uint32_t S) {
-  const uint32_t h = (uint32_t)(M >> (32 - fine_bits));
-  return (uint32_t)(((uint64_t)h * S) >> 32);
-}
-
 // The table is keyed by mix64(kmer); an empty slot has cnt == 0 (every filled slot has
-// the 0x40000000 "present" bit).  Linear probing stays inside the k-mer's slice, which
-// always holds an empty slot.
+// the 0x40000000 "present" bit).  Linear probing stays inside the k-mer's slice.
 __device__ __forceinline__ const TabEntry *index_find(const IndexDev &X, uint64_t kmer) {
-  const uint64_t M = mix64(kmer);
-  const uint2 sl = X.slice[M >> (64 - X.fine_bits)];
-  uint32_t i = slice_home(M, X.fine_bits, sl.y);
-  for (uint32_t n = 0; n < sl.y; n++) {
-    const TabEntry *e = X.tab + sl.x + i;
+  uint64_t M = mix64(kmer);
+  uint64_t slot0 = M >> (64 - X.tab_bits);
+  uint64_t smask = (1ull << X.slice_bits) - 1;
+  uint64_t base = slot0 & ~smask;
+  for (uint64_t i = 0; i <= smask; i++) {
+    const TabEntry *e = X.tab + (base | ((slot0 + i) & smask));
     if (e->cnt == 0) return nullptr;
     if (e->key == M) return e;
-    i = (i + 1 == sl.y) ? 0 : i + 1;
   }
   return nullptr;
 }

@@ -377,40 +377,13 @@ __global__ void k_fine_big(uint64_t *M, uint64_t *P, const uint32_t *big_list,
   if (threadIdx.x == 0) atomicMax(max_distinct, s_runs);
 }
 
-// Distinct k-mers per fine bucket (run starts of its sorted records) -> its table slice:
-// 2 x distinct + 1 slots (load <= 1/2, and always one empty slot to end a probe).
-__global__ void __launch_bounds__(256) k_slice_sizes(const uint64_t *M, const uint32_t *fstart,
-                                                      const uint32_t *fcnt, uint32_t nfine,
-                                                      uint32_t *size, uint32_t *max_size) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t f = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= nfine) return;
-  const uint32_t fs = fstart[f], fn = fcnt[f];
-  uint32_t runs = 0;
-  for (uint32_t i = lane; i < fn; i += 64)
-    runs += (i == 0 || M[fs + i] != M[fs + i - 1]) ? 1u : 0u;
-  for (int o = 32; o > 0; o >>= 1) runs += __shfl_xor(runs, o);
-  if (lane == 0) {
-    const uint32_t S = 2 * runs + 1;
-    size[f] = S;
-    atomicMax(max_size, S);
-  }
-}
-
-__global__ void k_slice_meta(const uint32_t *size, const uint64_t *base, uint32_t nfine,
-                             uint2 *slice) {
-  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < nfine; f += gridDim.x * blockDim.x)
-    slice[f] = make_uint2((uint32_t)base[f], size[f]);
-}
-
 struct TableArgs {
   const uint64_t *M, *P;         // sorted records
   const uint32_t *fstart, *fcnt;
   TabEntry *tab;
-  const uint2 *slice;            // per fine bucket: {first slot, slots}
-  uint32_t nfine;                // total fine buckets (2^fine_bits)
-  uint32_t fine_bits;
-  uint32_t smax;                 // largest slice: LDS per wave
+  uint32_t nfine;                // total fine buckets (2^(cb+fb))
+  uint32_t slice_bits;
+  uint32_t tab_bits;
   // screened-end marking for skip k-mers (Mark_Screened_Ends_Single, :147)
   const uint32_t *len;
   uint32_t *rflags;              // bit1 lfrag_end_screened, bit2 rfrag_end_screened
@@ -420,20 +393,20 @@ struct TableArgs {
 
 #define OVL_HOPELESS_MATCH 90
 
-// One wave per fine bucket -> its table slice, built in LDS and written whole.
+// One wave per fine bucket -> one table slice.
 __global__ void __launch_bounds__(256) k_table(TableArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t f = blockIdx.x * (blockDim.x >> 6) + wave;
-  uint64_t *key = (uint64_t *)smem + (size_t)wave * A.smax * 2;   // S keys then S (off,cnt)
-  uint32_t *oc = (uint32_t *)(key + A.smax);
+  uint32_t S = 1u << A.slice_bits;
+  uint64_t *key = (uint64_t *)smem + (size_t)wave * S * 2;     // S keys then S (off,cnt)
+  uint32_t *oc = (uint32_t *)(key + S);
   if (f >= A.nfine) return;
-  const uint2 sl = A.slice[f];
-  const uint32_t S = sl.y;
   for (uint32_t i = lane; i < S; i += 64) { key[i] = 0; oc[2 * i] = 0; oc[2 * i + 1] = 0; }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t fs = A.fstart[f], fn = A.fcnt[f];
+  uint32_t pshift = 64 - A.tab_bits;
   // Run starts come from one ballot per 64 records, with a virtual start at fn; a run ends
   // at the next start: in the same batch, in the next one (looked ahead), or -- for a run
   // longer than a batch -- found by the whole wave scanning on.
@@ -482,11 +455,11 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
         }
         while (cnt > 0 && A.P[off] == OVL_SKIP_POS) { off++; cnt--; }   // duplicate markers
       }
-      uint32_t slot = slice_home(M, A.fine_bits, S);
+      uint32_t slot = (uint32_t)(M >> pshift) & (S - 1);
       for (;;) {
         uint32_t old = atomicCAS(&oc[2 * slot + 1], 0u, (cnt | flags | OVL_PRESENT));
         if (old == 0) break;
-        slot = (slot + 1 == S) ? 0 : slot + 1;
+        slot = (slot + 1) & (S - 1);
       }
       key[slot] = M;
       oc[2 * slot] = off;
@@ -495,7 +468,7 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  TabEntry *dst = A.tab + sl.x;
+  TabEntry *dst = A.tab + ((size_t)f << A.slice_bits);
   for (uint32_t i = lane; i < S; i += 64) {
     TabEntry e;
     e.key = key[i];

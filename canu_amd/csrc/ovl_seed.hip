@@ -80,9 +80,9 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
 #define OVL_PROBE_PU 4
 #endif
   constexpr int PU = OVL_PROBE_PU;
-  const uint32_t fbits = A.X.fine_bits;
+  const uint64_t smask = (1ull << A.X.slice_bits) - 1;
   for (uint32_t o0 = 0; o0 < nw; o0 += 64 * PU) {
-    uint64_t M[PU];
+    uint64_t M[PU], slot0[PU];
     bool ok[PU];
 #pragma unroll
     for (int q = 0; q < PU; q++) {
@@ -90,31 +90,22 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
       ok[q] = o < nw && (int32_t)(o + A.k) <= L;
       if (ok[q] && bad) ok[q] = (mask_at(bad, (int32_t)o) & kbits) == 0;
       M[q] = 0;
-      if (ok[q]) M[q] = mix64(bases_at(S.w, (int32_t)o) & A.X.kmask);
+      slot0[q] = 0;
+      if (ok[q]) {
+        M[q] = mix64(bases_at(S.w, (int32_t)o) & A.X.kmask);
+        slot0[q] = M[q] >> (64 - A.X.tab_bits);
+      }
     }
-    // the windows' slices {first slot, slots} (a 8-B-per-fine-bucket array, mostly cache
-    // resident), then their home entries
-    uint2 sl[PU];
-#pragma unroll
-    for (int q = 0; q < PU; q++) {
-      sl[q] = make_uint2(0, 1);
-      if (ok[q]) sl[q] = A.X.slice[M[q] >> (64 - fbits)];
-    }
-    uint32_t slot0[PU];
     TabEntry e[PU];
 #pragma unroll
     for (int q = 0; q < PU; q++) {
       e[q].key = 0; e[q].off = 0; e[q].cnt = 0;
-      slot0[q] = 0;
-      if (ok[q]) {
-        slot0[q] = slice_home(M[q], fbits, sl[q].y);
-        e[q] = A.X.tab[sl[q].x + slot0[q]];
-      }
+      if (ok[q]) e[q] = A.X.tab[slot0[q]];
     }
     // finish each window with its values passed in: a loop over q holding the unbounded
     // probe loop is not unrolled, and its dynamically indexed arrays went to scratch (80 B
     // per lane, ~3x the records' bytes of write traffic)
-    auto finish = [&](uint32_t o, bool okq, uint64_t Mq, uint2 slq, uint32_t s0, TabEntry t) {
+    auto finish = [&](uint32_t o, bool okq, uint64_t Mq, uint64_t s0, TabEntry t) {
       if (o >= nw) return;
       Probe pr;
       pr.off = 0;
@@ -122,13 +113,12 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
       if (okq) {
         // index_find's linear probe within the slice, from the entry already loaded
         bool found = false;
-        uint32_t idx = s0;
-        for (uint32_t i = 1;; i++) {
+        const uint64_t base = s0 & ~smask;
+        for (uint64_t i = 1;; i++) {
           if (t.cnt == 0) break;
           if (t.key == Mq) { found = true; break; }
-          if (i >= slq.y) break;
-          idx = (idx + 1 == slq.y) ? 0 : idx + 1;
-          t = A.X.tab[slq.x + idx];
+          if (i > smask) break;
+          t = A.X.tab[base | ((s0 + i) & smask)];
         }
         if (found) {
           const uint32_t c = t.cnt;
@@ -148,15 +138,15 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
       out[o] = pr;
     };
     static_assert(PU == 4 || PU == 8, "finish() calls below");
-    finish(o0 + lane, ok[0], M[0], sl[0], slot0[0], e[0]);
-    finish(o0 + 64 + lane, ok[1], M[1], sl[1], slot0[1], e[1]);
-    finish(o0 + 128 + lane, ok[2], M[2], sl[2], slot0[2], e[2]);
-    finish(o0 + 192 + lane, ok[3], M[3], sl[3], slot0[3], e[3]);
+    finish(o0 + lane, ok[0], M[0], slot0[0], e[0]);
+    finish(o0 + 64 + lane, ok[1], M[1], slot0[1], e[1]);
+    finish(o0 + 128 + lane, ok[2], M[2], slot0[2], e[2]);
+    finish(o0 + 192 + lane, ok[3], M[3], slot0[3], e[3]);
     if constexpr (PU == 8) {
-      finish(o0 + 256 + lane, ok[4], M[4], sl[4], slot0[4], e[4]);
-      finish(o0 + 320 + lane, ok[5], M[5], sl[5], slot0[5], e[5]);
-      finish(o0 + 384 + lane, ok[6], M[6], sl[6], slot0[6], e[6]);
-      finish(o0 + 448 + lane, ok[7], M[7], sl[7], slot0[7], e[7]);
+      finish(o0 + 256 + lane, ok[4], M[4], slot0[4], e[4]);
+      finish(o0 + 320 + lane, ok[5], M[5], slot0[5], e[5]);
+      finish(o0 + 384 + lane, ok[6], M[6], slot0[6], e[6]);
+      finish(o0 + 448 + lane, ok[7], M[7], slot0[7], e[7]);
     }
   }
   for (int s = 32; s > 0; s >>= 1) {
