@@ -12,6 +12,10 @@
 //   k_log_write2      per wave 128-B rows of 2-B cells, 2 per step, own 1 MiB region
 //                     per wave (k_extend's row log)
 //   k_scatter_write16 random 16-B stores into a 4 GiB array                  (k_coarse_scatter)
+//   k_log_read2       per wave, 16-row windows of 64 2-B cells around a drifting column of
+//                     the rows k_log_write2 wrote (k_extend's traceback reads)
+//   k_lane_read4      per wave, lane-interleaved 4-B words of its own 64 KiB region (the
+//                     layout and width of k_extend's spill reloads from scratch)
 //
 // usage: calib_traffic            (then tools/calib_traffic.py turns the two PMC passes into
 //                                  profiles/calib_traffic.json)
@@ -82,6 +86,31 @@ __global__ void k_log_write2(uint16_t *log, uint32_t rows) {
   }
 }
 
+// the traceback: rows e-1 .. e-16 read at 64 cells around the walk's column, window by
+// window down to row 0
+__global__ void k_log_read2(const uint16_t *log, uint32_t rows, uint32_t *sink) {
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const uint16_t *r = log + (size_t)wave * rows * 512;
+  uint32_t acc = 0;
+  for (uint32_t e0 = rows; e0 >= 16; e0 -= 16) {
+    const uint32_t col = (e0 * 37u) & 511u;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+      acc += r[(size_t)(e0 - 1 - i) * 512 + ((col + lane) & 511)];
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// spill reloads: a wave's 64 KiB region as 256 words per lane, word j of lane l at
+// 64 * j + l (the private-segment swizzle), each read once
+__global__ void k_lane_read4(const uint32_t *a, uint32_t words, uint32_t *sink) {
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const uint32_t *r = a + (size_t)wave * words * 64;
+  uint32_t acc = 0;
+  for (uint32_t j = 0; j < words; j++) acc ^= r[64 * j + lane];
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 __global__ void k_scatter_write16(uint4 *a, uint64_t an, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x)
@@ -126,6 +155,22 @@ int main() {
   hipLaunchKernelGGL(k_log_write2, dim3(waves / 4), dim3(256), 0, 0, (uint16_t *)big, rows);
   printf("CALIB k_log_write2 read_bytes 0 write_bytes %llu\n",
          (unsigned long long)waves * rows * 256ull);
+  // reads of those rows (4 GiB written just before: past the 256 MiB Infinity Cache)
+  hipLaunchKernelGGL(k_log_read2, dim3(waves / 64), dim3(256), 0, 0, (const uint16_t *)big,
+                     rows / 16, sink);
+  hipLaunchKernelGGL(k_log_read2, dim3(waves / 4), dim3(256), 0, 0, (const uint16_t *)big, rows,
+                     sink);
+  printf("CALIB k_log_read2 read_bytes %llu write_bytes 0\n",
+         (unsigned long long)waves * rows * 128ull);
+
+  // spill-reload layout over the 8 GiB table region (cold), 64 KiB per wave
+  const uint32_t lw = 256, lwaves = (uint32_t)(8 * GiB / (64ull * 1024));   // 131072 waves
+  hipLaunchKernelGGL(k_lane_read4, dim3(lwaves / 256), dim3(256), 0, 0, (const uint32_t *)table,
+                     lw, sink);
+  hipLaunchKernelGGL(k_lane_read4, dim3(lwaves / 4), dim3(256), 0, 0, (const uint32_t *)table, lw,
+                     sink);
+  printf("CALIB k_lane_read4 read_bytes %llu write_bytes 0\n",
+         (unsigned long long)lwaves * lw * 256ull);
 
   const uint64_t ns = 256ull << 20;                // 256 M random 16-B stores
   hipLaunchKernelGGL(k_scatter_write16, grid, block, 0, 0, big, n16, ns / 64);

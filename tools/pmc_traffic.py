@@ -10,7 +10,11 @@ tools/calib_traffic.hip (profiles/calib_traffic.json): coalesced streaming reads
 reported at half their bytes (r = 2, as MI355X_MICROARCH.md documents), random 16-B loads
 (k_probe's table probes) at 64 B each -- one 64-B request, r = 1.  WRITE_SIZE reads the
 bytes of streaming stores exactly (calibrated 1.00) and counts a scattered 16-B store as
-the 32 B it writes (2.00), so it is taken as is.
+the 32 B it writes (2.00), so it is taken as is.  k_extend's own read patterns were
+calibrated in round 3: its spill reloads (lane-interleaved 4-B words, k_lane_read4) report
+0.50 of their bytes, like a coalesced stream, and its traceback's 2-B row-log reads
+(k_log_read2) 0.88 -- a 128-B row read touching a second line half the time -- so r = 2
+holds for k_extend too (profiles/calib_traffic.json).
 
     python tools/pmc_traffic.py <tag> [the bench.py arguments of the profiled run]
 
