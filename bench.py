@@ -158,7 +158,12 @@ def main() -> None:
 
     seed_only = job.seed_only() if world == 1 and not args.no_seed_only else None
     shard = job.shard_timing(ms_step) if world == 1 and not args.no_shard_timing else None
-    xgmi = job.index_allgather_timing(torch) if world > 1 and backend == "nccl" else None
+    xgmi = None
+    if world > 1 and backend == "nccl":
+        try:
+            xgmi = job.index_allgather_timing(torch)
+        except Exception as e:          # a side measurement: never lose the bench line to it
+            xgmi = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "configs2":
