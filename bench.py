@@ -268,11 +268,12 @@ class Configs2:
         same = all(np.isclose(float(gw[k]), float(mine[k])) for k in
                    ("reads", "read_len", "coverage", "read_error", "seed", "k", "maxerate",
                     "minlength"))
-        if not same:
-            return {"checked": False, "reason": "workload differs from the digest's"}
         t0 = time.time()
         rec = self.oic.fetch()
         mh = digest.multiset_hash(rec)
+        if not same:       # still fingerprinted, so library variants can be compared
+            return {"checked": False, "reason": "workload differs from the digest's",
+                    "records": int(rec.shape[0]), "multiset_hash": f"{mh:016x}"}
         # the multiset hash adds up over the ranks' disjoint query shards; the sum is taken
         # as two 32-bit halves so the int64 all-reduce cannot overflow
         lo = int(reduce(mh & 0xFFFFFFFF, SUM, torch.int64))

@@ -1228,7 +1228,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         return -1;
     // persistent grid: as many blocks as are resident at once (registers and LDS), so no
     // block starts only after the work queue has drained; within the scratch budget
-    uint32_t waves = 24u * c->n_cu;
+    uint32_t waves = 4u * OVL_EXT_OCC * c->n_cu;
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kfn, 64 * g.wpb, g.lds) == hipSuccess &&
         bpc > 0)
@@ -1245,7 +1245,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // longest loaded read inside its tier, so its scratch (and a short-read job's launch) is
   // exactly what a job without the longer reads would get.
   {
-    const size_t tier_cap[3] = {52 * 1024, 52 * 1024, 160 * 1024};
+    const size_t tier_cap[3] = {OVL_EXT_OCC == 8 ? 40 * 1024 : 52 * 1024, 52 * 1024, 160 * 1024};
     const uint32_t tier_wpb[3] = {8, 6, 1};
     uint32_t prev = 0;
     for (int t = 0; t < 3; t++) {

@@ -1693,8 +1693,11 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
 // L16, generic kernel: GR -- the rows and the Edit_Match_Limit table stay in global memory
 // (error limits past what a CU's LDS holds; see wave_ped).
 // ORD (with STAGE = false): the -l kernel, one unit per wave (see ExtendArgs.olim).
+#ifndef OVL_EXT_OCC
+#define OVL_EXT_OCC 6            // waves per SIMD the staged kernel is compiled for
+#endif
 template <bool STAGE, bool L16, bool ORD = false>
-__global__ void __launch_bounds__(512, 6) k_extend(ExtendArgs X) {
+__global__ void __launch_bounds__(512, OVL_EXT_OCC) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;

@@ -8,8 +8,8 @@ mkdir -p $R/gpurun_out
 for pass in 1 2; do
   for f in $R/canu_amd/lib/ab_*.so; do
     n=$(basename $f .so)
-    CANU_OVL_LIB=$f timeout -k 10 240 python $R/bench.py --reads ${AB_READS:-10000} --steps ${AB_STEPS:-3} --warmup 1 --no-cpu-baseline > $R/gpurun_out/ab_run_$n.log 2>&1 || exit 1
-    echo "$pass $n $(grep -o "\"ms_per_step\": [0-9.]*" $R/gpurun_out/ab_run_$n.log) $(grep -o "\"breakdown_ms\": {[^}]*}" $R/gpurun_out/ab_run_$n.log)"
+    CANU_OVL_LIB=$f timeout -k 10 240 python $R/bench.py --reads ${AB_READS:-10000} --steps ${AB_STEPS:-3} --warmup 1 --no-cpu-baseline ${AB_ARGS:-} > $R/gpurun_out/ab_run_$n.log 2>&1 || exit 1
+    echo "$pass $n $(grep -o "\"multiset_hash\": \"[0-9a-f]*\"" $R/gpurun_out/ab_run_$n.log) $(grep -o "\"ms_per_step\": [0-9.]*" $R/gpurun_out/ab_run_$n.log) $(grep -o "\"breakdown_ms\": {[^}]*}" $R/gpurun_out/ab_run_$n.log)"
   done
 done
 [ "${AB_PMC:-0}" = 1 ] || exit 0
