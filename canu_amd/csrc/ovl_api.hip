@@ -754,11 +754,25 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
     while (cap < 2 * mean && cap < 1024) cap <<= 1;
     F.cap = cap;
   }
-  const size_t fine_lds = 2ull * OVL_FINE_WAVES * F.cap * 8 + 2ull * nfb * 4;
-  if (fine_lds > 65536)
-    HIPC(hipFuncSetAttribute(reinterpret_cast<const void *>(k_fine),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)fine_lds));
-  hipLaunchKernelGGL(k_fine, dim3(ncb), dim3(OVL_FINE_WAVES * 64), fine_lds, s, F);
+  {
+    // the sort phase: runs grouped in an LDS hash table, records in registers (cap / 64 per
+    // lane); bitonic sorts when the grouped layout would not fit a CU's LDS (cap 1024) or
+    // when OVL_FINE_BITONIC=1 (A/B)
+    const char *fb_env = getenv("OVL_FINE_BITONIC");
+    const bool group = !(fb_env && atoi(fb_env)) &&
+                       fine_lds_bytes(true, nfb, F.cap) + 256 <= 160 * 1024;
+    const size_t fine_lds = fine_lds_bytes(group, nfb, F.cap);
+    const void *kf =
+        !group           ? reinterpret_cast<const void *>(k_fine<1, false>)
+        : F.cap <= 64    ? reinterpret_cast<const void *>(k_fine<1, true>)
+        : F.cap <= 128   ? reinterpret_cast<const void *>(k_fine<2, true>)
+        : F.cap <= 256   ? reinterpret_cast<const void *>(k_fine<4, true>)
+                         : reinterpret_cast<const void *>(k_fine<8, true>);
+    if (fine_lds > 65536)
+      HIPC(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fine_lds));
+    void *kargs[] = {&F};
+    HIPC(hipLaunchKernel(kf, dim3(ncb), dim3(OVL_FINE_WAVES * 64), kargs, fine_lds, s));
+  }
   HIPC(hipGetLastError());
   uint32_t hm[4];
   HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));

@@ -203,6 +203,98 @@ __device__ void wave_bitonic(uint64_t *sM, uint64_t *sP, uint32_t n2, uint32_t l
   }
 }
 
+// Wave-level grouping of one fine bucket (fn <= H records, H a power of two >= 64):
+// every k-mer's records become one contiguous run in position-descending order -- the order
+// Hash_Insert chains them (Build_Hash_Index.C:296-341) -- with the runs in the slot order of
+// an LDS hash table over the bucket's keys.  The index only needs each k-mer's run
+// contiguous and ordered (k_table maps a key to its run, k_first_reads reads a run's last
+// record), not the runs ordered by key, so this replaces a comparison sort of the bucket
+// (28-36 compare-exchange stages of LDS traffic) with one insert per record, a scan over the
+// slots and a rank within the record's own run.  Returns the number of distinct keys.
+//   kT: H u64 keys, cT: H u32 counts -> run starts, sP: H u64 staged positions.
+template <int EM>
+__device__ uint32_t wave_group_runs(const Rec2 *__restrict__ in, uint64_t *__restrict__ outM,
+                                    uint64_t *__restrict__ outP, uint32_t fn, uint32_t H,
+                                    uint64_t *kT, uint32_t *cT, uint64_t *sP, uint64_t empty,
+                                    uint32_t lane) {
+  for (uint32_t i = lane; i < H; i += 64) { kT[i] = empty; cT[i] = 0; }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint64_t m[EM], p[EM];
+  uint32_t sa[EM];                               // slot | arrival << 16
+#pragma unroll
+  for (int e = 0; e < EM; e++) {
+    const uint32_t i = lane + 64u * e;
+    m[e] = empty;
+    p[e] = 0;
+    if (i < fn) { const Rec2 r = in[i]; m[e] = r.m; p[e] = r.p; }
+  }
+#pragma unroll
+  for (int e = 0; e < EM; e++) {
+    sa[e] = 0;
+    if (lane + 64u * e < fn) {
+      uint32_t s = (uint32_t)m[e] & (H - 1);     // low bits of the mix: the bucket fixes the top
+      for (;;) {
+        const unsigned long long old =
+            atomicCAS((unsigned long long *)&kT[s], (unsigned long long)empty,
+                      (unsigned long long)m[e]);
+        if (old == empty || old == m[e]) break;
+        s = (s + 1) & (H - 1);
+      }
+      sa[e] = s | (atomicAdd(&cT[s], 1u) << 16);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // run starts: exclusive scan of the counts in slot order (each lane H/64 slots)
+  const uint32_t per = H >> 6, b0 = lane * per;
+  uint32_t run = 0, distinct = 0;
+  for (uint32_t j = 0; j < per; j++) {
+    const uint32_t c = cT[b0 + j];
+    run += c;
+    distinct += c ? 1u : 0u;
+  }
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (lane >= (uint32_t)o) inc += v;
+  }
+  uint32_t acc = inc - run;
+  for (uint32_t j = 0; j < per; j++) {
+    const uint32_t c = cT[b0 + j];
+    cT[b0 + j] = acc;
+    acc += c;
+  }
+  for (int o = 32; o > 0; o >>= 1) distinct += __shfl_xor(distinct, o);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+  for (int e = 0; e < EM; e++)
+    if (lane + 64u * e < fn) sP[cT[sa[e] & 0xffffu] + (sa[e] >> 16)] = p[e];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // rank within the run: positions descending; equal positions (repeated skip markers) by
+  // arrival
+#pragma unroll
+  for (int e = 0; e < EM; e++) {
+    if (lane + 64u * e < fn) {
+      const uint32_t s = sa[e] & 0xffffu, a = sa[e] >> 16;
+      const uint32_t b = cT[s], end = (s + 1 < H) ? cT[s + 1] : fn;
+      uint32_t rank = 0;
+      for (uint32_t j = b; j < end; j++) {
+        const uint64_t q = sP[j];
+        rank += (q > p[e] || (q == p[e] && j - b < a)) ? 1u : 0u;
+      }
+      outM[b + rank] = m[e];
+      outP[b + rank] = p[e];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  return distinct;
+}
+
 #define OVL_FINE_WAVES  8
 #define OVL_FB_MAX      4096
 #ifndef OVL_FINE_PSCAN
@@ -223,14 +315,27 @@ struct FineArgs {
                                  // buckets go to k_fine_big
 };
 
+// LDS of k_fine: the fine split's bins (h, cur: nf u32 each) and, after it, the waves' sort
+// buffers.  Grouped runs (GROUP): per wave [kT: cap u64][sP: cap u64][cT: cap u32], overlaid
+// on the bins (the sort phase takes its buckets' bounds from fstart / fcnt); bitonic:
+// [sM: 8 x cap u64][sP: 8 x cap u64] then the bins.
+__host__ __device__ inline size_t fine_lds_bytes(bool group, uint32_t nf, uint32_t cap) {
+  if (group) {
+    const size_t sort = (size_t)OVL_FINE_WAVES * cap * 20, bins = (size_t)nf * 8;
+    return sort > bins ? sort : bins;
+  }
+  return 2ull * OVL_FINE_WAVES * cap * 8 + 2ull * nf * 4;
+}
+
+template <int EM, bool GROUP>
 __global__ void __launch_bounds__(OVL_FINE_WAVES * 64)
 k_fine(FineArgs A) {
   // dynamic LDS sized to the fine buckets (2^fb bins, cap records per wave) so that
-  // several blocks share a CU: [sM: 8 x cap u64][sP: 8 x cap u64][h: nf u32][cur: nf u32]
+  // several blocks share a CU (fine_lds_bytes)
   extern __shared__ uint64_t s_fine[];
   uint32_t nf = 1u << A.fb_bits;
   const uint32_t cap = A.cap;
-  uint32_t *h = (uint32_t *)(s_fine + 2 * OVL_FINE_WAVES * cap);
+  uint32_t *h = GROUP ? (uint32_t *)s_fine : (uint32_t *)(s_fine + 2 * OVL_FINE_WAVES * cap);
   uint32_t *cur = h + nf;
   uint32_t cb = blockIdx.x;
   uint32_t n = A.ccnt[cb], s0 = A.cstart[cb];
@@ -285,15 +390,23 @@ k_fine(FineArgs A) {
   __syncthreads();
 
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t *kT = s_fine + (size_t)wave * (2 * cap + cap / 2);
+  uint64_t *sPw = kT + cap;
+  uint32_t *cT = (uint32_t *)(sPw + cap);
+  // no stored key has the bucket's top bits flipped
+  const uint64_t empty = ~(((uint64_t)cb) << (64 - A.cb_bits)) & (~0ull << (64 - A.cb_bits));
   uint64_t *wM = s_fine + (size_t)wave * cap, *wP = s_fine + (size_t)(OVL_FINE_WAVES + wave) * cap;
   __shared__ uint32_t s_runmax;                  // distinct k-mers of the block's largest bucket
   if (threadIdx.x == 0) s_runmax = 0;
   __syncthreads();
   uint32_t wave_max_runs = 0;
   for (uint32_t f = wave; f < nf; f += OVL_FINE_WAVES) {
-    uint32_t fn = h[f];
+    // grouped: the bins are overwritten by the sort buffers, bounds from the global copies;
+    // bitonic: cur[] now holds the fine bucket end
+    const uint32_t fn = GROUP ? __builtin_amdgcn_readfirstlane(A.fcnt[cb * nf + f]) : h[f];
     if (fn == 0) continue;
-    uint32_t fs = s0 + cur[f] - fn;              // cur[] now holds the fine bucket end
+    const uint32_t fs = GROUP ? __builtin_amdgcn_readfirstlane(A.fstart[cb * nf + f])
+                              : s0 + cur[f] - fn;
     if (fn > cap) {
       // too large for the LDS sort: copy out unsorted, k_fine_big sorts it in place
       for (uint32_t i = lane; i < fn; i += 64) {
@@ -306,6 +419,14 @@ k_fine(FineArgs A) {
         A.big_list[2 * j] = fs;
         A.big_list[2 * j + 1] = fn;
       }
+      continue;
+    }
+    if constexpr (GROUP) {
+      uint32_t H = 64;
+      while (H < 2 * fn && H < cap) H <<= 1;
+      const uint32_t runs = wave_group_runs<EM>(A.midR + fs, A.outM + fs, A.outP + fs, fn, H,
+                                                kT, cT, sPw, empty, lane);
+      wave_max_runs = runs > wave_max_runs ? runs : wave_max_runs;
       continue;
     }
     uint32_t n2 = 1;
