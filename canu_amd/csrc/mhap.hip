@@ -22,6 +22,7 @@
 //                  LDS), vote the orientation, radix-select the median offset, count the
 //                  sketch entries inside the implied overlap, Jaccard -> Mash distance.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -389,20 +390,44 @@ __global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
         if (!((vm >> i) & 1u)) { XL[i] = l0; XH[i] = h0; W[i] = w0; }
     }
     const bool live = vm != 0;
-    for (int32_t j = 0; j < H; j++) {
-      int32_t m = I32MAX;
+    // The draws per slot are a per-lane loop; when every live slot of the wave has the same
+    // small weight (w = 2: a distinct k-mer at the default multiplier r + (1 - r) X = 1.9,
+    // canu's case; or w = 1) the draws are straight-line code instead (no exec-mask loop
+    // per slot and function)
+    bool all1 = true, all2 = true;
 #pragma unroll
-      for (int i = 0; i < RKW; i++) {
-        for (int32_t t = 0; t < W[i]; t++) {
-          xs64(XL[i], XH[i]);
-          const int32_t v = (int32_t)XL[i];
-          m = v < m ? v : m;
+    for (int i = 0; i < RKW; i++) { all1 &= W[i] == 1; all2 &= W[i] == 2; }
+    const int32_t wu = __builtin_amdgcn_ballot_w64(live && !all2) == 0 ? 2
+                     : __builtin_amdgcn_ballot_w64(live && !all1) == 0 ? 1 : 0;
+    auto run = [&](auto wc) {
+      constexpr int WC = decltype(wc)::value;
+      for (int32_t j = 0; j < H; j++) {
+        int32_t m = I32MAX;
+#pragma unroll
+        for (int i = 0; i < RKW; i++) {
+          if constexpr (WC > 0) {
+#pragma unroll
+            for (int t = 0; t < WC; t++) {
+              xs64(XL[i], XH[i]);
+              const int32_t v = (int32_t)XL[i];
+              m = v < m ? v : m;
+            }
+          } else {
+            for (int32_t t = 0; t < W[i]; t++) {
+              xs64(XL[i], XH[i]);
+              const int32_t v = (int32_t)XL[i];
+              m = v < m ? v : m;
+            }
+          }
         }
+        m = live ? m : I32MAX;
+        m = wave_min(m);
+        if (lane == 0 && m < wm[j]) wm[j] = m;
       }
-      m = live ? m : I32MAX;
-      m = wave_min(m);
-      if (lane == 0 && m < wm[j]) wm[j] = m;
-    }
+    };
+    if (wu == 2)      run(std::integral_constant<int, 2>());
+    else if (wu == 1) run(std::integral_constant<int, 1>());
+    else              run(std::integral_constant<int, 0>());
   }
   __syncthreads();
   for (int32_t j = tid; j < H; j += 256) {
