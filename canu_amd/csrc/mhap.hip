@@ -237,7 +237,10 @@ __global__ void __launch_bounds__(256) k_mh_sketch(SketchArgs A) {
 //                   the run length and the -f table, then the sketch loop of k_mh_sketch
 //                   with w draws per slot and function
 constexpr int RKK = 16;           // positions per thread in k_mh_kmer_keys
-constexpr int RKW = 16;           // distinct k-mers per thread per round in k_mh_sketch_w
+#ifndef MH_RKW
+#define MH_RKW 8
+#endif
+constexpr int RKW = MH_RKW;       // distinct k-mers per thread per round in k_mh_sketch_w
 
 struct KeyArgs {
   const uint8_t *bases;
@@ -702,18 +705,24 @@ __global__ void __launch_bounds__(128) k_mh_compare(CmpArgs A) {
     const uint64_t *bg = A.ordered + (size_t)t * S;
     for (uint32_t i = lane; i < nb; i += 64) bk[i] = bg[i];
     wave_sync();
-    // shared entries, in A's order
+    // shared entries (each A entry with the first B entry of its hash; the median and the
+    // counts below only need them as a set): lane l merges its own run of A,
+    // A[l c .. l c + c), against B from one binary search for the run's first hash -- about
+    // c + nb / 64 LDS reads per lane instead of a binary search (log2 nb reads) per entry
     uint32_t nsh = 0, nsame = 0;
-    for (uint32_t i0 = 0; i0 < na; i0 += 64) {
-      const uint32_t i = i0 + lane;
+    const uint32_t crun = (na + 63) / 64;
+    const uint32_t a_lo = lane * crun, a_hi = a_lo + crun < na ? a_lo + crun : na;
+    uint32_t bp = a_lo < a_hi ? lds_lower_bound_hash(bk, nb, (uint32_t)(ak[a_lo] >> 32)) : nb;
+    for (uint32_t st = 0; st < crun; st++) {
+      const uint32_t i = a_lo + st;
       bool found = false, same = false;
       uint32_t pa = 0, pb = 0;
-      if (i < na) {
+      if (i < a_hi) {
         const uint64_t ka = ak[i];
         const uint32_t h = (uint32_t)(ka >> 32);
-        const uint32_t ix = lds_lower_bound_hash(bk, nb, h);
-        if (ix < nb && (uint32_t)(bk[ix] >> 32) == h) {
-          const uint64_t kb = bk[ix];
+        while (bp < nb && (uint32_t)(bk[bp] >> 32) < h) bp++;
+        if (bp < nb && (uint32_t)(bk[bp] >> 32) == h) {
+          const uint64_t kb = bk[bp];
           found = true;
           pa = (uint32_t)(ka >> 1) & 0x7FFFFFFFu;
           pb = (uint32_t)(kb >> 1) & 0x7FFFFFFFu;
