@@ -1232,7 +1232,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         int nb = atoi(bp);
         if (nb > 0) g.lds = std::max<size_t>(g.lds, (160 * 1024) / nb - 256);
       }
-    uint64_t st = (uint64_t)(g.ecap + 2) * 64 * OVL_RJ / (g.l16 ? 2 : 1);   // the row log
+    uint64_t st = (uint64_t)(g.ecap + 2) * OVL_LOGW / (g.l16 ? 2 : 1);   // the row log
     if (window) st = std::max<uint64_t>(st, 3ull * (g.ecap + 9) + 2ull * L + 64);
     g.stride = (st + 63) & ~63ull;
     const void *kfn = g.l16 ? reinterpret_cast<const void *>(k_extend<true, true>)

@@ -441,7 +441,11 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 // forward.C:170 writes around the band, so the neighbours d-1 / d+1 come from DPP wave
 // shifts with no LDS round trip.  Row e is logged band-compact as [nl-2, nr+2] (masked)
 // for the traceback.
+#ifndef OVL_RJ
 #define OVL_RJ 8
+#endif
+#define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
+static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 
 #ifdef OVL_PROFILE
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -552,7 +556,7 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
                                                     int32_t tb_d, int32_t last, int32_t *dst,
                                                     uint32_t lane, int32_t &last_out,
                                                     int32_t &nd_out) {
-  constexpr int W = 64 * OVL_RJ;               // cells per logged row, cell = d mod W
+  constexpr int W = OVL_LOGW;                  // cells per logged row, cell = d mod W
   // rows per window (lanes cover dc-31..dc+31): 16 keeps the unrolled walk and its code
   // registers within wave_ped_reg's 80 VGPRs (24 spills; 16 vs 24: -1 % extension time)
   constexpr int TBR = 16;
@@ -681,7 +685,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   int32_t max_score_len = 0, max_score_best_e = 0;
   // Max_Score_Best_d is kept as the row key and window base it decodes from (decoded once,
   // after the loop): B + 64J-1 - (key & 64J-1)
-  int32_t ms_key = 64 * J - 1, ms_B = 0;
+  int32_t ms_key = (1 << 9) - 1, ms_B = 0;
   int32_t longest = 0;
   int32_t pl = 0, pr = 0;
   int32_t tb_e = -1, tb_d = 0, tb_last = 0;
@@ -705,13 +709,13 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   // of the next row would wait for the log stores too
   typedef __attribute__((address_space(1))) cell_t g_cell_t;
   g_cell_t *clog = uni_ptr((g_cell_t *)rows);     // scalar base: stores use saddr + offset
-  clog[(B + (int32_t)lane) & (64 * J - 1)] = (cell_t)R[0];
+  clog[(B + (int32_t)lane) & (OVL_LOGW - 1)] = (cell_t)R[0];
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
   constexpr int JU = 1;
-  constexpr int WB = 9;                        // log2(64 * J): window offset bits of a key
-  static_assert(64 * J == (1 << WB), "key layout assumes a 512-diagonal window");
-  const int32_t lkey = 64 * J - 1 - (int32_t)lane;
+  constexpr int WB = 9;                        // window offset bits of a key
+  static_assert(64 * J <= (1 << WB), "key layout assumes a window of at most 512 diagonals");
+  const int32_t lkey = (1 << WB) - 1 - (int32_t)lane;
 
   int32_t e = 1;
   bool ended = false;
@@ -906,7 +910,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
     int32_t kmx = NEG;
     const uint32_t kspan = (uint32_t)(nr - nl);
     const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
-    g_cell_t *crow = clog + (size_t)e * (64 * J);
+    g_cell_t *crow = clog + (size_t)e * OVL_LOGW;
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jrs) break;
@@ -915,7 +919,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
       R[j] = v;
       const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
       kmx = key > kmx ? key : kmx;
-      crow[(d & (64 * J - 1))] = (cell_t)v;
+      crow[(d & (OVL_LOGW - 1))] = (cell_t)v;
     }
     const int32_t K = wave_max(kmx);
     const int32_t M = K >> WB;
@@ -938,7 +942,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
     PROF_ADD(pc_rest, pt_chunks, pt_rest);
   }
   if (out.ovf) return out;
-  const int32_t max_score_best_d = ms_B + (64 * J - 1) - (ms_key & (64 * J - 1));
+  const int32_t max_score_best_d = ms_B + ((1 << 9) - 1) - (ms_key & ((1 << 9) - 1));
   if (ended) {                               // forward.C:177-232, at row e
     double  score = end_row * bmv - e;
     int32_t tail_len = end_row - max_score_len;
