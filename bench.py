@@ -182,6 +182,8 @@ def main() -> None:
             "breakdown_ms": {"index": round(st["ms_index"], 2), "seed": round(st["ms_seed"], 2),
                              "extend": round(st["ms_extend"], 2)},
             "seed_hits": st["seed_hits"], "seed_nodes": st["seed_nodes"], "pairs": st["pairs"],
+            "pair_kernels": {"staged": st.get("staged_pairs"), "long": st.get("long_pairs"),
+                             "generic": st.get("generic_pairs")},
             "setup_s": round(setup_s, 1),
             "roofline": roof,
             "probe_roofline": probe_roof,

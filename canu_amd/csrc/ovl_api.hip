@@ -1055,7 +1055,10 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
     if (hist.alloc(nr)) return fail(OVL_ERR_OOM, "first-read histogram");
     HIPC(hipMemsetAsync(hist.p, 0, 4ull * nr, s));
     uint32_t n = (uint32_t)c->index_records;
-    if (n)
+    if (n && nr <= 2u * OVL_FR_WORDS)
+      hipLaunchKernelGGL(k_first_reads_lds, dim3((n + OVL_FR_CHUNK - 1) / OVL_FR_CHUNK), dim3(1024),
+                         0, s, c->d_tmpM2.p, c->d_occ.p, n, bgn, nr, hist.p);
+    else if (n)
       hipLaunchKernelGGL(k_first_reads, dim3(std::min<uint32_t>((n + 255) / 256, 16384)), dim3(256),
                          0, s, c->d_tmpM2.p, c->d_occ.p, n, bgn, hist.p);
     HIPC(hipGetLastError());

@@ -614,6 +614,38 @@ __global__ void k_first_reads(const uint64_t *__restrict__ M, const uint64_t *__
   }
 }
 
+// The same count with the histogram privatised in LDS: every read takes thousands of run
+// ends, so the global atomics above queue on a few thousand addresses (7 ms per build of a
+// canu-sized batch).  A block counts OVL_FR_CHUNK consecutive records into 16-bit LDS bins
+// (two per word: a block's count per read stays below 2^16) and adds its nonzero bins to
+// the global histogram.  nr (reads of the build) <= 2 * OVL_FR_WORDS.
+#define OVL_FR_WORDS 16384
+#define OVL_FR_CHUNK 65535
+__global__ void __launch_bounds__(1024) k_first_reads_lds(const uint64_t *__restrict__ M,
+                                                          const uint64_t *__restrict__ P,
+                                                          uint32_t n, uint32_t h0_iid, uint32_t nr,
+                                                          uint32_t *hist) {
+  __shared__ uint32_t bins[OVL_FR_WORDS];
+  const uint32_t nw = (nr + 1) / 2;
+  for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) bins[w] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * OVL_FR_CHUNK;
+  const uint32_t i1 = (uint32_t)(b0 + OVL_FR_CHUNK < n ? b0 + OVL_FR_CHUNK : n);
+  for (uint32_t i = (uint32_t)b0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint64_t p = P[i];
+    if (p == OVL_SKIP_POS) continue;
+    if (i + 1 < n && M[i + 1] == M[i]) continue;
+    const uint32_t r = (uint32_t)(p >> 32) - h0_iid;
+    atomicAdd(&bins[r >> 1], (r & 1u) ? 0x10000u : 1u);
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+    const uint32_t v = bins[w];
+    if (v & 0xFFFFu) atomicAdd(&hist[2 * w], v & 0xFFFFu);
+    if ((v >> 16) && 2 * w + 1 < nr) atomicAdd(&hist[2 * w + 1], v >> 16);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Small utilities
 
