@@ -1233,15 +1233,24 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     size_t lds = 0;
     bool l16 = false;
     uint64_t stride = 0;
+    bool wide = false;             // the 2 x OVL_RJ-chunk register window (wide bands)
+  };
+  // the staged kernel instance of a class
+  auto stage_kernel = [](bool l16, bool wide) -> const void * {
+    if (wide) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, 2 * OVL_RJ>)
+                         : reinterpret_cast<const void *>(k_extend<true, false, false, 2 * OVL_RJ>);
+    return l16 ? reinterpret_cast<const void *>(k_extend<true, true>)
+               : reinterpret_cast<const void *>(k_extend<true, false>);
   };
   const uint64_t SCRATCH_BUDGET = 24ull << 30;
   std::vector<ExtClass> ext_stage;
   auto per_wave_bytes = [](const ExtClass &g) {
     return g.stride * 4 + 16ull * (g.ecap + 2) + 28ull * (g.ecap + 8);
   };
-  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob) -> int {
+  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob, bool wide = false) -> int {
     ExtClass g;
     g.len = L;
+    g.wide = wide;
     g.ecap = ecap_of(L);
     g.sw = sw_of(L);
     g.l16 = L < 16384;
@@ -1255,11 +1264,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         int nb = atoi(bp);
         if (nb > 0) g.lds = std::max<size_t>(g.lds, (160 * 1024) / nb - 256);
       }
-    uint64_t st = (uint64_t)(g.ecap + 2) * OVL_LOGW / (g.l16 ? 2 : 1);   // the row log
+    const uint64_t lw = wide ? std::max<uint64_t>(OVL_LOGW, 128 * OVL_RJ) : OVL_LOGW;
+    uint64_t st = (uint64_t)(g.ecap + 2) * lw / (g.l16 ? 2 : 1);   // the row log
     if (window) st = std::max<uint64_t>(st, 3ull * (g.ecap + 9) + 2ull * L + 64);
     g.stride = (st + 63) & ~63ull;
-    const void *kfn = g.l16 ? reinterpret_cast<const void *>(k_extend<true, true>)
-                            : reinterpret_cast<const void *>(k_extend<true, false>);
+    const void *kfn = stage_kernel(g.l16, wide);
     if (g.lds > 64 * 1024)
       if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess)
         return -1;
@@ -1272,7 +1281,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       waves = std::min<uint32_t>(waves, (uint32_t)bpc * g.wpb * c->n_cu);
     while (waves > g.wpb && (uint64_t)waves * per_wave_bytes(g) > SCRATCH_BUDGET) waves /= 2;
     g.waves = std::max<uint32_t>(g.wpb, (waves / g.wpb) * g.wpb);
-    c->ext_classes.push_back(g.len);
+    if (!wide) c->ext_classes.push_back(g.len);
     ext_stage.push_back(g);
     return 0;
   };
@@ -1294,6 +1303,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       if (make_stage(L, tier_cap[t], t == 0)) return fail(OVL_ERR_HIP, "staged kernel setup");
       prev = L;
     }
+    // the wide class: the pairs of every staged class whose band outgrew the register window
+    // (the rest of their deferrals -- 'n' bases -- pass on to the generic kernel)
+    if (!ext_stage.empty() && !getenv("OVL_NO_WIDE") &&
+        make_stage(ext_stage.back().len, 160 * 1024, false, true))
+      return fail(OVL_ERR_HIP, "wide staged kernel setup");
   }
   // the generic kernel: every read length; rows in LDS while two row buffers and the
   // Edit_Match_Limit table fit a CU, else in global memory (GR)
@@ -1376,7 +1390,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   uint32_t n_probe_launch = 0, n_ext_launch = 0;
   uint32_t nu = (uint32_t)units.size();
   uint32_t u0 = 0;
-  const uint32_t ctr_next[3] = {5, 11, 13}, ctr_defer[3] = {8, 12, 14};
+  const uint32_t ctr_next[4] = {5, 11, 13, 15}, ctr_defer[4] = {8, 12, 14, 10};
   bool pending[2] = {false, false};
   uint32_t slot_pairs[2] = {0, 0};
   // chunk i's extension has finished: its counters, class split and time
@@ -1578,7 +1592,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
           EA.defer = defer_buf[ci & 1];
           EA.ndefer = x_ctr.p + ctr_defer[ci];
           n_ext_launch++;
-          if (g.l16)
+          if (g.wide && g.l16)
+            hipLaunchKernelGGL((k_extend<true, true, false, 2 * OVL_RJ>), dim3(g.waves / g.wpb),
+                               dim3(64 * g.wpb), g.lds, xs, EA);
+          else if (g.wide)
+            hipLaunchKernelGGL((k_extend<true, false, false, 2 * OVL_RJ>), dim3(g.waves / g.wpb),
+                               dim3(64 * g.wpb), g.lds, xs, EA);
+          else if (g.l16)
             hipLaunchKernelGGL((k_extend<true, true>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
           else
             hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);

@@ -551,12 +551,12 @@ typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 // time the previous rows are loaded into registers (lane = diagonal offset -31..31 from the
 // window's first position), every lane's step is decided in parallel, and the walk is
 // scalar, one readlane per row.
-template <bool L16>
+template <bool L16, int LW = OVL_LOGW>
 __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t tb_e,
                                                     int32_t tb_d, int32_t last, int32_t *dst,
                                                     uint32_t lane, int32_t &last_out,
                                                     int32_t &nd_out) {
-  constexpr int W = OVL_LOGW;                  // cells per logged row, cell = d mod W
+  constexpr int W = LW;                        // cells per logged row, cell = d mod W
   // rows per window (lanes cover dc-31..dc+31): 16 keeps the unrolled walk and its code
   // registers within wave_ped_reg's 80 VGPRs (24 spills; 16 vs 24: -1 % extension time)
   constexpr int TBR = 16;
@@ -643,13 +643,18 @@ __device__ __forceinline__ double uni(double v) {
 #ifndef OVL_PED_ATTR
 #define OVL_PED_ATTR noinline
 #endif
-template <int DIR, typename SS, bool L16>
+template <int DIR, typename SS, bool L16, int RJ = OVL_RJ>
 __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
                                                          int32_t a0, int32_t m, const SS &T,
                                                          int32_t t0, int32_t n, int32_t limit,
                                                          const WaveMem &WM, int32_t *dst,
                                                          uint32_t lane) {
-  constexpr int J = OVL_RJ;
+  constexpr int J = RJ;
+  // cells per logged row (a power of two holding the register window) and the window
+  // offset bits of a row key
+  constexpr int LW = 64 * RJ > OVL_LOGW ? 64 * RJ : OVL_LOGW;
+  constexpr int WB = 64 * RJ > 512 ? 10 : 9;
+  static_assert(64 * J <= (1 << WB) && 64 * J <= LW, "key and log layout hold the window");
   static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
   limit = uni(limit);
   int32_t *rows = WM.rows;
@@ -685,7 +690,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   int32_t max_score_len = 0, max_score_best_e = 0;
   // Max_Score_Best_d is kept as the row key and window base it decodes from (decoded once,
   // after the loop): B + 64J-1 - (key & 64J-1)
-  int32_t ms_key = (1 << 9) - 1, ms_B = 0;
+  int32_t ms_key = (1 << WB) - 1, ms_B = 0;
   int32_t longest = 0;
   int32_t pl = 0, pr = 0;
   int32_t tb_e = -1, tb_d = 0, tb_last = 0;
@@ -709,12 +714,10 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   // of the next row would wait for the log stores too
   typedef __attribute__((address_space(1))) cell_t g_cell_t;
   g_cell_t *clog = uni_ptr((g_cell_t *)rows);     // scalar base: stores use saddr + offset
-  clog[(B + (int32_t)lane) & (OVL_LOGW - 1)] = (cell_t)R[0];
+  clog[(B + (int32_t)lane) & (LW - 1)] = (cell_t)R[0];
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
   constexpr int JU = 1;
-  constexpr int WB = 9;                        // window offset bits of a key
-  static_assert(64 * J <= (1 << WB), "key layout assumes a window of at most 512 diagonals");
   const int32_t lkey = (1 << WB) - 1 - (int32_t)lane;
 
   int32_t e = 1;
@@ -910,7 +913,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
     int32_t kmx = NEG;
     const uint32_t kspan = (uint32_t)(nr - nl);
     const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
-    g_cell_t *crow = clog + (size_t)e * OVL_LOGW;
+    g_cell_t *crow = clog + (size_t)e * LW;
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jrs) break;
@@ -919,7 +922,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
       R[j] = v;
       const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
       kmx = key > kmx ? key : kmx;
-      crow[(d & (OVL_LOGW - 1))] = (cell_t)v;
+      crow[(d & (LW - 1))] = (cell_t)v;
     }
     const int32_t K = wave_max(kmx);
     const int32_t M = K >> WB;
@@ -942,7 +945,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
     PROF_ADD(pc_rest, pt_chunks, pt_rest);
   }
   if (out.ovf) return out;
-  const int32_t max_score_best_d = ms_B + ((1 << 9) - 1) - (ms_key & ((1 << 9) - 1));
+  const int32_t max_score_best_d = ms_B + ((1 << WB) - 1) - (ms_key & ((1 << WB) - 1));
   if (ended) {                               // forward.C:177-232, at row e
     double  score = end_row * bmv - e;
     int32_t tail_len = end_row - max_score_len;
@@ -978,7 +981,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
-  ped_traceback_codes<L16>(WM, tb_e, tb_d, tb_last, dst, lane, last, nd);
+  ped_traceback_codes<L16, LW>(WM, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
 #ifdef OVL_PROFILE
@@ -1027,7 +1030,7 @@ struct ExtOut {
 #else
 #define UNI(v) (v)
 #endif
-template <bool FAST, bool L16, typename SS>
+template <bool FAST, bool L16, int RJ, typename SS>
 __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS &S,
                                    int32_t S_Len, const SS &T, int32_t T_Len,
                                    const WaveMem &WM, int32_t *stk, int32_t *RD,
@@ -1065,7 +1068,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     int32_t bn = s_first ? T_Right_Len : S_Right_Len;
     PedOut po;
     PROF_T(pc0);
-    if constexpr (FAST) po = wave_ped_reg<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    if constexpr (FAST) po = wave_ped_reg<1, SS, L16, RJ>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
     else                po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
 #ifdef OVL_PROFILE
     PROF_T(pc1);
@@ -1107,7 +1110,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     int32_t b0 = s_first ? T_Left_Begin : S_Left_Begin;
     PedOut po;
     PROF_T(pc2);
-    if constexpr (FAST) po = wave_ped_reg<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    if constexpr (FAST) po = wave_ped_reg<-1, SS, L16, RJ>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
     else                po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
 #ifdef OVL_PROFILE
     PROF_T(pc3);
@@ -1411,7 +1414,7 @@ __device__ bool lies_on_alignment(int32_t start, int32_t offset, int32_t s_lo, i
 // Returns false when the pair must be redone by the generic kernel (register window
 // overflow); nothing has been output for it then, and removed nodes are marked ~Len so the
 // generic kernel can restore them.
-template <bool FAST, bool L16, bool ORD, typename SS>
+template <bool FAST, bool L16, bool ORD, int RJ, typename SS>
 __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &un,
                              const SS &S, const SS &T, const WaveMem &WM, int32_t *stk,
                              int32_t *RD, int32_t *LD, unsigned long long *st, uint32_t lane,
@@ -1493,7 +1496,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     }
     if (!hit_limit) {
       PROF_T(px0);
-      ExtOut eo = extend_alignment<FAST, L16>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
+      ExtOut eo = extend_alignment<FAST, L16, RJ>(X, M, S, S_Len, T, t_len, WM, stk, RD, LD, lane);
 #ifdef OVL_PROFILE
       PROF_T(px1);
       if (X.dbg && lane == 0) atomicAdd(&X.dbg[15], px1 - px0);
@@ -1700,8 +1703,10 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
 #ifndef OVL_EXT_OCC
 #define OVL_EXT_OCC 6            // waves per SIMD the staged kernel is compiled for
 #endif
-template <bool STAGE, bool L16, bool ORD = false>
-__global__ void __launch_bounds__(512, OVL_EXT_OCC) k_extend(ExtendArgs X) {
+// RJ: register chunks of the staged kernel's row window (OVL_RJ; the wide class that takes
+// the pairs whose band outgrows it runs 2 x OVL_RJ at lower occupancy)
+template <bool STAGE, bool L16, bool ORD = false, int RJ = OVL_RJ>
+__global__ void __launch_bounds__(512, RJ > OVL_RJ ? 3 : OVL_EXT_OCC) k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -1762,7 +1767,7 @@ __global__ void __launch_bounds__(512, OVL_EXT_OCC) k_extend(ExtendArgs X) {
         Unit un = X.units[P.unit];
         Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
         Strand T = strand_fwd(X.R, P.tgt);
-        process_pair<false, L16, true>(X, P, un, S, T, WM, stk, RD, LD, st, lane, ab);
+        process_pair<false, L16, true, OVL_RJ>(X, P, un, S, T, WM, stk, RD, LD, st, lane, ab);
         lds_sync();
       };
       if ((uint64_t)(e - b) <= X.olim) {     // Process_String_Olaps.C:721
@@ -1800,7 +1805,7 @@ __global__ void __launch_bounds__(512, OVL_EXT_OCC) k_extend(ExtendArgs X) {
         StrandLP TL = stage_strand(T, tw, lane);
         lds_sync();
         PROF_T(pp0);
-        ok = process_pair<true, L16, false>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
+        ok = process_pair<true, L16, false, RJ>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
 #ifdef OVL_PROFILE
         PROF_T(pp1);
         if (X.dbg && lane == 0) atomicAdd(&X.dbg[13], pp1 - pp0);
@@ -1808,7 +1813,7 @@ __global__ void __launch_bounds__(512, OVL_EXT_OCC) k_extend(ExtendArgs X) {
       }
       if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
     } else {
-      process_pair<false, L16, false>(X, P, un, S, T, WM, stk, RD, LD, st, lane, nullptr);
+      process_pair<false, L16, false, OVL_RJ>(X, P, un, S, T, WM, stk, RD, LD, st, lane, nullptr);
     }
     lds_sync();
   }
