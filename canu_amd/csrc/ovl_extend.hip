@@ -551,8 +551,21 @@ typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 // time the previous rows are loaded into registers (lane = diagonal offset -31..31 from the
 // window's first position), every lane's step is decided in parallel, and the walk is
 // scalar, one readlane per row.
+//
+// The walk itself is cheap; what it waits for is the log.  So the rows of OVL_TB_G windows
+// are loaded in one burst (one memory round trip instead of one per window), every window of
+// the burst centred at the burst's first position dc.  A window can be walked from these
+// lanes while its first position d stays within 15 of dc: its 16 steps then read lanes
+// 31 + (d - dc) +- 15, inside the lanes 1..61 whose DPP neighbours are real cells.  The
+// first window of a burst always can; when a later one cannot (the path drifted), the next
+// burst starts there.  Measured (10k x 10 kb, records identical): 2 windows per burst the
+// same as 1, 3 windows +3-4 % (the 48 row registers) -- the other waves of the SIMD already
+// hide the log's latency, so the default stays one window per load.
+#ifndef OVL_TB_G
+#define OVL_TB_G 1
+#endif
 template <bool L16, int LW = OVL_LOGW>
-__device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t tb_e,
+__device__ __forceinline__ void ped_traceback_codes(int32_t *log, int32_t tb_e,
                                                     int32_t tb_d, int32_t last, int32_t *dst,
                                                     uint32_t lane, int32_t &last_out,
                                                     int32_t &nd_out) {
@@ -560,60 +573,73 @@ __device__ __forceinline__ void ped_traceback_codes(const WaveMem &WM, int32_t t
   // rows per window (lanes cover dc-31..dc+31): 16 keeps the unrolled walk and its code
   // registers within wave_ped_reg's 80 VGPRs (24 spills; 16 vs 24: -1 % extension time)
   constexpr int TBR = 16;
-  g_ci32 *rows = (g_ci32 *)WM.rows;
+  constexpr int G = OVL_TB_G;                  // windows per burst of log loads
+  g_ci32 *rows = (g_ci32 *)log;
   typedef __attribute__((address_space(1))) const int16_t g_ci16;
-  g_ci16 *rows16 = (g_ci16 *)WM.rows;
+  g_ci16 *rows16 = (g_ci16 *)log;
   typedef __attribute__((address_space(1))) int32_t g_i32;
   g_i32 *gdst = (g_i32 *)dst;                  // global, not flat (see wave_ped_reg's log)
   vm_sync();                                  // the log is complete
   int32_t d = __builtin_amdgcn_readfirstlane(tb_d);
   last = __builtin_amdgcn_readfirstlane(last);
-  tb_e = __builtin_amdgcn_readfirstlane(tb_e);
+  int32_t kh = __builtin_amdgcn_readfirstlane(tb_e);
   int32_t nd = 0;
-  for (int32_t kh = tb_e; kh >= 1; kh -= TBR) {
+  while (kh >= 1) {
     const int32_t dc = d;
     const int32_t cell = (dc - 31 + (int32_t)(lane < 63 ? lane : 62)) & (W - 1);
-    int32_t V[TBR];
+    int32_t V[G * TBR];
 #pragma unroll
-    for (int i = 0; i < TBR; i++) {
+    for (int i = 0; i < G * TBR; i++) {
       const int32_t kk = kh - 1 - i < 0 ? 0 : kh - 1 - i;   // row k-1 for k = kh - i
       if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
       else               V[i] = rows[(size_t)kk * W + cell];
     }
-    // Every lane's winner first, lane-parallel (VALU, DPP neighbours): C[i] at lane x is
-    // (the value the walk would take as `last`) << 2 | (from + 1), with the reference's
-    // order -- d-1 only if strictly better than d, d+1 only if strictly better than both.
-    // The walk is then one readlane and a few scalar operations per row; the window's
-    // deltas collect in one VGPR (lane j = its j-th delta) stored once per window.
-    const int32_t nsteps = kh < TBR ? kh : TBR;
-#pragma unroll
-    for (int i = 0; i < TBR; i++) {
-      const int32_t v = V[i];
-      const int32_t vm = dpp_from_lower(v, -2), vp = dpp_from_upper(v, -2);
-      const int32_t a = v + 1, c = vp + 1;
-      const int32_t m = vm > a ? vm : a;
-      const int32_t f = c > m ? 2 : (vm > a ? 0 : 1);
-      V[i] = ((f == 0 ? vm : vp) << 2) | f;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    int32_t buf = 0, nb = 0;
-    int32_t x = 31;                            // lane of diagonal d: 31 + d - dc
-#pragma unroll
-    for (int i = 0; i < TBR; i++) {
-      if (i < nsteps) {
-        const int32_t w = __builtin_amdgcn_readlane(V[i], x);
-        const int32_t f3 = w & 3, nl = w >> 2;   // f3: 0 d-1, 1 d, 2 d+1
-        const int32_t val = f3 == 0 ? nl - last - 1 : last - nl;
-        buf = (int32_t)lane == nb ? val : buf;
-        const int32_t mv = f3 != 1;
-        nb += mv;
-        last = mv ? nl : last;
-        x += f3 - 1;
+#pragma unroll 1
+    for (int g = 0; g < G; g++) {
+      if (g > 0) {
+        const int32_t off = d - dc;
+        if (kh < 1 || off > 15 || off < -15) break;
       }
+      // Every lane's winner first, lane-parallel (VALU, DPP neighbours): C[i] at lane x is
+      // (the value the walk would take as `last`) << 2 | (from + 1), with the reference's
+      // order -- d-1 only if strictly better than d, d+1 only if strictly better than both.
+      // The walk is then one readlane and a few scalar operations per row; the window's
+      // deltas collect in one VGPR (lane j = its j-th delta) stored once per window.
+      const int32_t nsteps = kh < TBR ? kh : TBR;
+      int32_t C[TBR];
+#pragma unroll
+      for (int i = 0; i < TBR; i++) {
+        const int32_t v = V[i];
+        const int32_t vm = dpp_from_lower(v, -2), vp = dpp_from_upper(v, -2);
+        const int32_t a = v + 1, c = vp + 1;
+        const int32_t m = vm > a ? vm : a;
+        const int32_t f = c > m ? 2 : (vm > a ? 0 : 1);
+        C[i] = ((f == 0 ? vm : vp) << 2) | f;
+      }
+      // the next window's rows move down (register moves; with G == 1 there are none)
+#pragma unroll
+      for (int i = 0; i + TBR < G * TBR; i++) V[i] = V[i + TBR];
+      __builtin_amdgcn_sched_barrier(0);
+      int32_t buf = 0, nb = 0;
+      int32_t x = 31 + d - dc;                 // lane of diagonal d
+#pragma unroll
+      for (int i = 0; i < TBR; i++) {
+        if (i < nsteps) {
+          const int32_t w = __builtin_amdgcn_readlane(C[i], x);
+          const int32_t f3 = w & 3, nl = w >> 2;   // f3: 0 d-1, 1 d, 2 d+1
+          const int32_t val = f3 == 0 ? nl - last - 1 : last - nl;
+          buf = (int32_t)lane == nb ? val : buf;
+          const int32_t mv = f3 != 1;
+          nb += mv;
+          last = mv ? nl : last;
+          x += f3 - 1;
+        }
+      }
+      d = dc + x - 31;
+      if ((int32_t)lane < nb) gdst[nd + (int32_t)lane] = buf;
+      nd += nb;
+      kh -= TBR;
     }
-    d = dc + x - 31;
-    if ((int32_t)lane < nb) gdst[nd + (int32_t)lane] = buf;
-    nd += nb;
   }
   last_out = last;
   nd_out = nd;
@@ -643,12 +669,21 @@ __device__ __forceinline__ double uni(double v) {
 #ifndef OVL_PED_ATTR
 #define OVL_PED_ATTR noinline
 #endif
+//
+// Everything the row loop reads arrives as a scalar argument (v0..v31 of the call), not
+// through references: a reference to the ExtendArgs / WaveMem / strand copies in the
+// kernel's scratch made every call start with flat loads from scratch and a full vmcnt(0)
+// wait (which also waited for the caller's spill stores and the row-0 log store).  X is
+// only read by the OVL_PROFILE build.
 template <int DIR, typename SS, bool L16, int RJ = OVL_RJ>
-__device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X, const SS &A,
-                                                         int32_t a0, int32_t m, const SS &T,
-                                                         int32_t t0, int32_t n, int32_t limit,
-                                                         const WaveMem &WM, int32_t *dst,
-                                                         uint32_t lane) {
+__device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
+    const ExtendArgs &X, int32_t e_cap, int32_t partial_i, int32_t mbed, double bmv_in,
+    double mbts, const lds_u64 *aw, int32_t a0, int32_t m, const lds_u64 *tw, int32_t t0,
+    int32_t n, int32_t limit, int32_t *rows, const lds_i32 *mlim, int32_t *dst,
+    uint32_t lane) {
+  SS A, T;
+  A.w = aw; A.len = 0;
+  T.w = tw; T.len = 0;
   constexpr int J = RJ;
   // cells per logged row (a power of two holding the register window) and the window
   // offset bits of a row key
@@ -657,13 +692,12 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   static_assert(64 * J <= (1 << WB) && 64 * J <= LW, "key and log layout hold the window");
   static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
   limit = uni(limit);
-  int32_t *rows = WM.rows;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;
   out.nd = 0;
   out.ovf = 0;
-  if (limit > X.e_cap - 2) {                   // not this kernel's class: defer the pair
+  if (limit > uni(e_cap) - 2) {                // not this kernel's class: defer the pair
     out.ovf = 1;
     return out;
   }
@@ -695,10 +729,10 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   int32_t pl = 0, pr = 0;
   int32_t tb_e = -1, tb_d = 0, tb_last = 0;
   bool finished = false;
-  const double bmv = uni(X.branch_match_value);
-  const bool partial = X.partial != 0;
-  const int32_t mbed = X.min_branch_end_dist;
-  const double mbts = X.min_branch_tail_slope;
+  const double bmv = uni(bmv_in);
+  const bool partial = uni(partial_i) != 0;
+  mbed = uni(mbed);
+  mbts = uni(mbts);
 #ifdef OVL_PROFILE
   unsigned long long pc_a = 0, pc_b = 0, pc_cont = 0, pc_c = 0;
   unsigned long long pc_chunks = 0, pc_rest = 0, pc_rows = 0, pc_nch = 0, pc_slide = 0,
@@ -723,55 +757,16 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   int32_t e = 1;
   bool ended = false;
   int32_t end_d = 0, end_row = 0, end_pp = 0;
-  for (; e <= limit; e++) {
+  // One exit: every way a row ends the loop (the end reached, an empty band, the band
+  // outgrowing the window, the error limit) sets `stop`, tested once per row; with four
+  // breaks the structurizer carried exit flags through every row's tail (~12 scalar
+  // instructions per row).  The window is re-anchored for the next row at the end of this
+  // one (row 1 needs none: B = -3, pl = pr = 0).
+  uint32_t stop = limit < 1 ? 1u : 0u;
+  while (!stop) {
     PROF_T(pt_row);
-    const int32_t ML = WM.mlim[e];
+    const int32_t ML = mlim[e];
     const int32_t right = pr + 1;
-    // The window is anchored at the band: B <= pl-3 < B+16, so the row's chunks are
-    // 0..jr with little waste in chunk 0.  When pl-3 leaves [B, B+16) the window moves to
-    // B = pl-9: whole chunks by register moves, the rest by one ds_bpermute per chunk
-    // (about one row in ten).  It must also hold pr+3 (the reads of this row and the log
-    // of the next).
-    if ((uint32_t)(pl - 3 - B) >= 16u) {
-      const int32_t nb = pl - 9;
-      int32_t sft = nb - B;
-      while (sft >= 64) {
-#pragma unroll
-        for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
-        R[J - 1] = -2;
-        sft -= 64;
-      }
-      while (sft <= -64) {
-#pragma unroll
-        for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
-        R[0] = -2;
-        sft += 64;
-      }
-      if (sft != 0) {
-        const int32_t ls = (int32_t)lane + sft;
-        const int32_t src = (ls & 63) << 2;
-        int32_t bp[J];
-#pragma unroll
-        for (int j = 0; j < J; j++) bp[j] = __builtin_amdgcn_ds_bpermute(src, R[j]);
-        if (sft > 0) {
-          const bool hi = ls >= 64;            // comes from the next chunk up
-#pragma unroll
-          for (int j = 0; j < J; j++) R[j] = hi ? (j + 1 < J ? bp[j + 1 < J ? j + 1 : j] : -2) : bp[j];
-        } else {
-          const bool lo = ls < 0;              // comes from the chunk below
-#pragma unroll
-          for (int j = 0; j < J; j++) R[j] = lo ? (j > 0 ? bp[j > 0 ? j - 1 : 0] : -2) : bp[j];
-        }
-      }
-      B = nb;
-#ifdef OVL_PROFILE
-      pc_recenter++;
-#endif
-    }
-    if (pr + 3 > B + 64 * J - 1) {
-      out.ovf = 1;
-      break;
-    }
     const int32_t jr = (right - B) >> 6;
 
     // ---- A+B per chunk: neighbours from row e-1 (DPP, no LDS), then the first 32-base
@@ -900,49 +895,101 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
         }
       }
       ended = true;
-      break;                                   // end reached
-    }
-    if (nlo == 0xffffffffu) break;             // Left > Right
-    const int32_t nl = B + (int32_t)nlo;
-    const int32_t nr = B + nro;
+      stop = 1;                                // end reached
+    } else if (nlo == 0xffffffffu) {
+      stop = 1;                                // Left > Right
+    } else {
+      const int32_t nl = B + (int32_t)nlo;
+      const int32_t nr = B + nro;
 
-    // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
-    // traceback (cells up to nr+2 are read), longest row with the first d on ties: one
-    // wave max over keys (value << WB | 64J-1 - window offset), so a larger value wins and
-    // among equal values the smaller d (values < 2^21 and -2 keep the order in 32 bits)
-    int32_t kmx = NEG;
-    const uint32_t kspan = (uint32_t)(nr - nl);
-    const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
-    g_cell_t *crow = clog + (size_t)e * LW;
+      // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
+      // traceback (cells up to nr+2 are read), longest row with the first d on ties: one
+      // wave max over keys (value << WB | 64J-1 - window offset), so a larger value wins and
+      // among equal values the smaller d (values < 2^21 and -2 keep the order in 32 bits)
+      int32_t kmx = NEG;
+      const uint32_t kspan = (uint32_t)(nr - nl);
+      const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
+      g_cell_t *crow = clog + (size_t)e * LW;
 #pragma unroll
-    for (int j = 0; j < J; j++) {
-      if (j >= JU && j > jrs) break;
-      const int32_t d = B + 64 * j + (int32_t)lane;
-      const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
-      R[j] = v;
-      const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
-      kmx = key > kmx ? key : kmx;
-      crow[(d & (LW - 1))] = (cell_t)v;
-    }
-    const int32_t K = wave_max(kmx);
-    const int32_t M = K >> WB;
-    if (M > longest) {                         // Longest, Best_d, Best_e of this row
-      longest = M;
-      // the score can only beat Max_Score on a row whose Longest grew: otherwise it is the
-      // previous row's score minus one (monotone in double too), and that was <= Max_Score
-      const double score = longest * bmv - e;
-      if (score > max_score) {
-        max_score = score;
-        max_score_len = longest;
-        ms_key = K;
-        ms_B = B;
-        max_score_best_e = e;
+      for (int j = 0; j < J; j++) {
+        if (j >= JU && j > jrs) break;
+        const int32_t d = B + 64 * j + (int32_t)lane;
+        const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
+        R[j] = v;
+        const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
+        kmx = key > kmx ? key : kmx;
+        crow[(d & (LW - 1))] = (cell_t)v;
+      }
+      const int32_t K = wave_max(kmx);
+      const int32_t M = K >> WB;
+      if (M > longest) {                         // Longest, Best_d, Best_e of this row
+        longest = M;
+        // the score can only beat Max_Score on a row whose Longest grew: otherwise it is the
+        // previous row's score minus one (monotone in double too), and that was <= Max_Score
+        const double score = longest * bmv - e;
+        if (score > max_score) {
+          max_score = score;
+          max_score_len = longest;
+          ms_key = K;
+          ms_B = B;
+          max_score_best_e = e;
+        }
+      }
+      pl = nl;
+      pr = nr;
+      PROF_T(pt_rest);
+      PROF_ADD(pc_rest, pt_chunks, pt_rest);
+      e++;
+      if (e > limit) {
+        stop = 1;
+      } else {
+        // The window is anchored at the band: B <= pl-3 < B+16, so the row's chunks are
+        // 0..jr with little waste in chunk 0.  When pl-3 leaves [B, B+16) the window moves to
+        // B = pl-9: whole chunks by register moves, the rest by one ds_bpermute per chunk
+        // (about one row in ten).  It must also hold pr+3 (the reads of this row and the log
+        // of the next).
+        if ((uint32_t)(pl - 3 - B) >= 16u) {
+          const int32_t nb = pl - 9;
+          int32_t sft = nb - B;
+          while (sft >= 64) {
+#pragma unroll
+            for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
+            R[J - 1] = -2;
+            sft -= 64;
+          }
+          while (sft <= -64) {
+#pragma unroll
+            for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
+            R[0] = -2;
+            sft += 64;
+          }
+          if (sft != 0) {
+            const int32_t ls = (int32_t)lane + sft;
+            const int32_t src = (ls & 63) << 2;
+            int32_t bp[J];
+#pragma unroll
+            for (int j = 0; j < J; j++) bp[j] = __builtin_amdgcn_ds_bpermute(src, R[j]);
+            if (sft > 0) {
+              const bool hi = ls >= 64;            // comes from the next chunk up
+#pragma unroll
+              for (int j = 0; j < J; j++) R[j] = hi ? (j + 1 < J ? bp[j + 1 < J ? j + 1 : j] : -2) : bp[j];
+            } else {
+              const bool lo = ls < 0;              // comes from the chunk below
+#pragma unroll
+              for (int j = 0; j < J; j++) R[j] = lo ? (j > 0 ? bp[j > 0 ? j - 1 : 0] : -2) : bp[j];
+            }
+          }
+          B = nb;
+#ifdef OVL_PROFILE
+          pc_recenter++;
+#endif
+        }
+        if (pr + 3 > B + 64 * J - 1) {         // the next row would not fit the window
+          out.ovf = 1;
+          stop = 1;
+        }
       }
     }
-    pl = nl;
-    pr = nr;
-    PROF_T(pt_rest);
-    PROF_ADD(pc_rest, pt_chunks, pt_rest);
   }
   if (out.ovf) return out;
   const int32_t max_score_best_d = ms_B + ((1 << WB) - 1) - (ms_key & ((1 << WB) - 1));
@@ -981,7 +1028,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(const ExtendArgs &X
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
-  ped_traceback_codes<L16, LW>(WM, tb_e, tb_d, tb_last, dst, lane, last, nd);
+  ped_traceback_codes<L16, LW>(rows, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
 #ifdef OVL_PROFILE
@@ -1068,8 +1115,13 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     int32_t bn = s_first ? T_Right_Len : S_Right_Len;
     PedOut po;
     PROF_T(pc0);
-    if constexpr (FAST) po = wave_ped_reg<1, SS, L16, RJ>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
-    else                po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
+    if constexpr (FAST)
+      po = wave_ped_reg<1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
+                                        X.branch_match_value, X.min_branch_tail_slope, A.w, a0,
+                                        am, B.w, b0, bn, error_limit, WM.rows, WM.mlim, stk,
+                                        lane);
+    else
+      po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
 #ifdef OVL_PROFILE
     PROF_T(pc1);
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc1 - pc0);
@@ -1110,8 +1162,13 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     int32_t b0 = s_first ? T_Left_Begin : S_Left_Begin;
     PedOut po;
     PROF_T(pc2);
-    if constexpr (FAST) po = wave_ped_reg<-1, SS, L16, RJ>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
-    else                po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
+    if constexpr (FAST)
+      po = wave_ped_reg<-1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
+                                         X.branch_match_value, X.min_branch_tail_slope, A.w,
+                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.mlim, LD,
+                                         lane);
+    else
+      po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
 #ifdef OVL_PROFILE
     PROF_T(pc3);
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[12], pc3 - pc2);

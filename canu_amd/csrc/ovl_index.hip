@@ -296,6 +296,9 @@ __device__ uint32_t wave_group_runs(const Rec2 *__restrict__ in, uint64_t *__res
 }
 
 #define OVL_FINE_WAVES  8
+#ifndef OVL_FINE_PHASE
+#define OVL_FINE_PHASE  0        // 1 / 2: stop after the histogram / the split (timing only)
+#endif
 #define OVL_FB_MAX      4096
 #ifndef OVL_FINE_PSCAN
 #define OVL_FINE_PSCAN  1
@@ -375,6 +378,13 @@ k_fine(FineArgs A) {
   }
 #endif
   __syncthreads();
+#if OVL_FINE_PHASE == 1                          // timing experiment: histogram + scan only
+  for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) {   // empty buckets for k_table
+    A.fstart[cb * nf + f] = s0;
+    A.fcnt[cb * nf + f] = 0;
+  }
+  return;
+#endif
   for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) {
     A.fstart[cb * nf + f] = s0 + cur[f];
     A.fcnt[cb * nf + f] = h[f];
@@ -388,6 +398,10 @@ k_fine(FineArgs A) {
   }
   __threadfence_block();
   __syncthreads();
+#if OVL_FINE_PHASE == 2                          // timing experiment: + the fine split
+  for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) A.fcnt[cb * nf + f] = 0;
+  return;
+#endif
 
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t *kT = s_fine + (size_t)wave * (2 * cap + cap / 2);
