@@ -196,6 +196,9 @@ struct ovl_ctx {
   uint64_t cut_windows_hint = 0; // windows of the job's last load-cut batch (0: none yet)
   DBuf<TabEntry> d_tab;
   uint32_t tab_bits = 0, slice_bits = 0;
+  DBuf<uint64_t> d_bloom;        // the batch's Bloom filter (built on first use per index)
+  bool bloom_ok = false;
+  uint32_t bloom_bits = 0;
 
   // find_overlaps working buffers: kept across calls (grow-only), hipMalloc of tens of
   // GB per call would cost seconds
@@ -676,6 +679,7 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   c->hash_bgn_iid = bgn;
   c->hash_end_iid = end;
   c->have_index = false;
+  c->bloom_ok = false;
   HIPC(hipEventRecord(c->ev[0], s));
   hipLaunchKernelGGL(k_clear_screen, dim3((c->nreads + 255) / 256), dim3(256), 0, s,
                      c->d_flags.p, c->nreads);
@@ -1110,7 +1114,40 @@ IndexDev index_dev(const ovl_ctx *c) {
   X.slice_bits = c->slice_bits;
   X.k = c->P.kmer_len;
   X.kmask = (1ull << (2 * c->P.kmer_len)) - 1;
+  X.bloom = nullptr;
+  X.bloom_bits = 0;
   return X;
+}
+
+// The current index's Bloom filter (k_bloom_build over the table), ~8 bits per indexed
+// window (>= distinct k-mers): at canu's --hashbits 23 --hashload 0.75 a batch of ~130 M
+// distinct k-mers takes ~130 MB, a fraction of its table and within the MALL.
+static int ensure_bloom(ovl_ctx *c) {
+  if (c->bloom_ok) return OVL_OK;
+  uint32_t bits = 10;
+  while (bits < 34 && (1ull << bits) < (c->index_records + 7) / 8) bits++;
+  if (c->d_bloom.alloc(1ull << bits)) return fail(OVL_ERR_OOM, "bloom filter 2^%u words", bits);
+  HIPC(hipMemsetAsync(c->d_bloom.p, 0, 8ull << bits, c->stream));
+  const uint64_t nslots = 1ull << c->tab_bits;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((nslots + 255) / 256, 8ull * c->n_cu);
+  hipLaunchKernelGGL(k_bloom_build, dim3(grid), dim3(256), 0, c->stream, c->d_tab.p, nslots,
+                     c->d_bloom.p, bits);
+  HIPC(hipGetLastError());
+  c->bloom_bits = bits;
+  c->bloom_ok = true;
+  return OVL_OK;
+}
+
+// Whether a search of ref reads bgn..end should probe through the Bloom filter: when at
+// least 3/4 of them lie outside the hash range (OverlapDriver's later batches, probed by
+// every earlier query), most of their windows miss the table.  OVL_BLOOM=0/1 forces it.
+static bool use_bloom(const ovl_ctx *c, uint32_t bgn, uint32_t end) {
+  if (const char *e = getenv("OVL_BLOOM")) return atoi(e) != 0;
+  if (end < bgn) return false;
+  const uint64_t q = (uint64_t)end - bgn + 1;
+  const uint32_t lo = std::max(bgn, c->hash_bgn_iid), hi = std::min(end, c->hash_end_iid);
+  const uint64_t inside = hi >= lo ? (uint64_t)hi - lo + 1 : 0;
+  return 4 * (q - inside) >= 3 * q;
 }
 
 // Process_Overlaps (overlapInCore-Process_Overlaps.C:101-137) over ref reads bgn..end of
@@ -1692,6 +1729,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     A.nu = A.nn = A.np = 0;
     return rc;
   };
+  // the filter is built once per index, before the first search that wants it
+  const bool bloom = nu > 0 && use_bloom(c, bgn, end);
+  if (bloom)
+    if (int rc = ensure_bloom(c)) return rc;
   uint64_t chunk = 0;
   while (u0 < nu) {
     const int slot = pipe ? (int)(chunk & 1) : 0;
@@ -1720,6 +1761,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     ProbeArgs PA;
     PA.R = c->reads();
     PA.X = index_dev(c);
+    if (bloom) {
+      PA.X.bloom = c->d_bloom.p;
+      PA.X.bloom_bits = c->bloom_bits;
+    }
     PA.units = d_units.p;
     PA.rbase = d_rbase.p;
     PA.nunits = nb;
@@ -1728,7 +1773,8 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     PA.unit_flags = d_uflags.p;
     PA.k = k;
     HIPC(hipEventRecord(c->ev[2], s));
-    hipLaunchKernelGGL(k_probe, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
+    if (bloom) hipLaunchKernelGGL(k_probe<true>, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
+    else       hipLaunchKernelGGL(k_probe<false>, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
     n_probe_launch++;
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev[3], s));
@@ -2020,7 +2066,7 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
     PA.unit_hits = fb.uhits.p;
     PA.unit_flags = fb.uflags.p;
     PA.k = k;
-    hipLaunchKernelGGL(k_probe, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
+    hipLaunchKernelGGL(k_probe<false>, dim3((nb + 3) / 4), dim3(256), 0, s, PA);
     HitArgs HA;
     HA.R = c->reads();
     HA.occ = c->d_occ.p;

@@ -211,7 +211,23 @@ struct IndexDev {
   uint32_t        slice_bits;// log2(slots per slice)
   uint32_t        k;
   uint64_t        kmask;
+  const uint64_t *bloom;     // blocked Bloom filter of the table's keys, or null
+  uint32_t        bloom_bits;// log2(its 64-bit words)
 };
+
+// The blocked Bloom filter of a hash batch's distinct k-mers (every table entry, the -k
+// skip entries included): one 64-bit word per key, 4 bits in it.  No false negatives, so a
+// window it rejects is a window the table lookup would not have found.  The word comes from
+// the low bits of mix64(kmer) (the table slot uses the top bits), the bits from an odd
+// multiple of it.
+__host__ __device__ __forceinline__ uint64_t bloom_word(uint64_t M, uint32_t bits) {
+  return M & ((1ull << bits) - 1);
+}
+__host__ __device__ __forceinline__ uint64_t bloom_mask(uint64_t M) {
+  const uint64_t h = M * 0x9E3779B97F4A7C15ull;
+  return (1ull << (h >> 58)) | (1ull << ((h >> 52) & 63)) | (1ull << ((h >> 46) & 63)) |
+         (1ull << ((h >> 40) & 63));
+}
 
 // The table is keyed by mix64(kmer); an empty slot has cnt == 0 (every filled slot has
 // the 0x40000000 "present" bit).  Linear probing stays inside the k-mer's slice.

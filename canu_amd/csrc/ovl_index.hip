@@ -322,12 +322,43 @@ struct FineArgs {
 // buffers.  Grouped runs (GROUP): per wave [kT: cap u64][sP: cap u64][cT: cap u32], overlaid
 // on the bins (the sort phase takes its buckets' bounds from fstart / fcnt); bitonic:
 // [sM: 8 x cap u64][sP: 8 x cap u64] then the bins.
+#ifndef OVL_SPLIT_TILE
+#define OVL_SPLIT_TILE 2048      // records per LDS-staged tile of the fine split (0: direct)
+#endif
 __host__ __device__ inline size_t fine_lds_bytes(bool group, uint32_t nf, uint32_t cap) {
   if (group) {
-    const size_t sort = (size_t)OVL_FINE_WAVES * cap * 20, bins = (size_t)nf * 8;
+    // bins: h, cur (+ the tiled split's tile counts and starts and its staged records)
+    const size_t sort = (size_t)OVL_FINE_WAVES * cap * 20,
+                 bins = OVL_SPLIT_TILE ? (size_t)nf * 16 + (size_t)OVL_SPLIT_TILE * 16
+                                       : (size_t)nf * 8;
     return sort > bins ? sort : bins;
   }
   return 2ull * OVL_FINE_WAVES * cap * 8 + 2ull * nf * 4;
+}
+
+// Exclusive scan of nf <= 4096 LDS bins by a block of OVL_FINE_WAVES waves: each thread a
+// run of nf/512 bins, a wave scan of the runs, then the wave totals (a one-thread serial
+// scan of 4096 bins is a chain of dependent LDS round trips, ~0.1 ms per block).  Ends with
+// a barrier.
+__device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out, uint32_t nf,
+                                                uint32_t *s_wsum) {
+  const uint32_t per = (nf + blockDim.x - 1) / blockDim.x;
+  const uint32_t b0 = threadIdx.x * per;
+  uint32_t run = 0;
+  for (uint32_t f = b0; f < b0 + per && f < nf; f++) run += h[f];
+  uint32_t inc = run;
+  const uint32_t ln = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (ln >= (uint32_t)o) inc += v;
+  }
+  if (ln == 63) s_wsum[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t acc = inc - run;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) acc += s_wsum[w];
+  for (uint32_t f = b0; f < b0 + per && f < nf; f++) { out[f] = acc; acc += h[f]; }
+  __syncthreads();
 }
 
 template <int EM, bool GROUP>
@@ -335,7 +366,7 @@ __global__ void __launch_bounds__(OVL_FINE_WAVES * 64)
 k_fine(FineArgs A) {
   // dynamic LDS sized to the fine buckets (2^fb bins, cap records per wave) so that
   // several blocks share a CU (fine_lds_bytes)
-  extern __shared__ uint64_t s_fine[];
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_fine[];
   uint32_t nf = 1u << A.fb_bits;
   const uint32_t cap = A.cap;
   uint32_t *h = GROUP ? (uint32_t *)s_fine : (uint32_t *)(s_fine + 2 * OVL_FINE_WAVES * cap);
@@ -348,29 +379,9 @@ k_fine(FineArgs A) {
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     atomicAdd(&h[(uint32_t)(A.inR[s0 + i].m >> shift) & (nf - 1)], 1u);
   __syncthreads();
+  __shared__ uint32_t s_wsum[OVL_FINE_WAVES];
 #if OVL_FINE_PSCAN
-  {
-    // exclusive scan of the nf <= 4096 bins: each thread a run of nf/512 bins, a wave scan
-    // of the runs, then the 8 wave totals (a one-thread serial scan of 4096 bins is a chain
-    // of dependent LDS round trips, ~0.1 ms per block)
-    __shared__ uint32_t s_wsum[OVL_FINE_WAVES];
-    const uint32_t per = (nf + blockDim.x - 1) / blockDim.x;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t run = 0;
-    for (uint32_t f = b0; f < b0 + per && f < nf; f++) run += h[f];
-    uint32_t inc = run;
-    const uint32_t ln = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_up(inc, o);
-      if (ln >= (uint32_t)o) inc += v;
-    }
-    if (ln == 63) s_wsum[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    uint32_t acc = inc - run;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) acc += s_wsum[w];
-    for (uint32_t f = b0; f < b0 + per && f < nf; f++) { cur[f] = acc; acc += h[f]; }
-  }
+  block_scan_bins(h, cur, nf, s_wsum);
 #else
   if (threadIdx.x == 0) {                        // nf <= 4096: serial scan is cheap
     uint32_t acc = 0;
@@ -390,11 +401,58 @@ k_fine(FineArgs A) {
     A.fcnt[cb * nf + f] = h[f];
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const Rec2 r = A.inR[s0 + i];
-    uint32_t f = (uint32_t)(r.m >> shift) & (nf - 1);
-    uint32_t slot = atomicAdd(&cur[f], 1u);
-    A.midR[s0 + slot] = r;
+  if (GROUP && OVL_SPLIT_TILE) {
+    // The split through LDS, a tile of records at a time: each tile is ordered by fine
+    // bucket in LDS (tile counts, their scan, a rank from the count's atomic), then written
+    // out with consecutive threads on consecutive slots of a bucket -- runs instead of one
+    // scattered 16-B store per record, whose half-written lines (1,024 open buckets per
+    // block, three blocks per CU) cost the direct split 8.3 of k_fine's 14.8 ms at 50k x
+    // 10 kb.  A fine bucket's order does not matter: the grouping below orders it.
+    constexpr uint32_t T = OVL_SPLIT_TILE > 0 ? OVL_SPLIT_TILE : 512;
+    constexpr uint32_t RPT = T / (OVL_FINE_WAVES * 64);
+    static_assert(RPT * OVL_FINE_WAVES * 64 == T, "tile = whole rounds of the block");
+    uint32_t *tcnt = cur + nf, *tstart = tcnt + nf;
+    Rec2 *stage = (Rec2 *)(tstart + nf);
+    for (uint32_t t0 = 0; t0 < n; t0 += T) {
+      for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) tcnt[f] = 0;
+      __syncthreads();
+      Rec2 r[RPT];
+      uint32_t fb[RPT], rk[RPT];
+#pragma unroll
+      for (uint32_t q = 0; q < RPT; q++) {
+        const uint32_t i = t0 + q * blockDim.x + threadIdx.x;
+        fb[q] = 0xFFFFFFFFu;
+        if (i < n) {
+          r[q] = A.inR[s0 + i];
+          fb[q] = (uint32_t)(r[q].m >> shift) & (nf - 1);
+        }
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < RPT; q++)
+        if (fb[q] != 0xFFFFFFFFu) rk[q] = atomicAdd(&tcnt[fb[q]], 1u);
+      __syncthreads();
+      block_scan_bins(tcnt, tstart, nf, s_wsum);
+#pragma unroll
+      for (uint32_t q = 0; q < RPT; q++)
+        if (fb[q] != 0xFFFFFFFFu) stage[tstart[fb[q]] + rk[q]] = r[q];
+      __syncthreads();
+      const uint32_t tn = n - t0 < T ? n - t0 : T;
+      for (uint32_t j = threadIdx.x; j < tn; j += blockDim.x) {
+        const Rec2 x = stage[j];
+        const uint32_t f = (uint32_t)(x.m >> shift) & (nf - 1);
+        A.midR[s0 + cur[f] + (j - tstart[f])] = x;
+      }
+      __syncthreads();
+      for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cur[f] += tcnt[f];
+      __syncthreads();
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const Rec2 r = A.inR[s0 + i];
+      uint32_t f = (uint32_t)(r.m >> shift) & (nf - 1);
+      uint32_t slot = atomicAdd(&cur[f], 1u);
+      A.midR[s0 + slot] = r;
+    }
   }
   __threadfence_block();
   __syncthreads();
@@ -610,6 +668,18 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
     e.off = oc[2 * i];
     e.cnt = oc[2 * i + 1];
     dst[i] = e;
+  }
+}
+
+// The batch's Bloom filter from its table: every present entry (k-mers and skip entries).
+__global__ void k_bloom_build(const TabEntry *__restrict__ tab, uint64_t nslots, uint64_t *bloom,
+                              uint32_t bits) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const TabEntry e = tab[i];
+    if (e.cnt == 0) continue;
+    atomicOr((unsigned long long *)&bloom[bloom_word(e.key, bits)],
+             (unsigned long long)bloom_mask(e.key));
   }
 }
 

@@ -61,6 +61,10 @@ __device__ __forceinline__ uint32_t qualifying(const uint64_t *occ, uint32_t off
   return lo;
 }
 
+// BLOOM: windows whose k-mer the batch's Bloom filter rejects skip the table (OverlapDriver
+// batches probed by many more queries than they index: most windows miss, and the filter
+// is a fraction of the table's size).
+template <bool BLOOM>
 __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t u = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -94,6 +98,16 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
       if (ok[q]) {
         M[q] = mix64(bases_at(S.w, (int32_t)o) & A.X.kmask);
         slot0[q] = M[q] >> (64 - A.X.tab_bits);
+      }
+    }
+    if constexpr (BLOOM) {
+      uint64_t bw[PU];
+#pragma unroll
+      for (int q = 0; q < PU; q++) bw[q] = ok[q] ? A.X.bloom[bloom_word(M[q], A.X.bloom_bits)] : 0;
+#pragma unroll
+      for (int q = 0; q < PU; q++) {
+        const uint64_t bm = bloom_mask(M[q]);
+        if (ok[q] && (bw[q] & bm) != bm) { ok[q] = false; M[q] = 0; slot0[q] = 0; }
       }
     }
     TabEntry e[PU];
