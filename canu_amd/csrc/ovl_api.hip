@@ -196,9 +196,9 @@ struct ovl_ctx {
   uint64_t cut_windows_hint = 0; // windows of the job's last load-cut batch (0: none yet)
   DBuf<TabEntry> d_tab;
   uint32_t tab_bits = 0, slice_bits = 0;
-  DBuf<uint64_t> d_bloom;        // the batch's Bloom filter (built on first use per index)
+  DBuf<uint64_t> d_bloom;        // the batch's Bloom filter (driver batches: k_table)
   bool bloom_ok = false;
-  uint32_t bloom_bits = 0;
+  uint32_t bloom_w = 0;
 
   // find_overlaps working buffers: kept across calls (grow-only), hipMalloc of tens of
   // GB per call would cost seconds
@@ -673,7 +673,9 @@ static int apply_hash_libs(ovl_ctx *c, uint32_t lo, uint32_t hi) {
 }
 
 // The index over hash reads bgn..end (clipped to the loaded reads by the callers).
-static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
+// bloom: also build the batch's Bloom filter (OverlapDriver batches, whose searches are
+// mostly by reads outside the hash range; see use_bloom)
+static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = false) {
   hipStream_t s = c->stream;
   uint32_t k = c->P.kmer_len;
   c->hash_bgn_iid = bgn;
@@ -834,9 +836,23 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   T.rflags = c->d_flags.p;
   T.first_iid = c->first_iid;
   T.k = k;
+  T.bloom = nullptr;
+  T.bloom_w = 0;
+  if (bloom) {
+    // ~8 filter bits per indexed window (>= distinct k-mers) in every fine bucket's region,
+    // a power of two of 64-bit words, at most 64: ~130 MB for a batch of canu's
+    // --hashbits 23 --hashload 0.75
+    uint64_t words = (8ull * hm[0] + 64ull * nfine - 1) / (64ull * nfine);
+    uint32_t w = 0;
+    while (w < 6 && (1ull << w) < words) w++;
+    if (c->d_bloom.alloc((size_t)nfine << w)) return fail(OVL_ERR_OOM, "bloom filter");
+    T.bloom = c->d_bloom.p;
+    T.bloom_w = w;
+    c->bloom_w = w;
+  }
   uint32_t S = 1u << c->slice_bits;
   uint32_t wpb = std::max<uint32_t>(1, std::min<uint32_t>(4, 65536u / (16u * S)));
-  size_t lds = (size_t)wpb * 16u * S;
+  size_t lds = (size_t)wpb * (16u * S + (bloom ? 8u << T.bloom_w : 0u));
   if (lds > 65536) return fail(OVL_ERR_UNSUPPORTED, "k-mer slice too large (%u)", S);
   hipLaunchKernelGGL(k_table, dim3((nfine + wpb - 1) / wpb), dim3(64 * wpb), lds, s, T);
   HIPC(hipGetLastError());
@@ -849,6 +865,7 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end) {
   // the build scratch (2 x 16 B per window) stays allocated for the next build: freeing and
   // re-allocating gigabytes per job costs tens of ms on some hosts (and HBM is plentiful)
   c->have_index = true;
+  c->bloom_ok = bloom;
   return OVL_OK;
 }
 
@@ -1046,10 +1063,10 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
         eb = id;
       }
     }
-    if ((rc = build_index(c, bgn, eb)) == OVL_ERR_OOM) {
+    if ((rc = build_index(c, bgn, eb, true)) == OVL_ERR_OOM) {
       // the previous batch's search buffers make room (the next search grows them again)
       release_find_buffers(c);
-      rc = build_index(c, bgn, eb);
+      rc = build_index(c, bgn, eb, true);
     }
     if (rc) return rc;
     if (!load_may_cut) break;
@@ -1077,7 +1094,7 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
       if (entries >= entry_limit) { el = bgn + i; reached = true; break; }
     }
     if (reached) {
-      if (el < eb && (rc = build_index(c, bgn, el))) return rc;
+      if (el < eb && (rc = build_index(c, bgn, el, true))) return rc;
       e = el;
       uint64_t cw = 0;
       for (uint32_t id = bgn; id <= el; id++) {
@@ -1115,33 +1132,15 @@ IndexDev index_dev(const ovl_ctx *c) {
   X.k = c->P.kmer_len;
   X.kmask = (1ull << (2 * c->P.kmer_len)) - 1;
   X.bloom = nullptr;
-  X.bloom_bits = 0;
+  X.bloom_w = 0;
   return X;
-}
-
-// The current index's Bloom filter (k_bloom_build over the table), ~8 bits per indexed
-// window (>= distinct k-mers): at canu's --hashbits 23 --hashload 0.75 a batch of ~130 M
-// distinct k-mers takes ~130 MB, a fraction of its table and within the MALL.
-static int ensure_bloom(ovl_ctx *c) {
-  if (c->bloom_ok) return OVL_OK;
-  uint32_t bits = 10;
-  while (bits < 34 && (1ull << bits) < (c->index_records + 7) / 8) bits++;
-  if (c->d_bloom.alloc(1ull << bits)) return fail(OVL_ERR_OOM, "bloom filter 2^%u words", bits);
-  HIPC(hipMemsetAsync(c->d_bloom.p, 0, 8ull << bits, c->stream));
-  const uint64_t nslots = 1ull << c->tab_bits;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>((nslots + 255) / 256, 8ull * c->n_cu);
-  hipLaunchKernelGGL(k_bloom_build, dim3(grid), dim3(256), 0, c->stream, c->d_tab.p, nslots,
-                     c->d_bloom.p, bits);
-  HIPC(hipGetLastError());
-  c->bloom_bits = bits;
-  c->bloom_ok = true;
-  return OVL_OK;
 }
 
 // Whether a search of ref reads bgn..end should probe through the Bloom filter: when at
 // least 3/4 of them lie outside the hash range (OverlapDriver's later batches, probed by
 // every earlier query), most of their windows miss the table.  OVL_BLOOM=0/1 forces it.
 static bool use_bloom(const ovl_ctx *c, uint32_t bgn, uint32_t end) {
+  if (!c->bloom_ok) return false;                 // only driver batches build one
   if (const char *e = getenv("OVL_BLOOM")) return atoi(e) != 0;
   if (end < bgn) return false;
   const uint64_t q = (uint64_t)end - bgn + 1;
@@ -1729,10 +1728,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     A.nu = A.nn = A.np = 0;
     return rc;
   };
-  // the filter is built once per index, before the first search that wants it
   const bool bloom = nu > 0 && use_bloom(c, bgn, end);
-  if (bloom)
-    if (int rc = ensure_bloom(c)) return rc;
   uint64_t chunk = 0;
   while (u0 < nu) {
     const int slot = pipe ? (int)(chunk & 1) : 0;
@@ -1763,7 +1759,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     PA.X = index_dev(c);
     if (bloom) {
       PA.X.bloom = c->d_bloom.p;
-      PA.X.bloom_bits = c->bloom_bits;
+      PA.X.bloom_w = c->bloom_w;
     }
     PA.units = d_units.p;
     PA.rbase = d_rbase.p;

@@ -211,17 +211,20 @@ struct IndexDev {
   uint32_t        slice_bits;// log2(slots per slice)
   uint32_t        k;
   uint64_t        kmask;
-  const uint64_t *bloom;     // blocked Bloom filter of the table's keys, or null
-  uint32_t        bloom_bits;// log2(its 64-bit words)
+  const uint64_t *bloom;     // the batch's Bloom filter (partitioned by fine bucket), or null
+  uint32_t        bloom_w;   // log2(filter words per fine bucket)
 };
 
 // The blocked Bloom filter of a hash batch's distinct k-mers (every table entry, the -k
 // skip entries included): one 64-bit word per key, 4 bits in it.  No false negatives, so a
-// window it rejects is a window the table lookup would not have found.  The word comes from
-// the low bits of mix64(kmer) (the table slot uses the top bits), the bits from an odd
-// multiple of it.
-__host__ __device__ __forceinline__ uint64_t bloom_word(uint64_t M, uint32_t bits) {
-  return M & ((1ull << bits) - 1);
+// window it rejects is a window the table lookup would not have found.  The filter is
+// partitioned like the table: fine bucket f (the top bits of mix64(kmer), the table slice's
+// index) owns words [f << w, (f + 1) << w), so k_table builds each region in LDS beside its
+// slice and writes it whole -- no global atomics.  The word within the region comes from
+// the low bits of mix64(kmer), the 4 bits from an odd multiple of it.
+__host__ __device__ __forceinline__ uint64_t bloom_word(uint64_t slot0, uint32_t slice_bits,
+                                                       uint64_t M, uint32_t w) {
+  return ((slot0 >> slice_bits) << w) | (M & ((1ull << w) - 1));
 }
 __host__ __device__ __forceinline__ uint64_t bloom_mask(uint64_t M) {
   const uint64_t h = M * 0x9E3779B97F4A7C15ull;

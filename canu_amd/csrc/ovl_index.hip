@@ -582,6 +582,8 @@ struct TableArgs {
   uint32_t *rflags;              // bit1 lfrag_end_screened, bit2 rfrag_end_screened
   uint32_t first_iid;
   uint32_t k;
+  uint64_t *bloom;               // the batch's Bloom filter (bloom_word), or null
+  uint32_t bloom_w;              // log2(filter words per fine bucket)
 };
 
 #define OVL_HOPELESS_MATCH 90
@@ -594,8 +596,12 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
   uint32_t S = 1u << A.slice_bits;
   uint64_t *key = (uint64_t *)smem + (size_t)wave * S * 2;     // S keys then S (off,cnt)
   uint32_t *oc = (uint32_t *)(key + S);
+  // the fine bucket's Bloom filter region, after the waves' slices
+  const uint32_t BW = A.bloom ? 1u << A.bloom_w : 0u;
+  uint64_t *lb = (uint64_t *)smem + (size_t)(blockDim.x >> 6) * S * 2 + (size_t)wave * BW;
   if (f >= A.nfine) return;
   for (uint32_t i = lane; i < S; i += 64) { key[i] = 0; oc[2 * i] = 0; oc[2 * i + 1] = 0; }
+  for (uint32_t i = lane; i < BW; i += 64) lb[i] = 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t fs = A.fstart[f], fn = A.fcnt[f];
@@ -656,6 +662,7 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
       }
       key[slot] = M;
       oc[2 * slot] = off;
+      if (BW) atomicOr((unsigned long long *)&lb[M & (BW - 1)], (unsigned long long)bloom_mask(M));
     }
     cur_m = nxt_m;
   }
@@ -669,18 +676,7 @@ __global__ void __launch_bounds__(256) k_table(TableArgs A) {
     e.cnt = oc[2 * i + 1];
     dst[i] = e;
   }
-}
-
-// The batch's Bloom filter from its table: every present entry (k-mers and skip entries).
-__global__ void k_bloom_build(const TabEntry *__restrict__ tab, uint64_t nslots, uint64_t *bloom,
-                              uint32_t bits) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const TabEntry e = tab[i];
-    if (e.cnt == 0) continue;
-    atomicOr((unsigned long long *)&bloom[bloom_word(e.key, bits)],
-             (unsigned long long)bloom_mask(e.key));
-  }
+  for (uint32_t i = lane; i < BW; i += 64) A.bloom[((size_t)f << A.bloom_w) + i] = lb[i];
 }
 
 // Hash_Entries of Build_Hash_Index (Hash_Insert :336-341): a distinct k-mer takes a table

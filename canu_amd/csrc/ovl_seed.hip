@@ -103,7 +103,8 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
     if constexpr (BLOOM) {
       uint64_t bw[PU];
 #pragma unroll
-      for (int q = 0; q < PU; q++) bw[q] = ok[q] ? A.X.bloom[bloom_word(M[q], A.X.bloom_bits)] : 0;
+      for (int q = 0; q < PU; q++)
+        bw[q] = ok[q] ? A.X.bloom[bloom_word(slot0[q], A.X.slice_bits, M[q], A.X.bloom_w)] : 0;
 #pragma unroll
       for (int q = 0; q < PU; q++) {
         const uint64_t bm = bloom_mask(M[q]);

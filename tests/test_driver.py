@@ -242,3 +242,29 @@ def test_gpu_driver_library_filters(built):
     assert got.shape == ref.shape and np.array_equal(got, ref)
     for rk, ok in STAT_KEYS:
         assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_gpu_bloom_filter_is_exact(built, monkeypatch, mode):
+    """The probe's Bloom filter (OverlapDriver batches probed mostly by reads outside the
+    hash range; ensure_bloom / use_bloom in ovl_api.hip) has no false negatives, so records
+    and every -s counter are those of the table alone: the production-batch job of
+    10 kb reads in 70-read hash batches with the filter forced off (OVL_BLOOM=0) and on
+    for every search (OVL_BLOOM=1, also the searches it would skip) against the oracle."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    monkeypatch.setenv("OVL_BLOOM", mode)
+    rs = synth_reads(n_reads=301, read_len=10_000, genome_len=400_000, error_rate=0.015, seed=26)
+    P = _params()
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=70, Num_PThreads=8).finalize()
+    oic = OverlapInCore(O, device=0)
+    got = oic.run_driver(rs)
+    st = oic.stats()
+    oic.close()
+    want, wst, batches = oracle.run_oracle_driver(rs, P, threads=8, hashstrings=70,
+                                                  with_stats=True)
+    assert st["hash_batches"] == len(batches) >= 4
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for _, ok in STAT_KEYS:
+        assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
