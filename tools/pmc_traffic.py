@@ -98,12 +98,16 @@ def main():
     if not fetch or not write:
         sys.exit(f"no FETCH_SIZE / WRITE_SIZE passes for tag {tag} under {OUT}: "
                  "profiles/traffic.json left as it is")
-    avg_ns = {}
+    # instances of one kernel (k_extend's staged classes, k_probe<BLOOM>) add up: total time
+    # over total calls
+    tot_ns, calls_ns = defaultdict(float), defaultdict(int)
     if stats:
         for row in csv.DictReader(open(stats[0])):
             k = short(row["Name"])
             if k:
-                avg_ns[k] = float(row["AverageNs"])
+                tot_ns[k] += float(row["TotalDurationNs"])
+                calls_ns[k] += int(row["Calls"])
+    avg_ns = {k: tot_ns[k] / max(1, calls_ns[k]) for k in tot_ns}
     iss = issue(tag)
     traffic = {}
     with open(os.path.join(PROF, f"{tag}_traffic.csv"), "w") as f:
