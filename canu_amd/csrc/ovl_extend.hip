@@ -749,6 +749,8 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   typedef __attribute__((address_space(1))) cell_t g_cell_t;
   g_cell_t *clog = uni_ptr((g_cell_t *)rows);     // scalar base: stores use saddr + offset
   clog[(B + (int32_t)lane) & (LW - 1)] = (cell_t)R[0];
+  typedef __attribute__((address_space(1))) uint8_t g_u8;
+  g_u8 *clogb = (g_u8 *)clog;
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
   // interleave); their lanes beyond the band are inactive by the lane predicates
   constexpr int JU = 1;
@@ -758,12 +760,13 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   bool ended = false;
   int32_t end_d = 0, end_row = 0, end_pp = 0;
   // One exit: every way a row ends the loop (the end reached, an empty band, the band
-  // outgrowing the window, the error limit) sets `stop`, tested once per row; with four
-  // breaks the structurizer carried exit flags through every row's tail (~12 scalar
+  // outgrowing the window, the error limit) makes `go` negative, tested once per row; with
+  // four breaks the structurizer carried exit flags through every row's tail (~12 scalar
   // instructions per row).  The window is re-anchored for the next row at the end of this
   // one (row 1 needs none: B = -3, pl = pr = 0).
-  uint32_t stop = limit < 1 ? 1u : 0u;
-  while (!stop) {
+  int32_t end_e = 0;
+  int32_t go = limit - 1;                      // the loop runs while go >= 0
+  while (go >= 0) {
     PROF_T(pt_row);
     const int32_t ML = mlim[e];
     const int32_t right = pr + 1;
@@ -847,29 +850,49 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     PROF_T(pt_cont);
     PROF_ADD(pc_cont, pt_b, pt_cont);
     // ---- C: end test and Edit_Match_Limit pruning, one pass ---------------------------
-    // (scalar work per chunk kept minimal: the end masks are only OR-ed -- the end row is
-    // rare and re-scanned below -- and the kept range is two unsigned mins, of window
-    // offsets and of reversed offsets: s_ff1 / s_flbit give -1 on an empty mask, so an
-    // empty chunk contributes ~0u to both)
-    uint64_t endany = 0;
-    uint32_t nlo = 0xffffffffu;                // min window offset of a kept lane
-    uint32_t nhi = 0xffffffffu;                // min reversed offset (64J-1 - o) of one
+    // Only two masks are reduced on the common row: the kept range's left end lies in chunk
+    // 0 (the window is anchored at the band's left edge) and its right end in the last
+    // chunk, jr.  So chunk 0's and chunk jr's kept masks are kept and the other chunks cost
+    // no scalar work; when either is empty (~2 % of rows: the pruning emptied the band's
+    // first or last chunk, or the whole band) every chunk is rescanned below.  The end test
+    // is a per-lane min of the bases left, one ballot per row.  (The per-chunk s_ff1 /
+    // s_flbit / min reduction was 6 scalar instructions per chunk.)
+    int32_t rmin = RM[0];
+    uint64_t km0 = 0, kml = 0;
 #pragma unroll
     for (int j = 0; j < J; j++) {
       if (j >= JU && j > jr) break;
       const int32_t d = B + 64 * j + (int32_t)lane;
-      endany |= __builtin_amdgcn_ballot_w64(RM[j] == 0);
-      const uint64_t km = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
-      // s_ff1 / s_flbit give ~0u on an empty mask, which the unsigned mins ignore: no
-      // compare-and-select per chunk (the compiler does not know that of ctz / clz and
-      // adds one; 3 scalar instructions of 12 per chunk, -1.6 % extension time)
-      uint32_t f1, fb;
-      asm("s_ff1_i32_b64 %0, %1" : "=s"(f1) : "s"(km));
-      asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(km));
-      const uint32_t c1 = f1 | (uint32_t)(64 * j);
-      nlo = c1 < nlo ? c1 : nlo;
-      const uint32_t g = fb | (uint32_t)(64 * (J - 1 - j));
-      nhi = g < nhi ? g : nhi;
+      if (j > 0) rmin = RM[j] < rmin ? RM[j] : rmin;
+      kml = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
+      if (j == 0) km0 = kml;
+    }
+    const uint64_t endany = __builtin_amdgcn_ballot_w64(rmin == 0);
+    uint32_t nlo, nhi;                         // min window offset of a kept lane; min
+                                               // reversed offset (64J-1 - o) of one
+    // s_ff1 / s_flbit give ~0u on an empty mask: one signed test of their OR sends the row
+    // to the rescan (a boolean AND of the two mask tests cost 6 scalar instructions)
+    asm("s_ff1_i32_b64 %0, %1" : "=s"(nlo) : "s"(km0));
+    asm("s_flbit_i32_b64 %0, %1" : "=s"(nhi) : "s"(kml));
+    if ((int32_t)(nlo | nhi) >= 0) {
+      nhi += (uint32_t)(64 * (J - 1)) - (uint32_t)(jr << 6);
+    } else {
+      // the unsigned mins ignore an empty chunk's ~0u
+      nlo = 0xffffffffu;
+      nhi = 0xffffffffu;
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        if (j >= JU && j > jr) break;
+        const int32_t d = B + 64 * j + (int32_t)lane;
+        const uint64_t km = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
+        uint32_t f1, fb;
+        asm("s_ff1_i32_b64 %0, %1" : "=s"(f1) : "s"(km));
+        asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(km));
+        const uint32_t c1 = f1 | (uint32_t)(64 * j);
+        nlo = c1 < nlo ? c1 : nlo;
+        const uint32_t g = fb | (uint32_t)(64 * (J - 1 - j));
+        nhi = g < nhi ? g : nhi;
+      }
     }
     const int32_t nro = 64 * J - 1 - (int32_t)nhi;
 
@@ -879,10 +902,17 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
 #ifdef OVL_PROFILE
     pc_rows++;
 #endif
+    // Every way a row ends the loop sets e past the limit (the end row keeps its own e in
+    // end_e; an empty band needs none) and falls through to one signed test of two
+    // differences, so the common row reaches the back-edge with no stop flag: e > limit, or
+    // the next row would not fit the window (pr + 3 > B + 64J - 1 -- told apart after the
+    // loop by e <= limit: the pair is deferred).  The flag of a three-way branch cost ~6
+    // scalar instructions per row.
     if (endany) {                              // the first d in order that reached the end
+      // lowest chunk last (no break: the rare row stays out of the common row's CFG)
 #pragma unroll
-      for (int j = 0; j < J; j++) {
-        if (j >= JU && j > jr) break;
+      for (int j = J - 1; j >= 0; j--) {
+        if (j >= JU && j > jr) continue;
         const uint64_t em = __builtin_amdgcn_ballot_w64(RM[j] == 0);
         if (em) {
           const int32_t l = (int32_t)__builtin_ctzll(em);
@@ -891,13 +921,13 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
           // row e-1 at d+1 (R still holds row e-1)
           end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
                  : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
-          break;
         }
       }
       ended = true;
-      stop = 1;                                // end reached
+      end_e = e;
+      e = limit + 1;
     } else if (nlo == 0xffffffffu) {
-      stop = 1;                                // Left > Right
+      e = limit + 1;                           // Left > Right (e is not read after)
     } else {
       const int32_t nl = B + (int32_t)nlo;
       const int32_t nr = B + nro;
@@ -905,11 +935,13 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       // prune to [nl, nr] (the rest becomes the -2 sentinel), log the row for the
       // traceback (cells up to nr+2 are read), longest row with the first d on ties: one
       // wave max over keys (value << WB | 64J-1 - window offset), so a larger value wins and
-      // among equal values the smaller d (values < 2^21 and -2 keep the order in 32 bits)
+      // among equal values the smaller d (values < 2^21 and -2 keep the order in 32 bits).
+      // The row's stripe is a 32-bit byte offset OR-ed with the cell's (the stripe is a power
+      // of two): one scalar shift per row instead of a 64-bit row pointer.
       int32_t kmx = NEG;
       const uint32_t kspan = (uint32_t)(nr - nl);
       const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
-      g_cell_t *crow = clog + (size_t)e * LW;
+      const uint32_t erow = (uint32_t)e * (uint32_t)(LW * sizeof(cell_t));
 #pragma unroll
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jrs) break;
@@ -918,7 +950,8 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
         R[j] = v;
         const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
         kmx = key > kmx ? key : kmx;
-        crow[(d & (LW - 1))] = (cell_t)v;
+        *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
+            (cell_t)v;
       }
       const int32_t K = wave_max(kmx);
       const int32_t M = K >> WB;
@@ -940,60 +973,57 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       PROF_T(pt_rest);
       PROF_ADD(pc_rest, pt_chunks, pt_rest);
       e++;
-      if (e > limit) {
-        stop = 1;
-      } else {
-        // The window is anchored at the band: B <= pl-3 < B+16, so the row's chunks are
-        // 0..jr with little waste in chunk 0.  When pl-3 leaves [B, B+16) the window moves to
-        // B = pl-9: whole chunks by register moves, the rest by one ds_bpermute per chunk
-        // (about one row in ten).  It must also hold pr+3 (the reads of this row and the log
-        // of the next).
-        if ((uint32_t)(pl - 3 - B) >= 16u) {
-          const int32_t nb = pl - 9;
-          int32_t sft = nb - B;
-          while (sft >= 64) {
+      // The window is anchored at the band: B <= pl-3 < B+16, so the row's chunks are
+      // 0..jr with little waste in chunk 0.  When pl-3 leaves [B, B+16) the window moves to
+      // B = pl-9: whole chunks by register moves, the rest by one ds_bpermute per chunk
+      // (about one row in ten).  It must also hold pr+3 (the reads of this row and the log
+      // of the next).  (Past the limit B is no longer read.)
+      if ((uint32_t)(pl - 3 - B) >= 16u) {
+        const int32_t nb = pl - 9;
+        int32_t sft = nb - B;
+        while (sft >= 64) {
 #pragma unroll
-            for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
-            R[J - 1] = -2;
-            sft -= 64;
+          for (int j = 0; j < J - 1; j++) R[j] = R[j + 1];
+          R[J - 1] = -2;
+          sft -= 64;
+        }
+        while (sft <= -64) {
+#pragma unroll
+          for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
+          R[0] = -2;
+          sft += 64;
+        }
+        if (sft != 0) {
+          const int32_t ls = (int32_t)lane + sft;
+          const int32_t src = (ls & 63) << 2;
+          int32_t bp[J];
+#pragma unroll
+          for (int j = 0; j < J; j++) bp[j] = __builtin_amdgcn_ds_bpermute(src, R[j]);
+          if (sft > 0) {
+            const bool hi = ls >= 64;            // comes from the next chunk up
+#pragma unroll
+            for (int j = 0; j < J; j++) R[j] = hi ? (j + 1 < J ? bp[j + 1 < J ? j + 1 : j] : -2) : bp[j];
+          } else {
+            const bool lo = ls < 0;              // comes from the chunk below
+#pragma unroll
+            for (int j = 0; j < J; j++) R[j] = lo ? (j > 0 ? bp[j > 0 ? j - 1 : 0] : -2) : bp[j];
           }
-          while (sft <= -64) {
-#pragma unroll
-            for (int j = J - 1; j > 0; j--) R[j] = R[j - 1];
-            R[0] = -2;
-            sft += 64;
-          }
-          if (sft != 0) {
-            const int32_t ls = (int32_t)lane + sft;
-            const int32_t src = (ls & 63) << 2;
-            int32_t bp[J];
-#pragma unroll
-            for (int j = 0; j < J; j++) bp[j] = __builtin_amdgcn_ds_bpermute(src, R[j]);
-            if (sft > 0) {
-              const bool hi = ls >= 64;            // comes from the next chunk up
-#pragma unroll
-              for (int j = 0; j < J; j++) R[j] = hi ? (j + 1 < J ? bp[j + 1 < J ? j + 1 : j] : -2) : bp[j];
-            } else {
-              const bool lo = ls < 0;              // comes from the chunk below
-#pragma unroll
-              for (int j = 0; j < J; j++) R[j] = lo ? (j > 0 ? bp[j > 0 ? j - 1 : 0] : -2) : bp[j];
-            }
-          }
-          B = nb;
+        }
+        B = nb;
 #ifdef OVL_PROFILE
-          pc_recenter++;
+        pc_recenter++;
 #endif
-        }
-        if (pr + 3 > B + 64 * J - 1) {         // the next row would not fit the window
-          out.ovf = 1;
-          stop = 1;
-        }
       }
     }
+    go = (limit - e) | (B + 64 * J - 4 - pr);
   }
+  // stopped with rows left to compute: the window overflowed (every other stop sets e
+  // past the limit)
+  if (e <= limit) out.ovf = 1;
   if (out.ovf) return out;
   const int32_t max_score_best_d = ms_B + ((1 << WB) - 1) - (ms_key & ((1 << WB) - 1));
-  if (ended) {                               // forward.C:177-232, at row e
+  if (ended) {                               // forward.C:177-232, at row end_e
+    const int32_t e = end_e;
     double  score = end_row * bmv - e;
     int32_t tail_len = end_row - max_score_len;
     double  slope = (double)(max_score - score) / tail_len;
