@@ -1627,6 +1627,19 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
           EA.pair_next = x_ctr.p + ctr_next[ci];
           EA.defer = defer_buf[ci & 1];
           EA.ndefer = x_ctr.p + ctr_defer[ci];
+          // without the pipeline, a later class whose input list is empty is not launched
+          // (the host reads the previous class's defer count, as for the generic kernel
+          // below): the bench job's one staged launch then is the extension's only launch
+          bool launch = true;
+          if (!pipe && ci > 0) {
+            uint32_t nd = 0;
+            HIPC(hipMemcpyAsync(&nd, x_ctr.p + ctr_defer[ci - 1], 4, hipMemcpyDeviceToHost, xs));
+            HIPC(hipStreamSynchronize(xs));
+            launch = nd > 0;
+          }
+          if (!launch) {
+            // an empty class defers nothing: its counter stays 0 for the next one
+          } else {
           n_ext_launch++;
           if (g.wide && g.l16)
             hipLaunchKernelGGL((k_extend<true, true, false, 2 * OVL_RJ>), dim3(g.waves / g.wpb),
@@ -1639,6 +1652,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
           else
             hipLaunchKernelGGL((k_extend<true, false>), dim3(g.waves / g.wpb), dim3(64 * g.wpb), g.lds, xs, EA);
           HIPC(hipGetLastError());
+          }
           EA.list = defer_buf[ci & 1];
           EA.npairs_dev = x_ctr.p + ctr_defer[ci];
           EA.restore = 1;          // a deferred pair may have had nodes removed (~Len)
