@@ -52,6 +52,23 @@ def test_basic_default(built):
     assert got.shape[0] > 100
 
 
+def test_extension_launches_only_classes_with_pairs(built):
+    """Later extension classes whose input list is empty are not launched (find_impl reads
+    the previous class's defer count): 2 kb reads fit the one staged tier, so the job makes
+    one launch plus one per later class (wide, generic) that actually received pairs."""
+    rs = synth_reads(150, 2000, 30_000, 0.02, seed=1)
+    oic = OverlapInCore(_params(), device=0)
+    oic.load_reads(rs)
+    oic.build_hash_index(1, 0xFFFFFFFF)
+    oic.find_overlaps(1, 0xFFFFFFFF)
+    st = oic.stats()
+    oic.close()
+    assert st["pairs"] > 0
+    want = 1 + (st["long_pairs"] > 0) + (st["generic_pairs"] > 0)
+    assert st["extend_launches"] == want, (st["extend_launches"], st["staged_pairs"],
+                                           st["long_pairs"], st["generic_pairs"])
+
+
 def test_high_erate(built):
     rs = synth_reads(100, 3000, 30_000, 0.05, seed=2)
     _check(rs, _params(erate=0.144))
