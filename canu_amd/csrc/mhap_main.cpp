@@ -101,13 +101,20 @@ bool read_filter(const char *path, uint32_t k, std::string &kmers, std::vector<d
   gzFile G = gzopen(path, "rb");
   if (!G) return false;
   char buf[4096];
+  bool first = true;
   while (gzgets(G, buf, sizeof buf)) {
-    char *tab = strchr(buf, '\t');
-    if (!tab) continue;                          // the count line
-    const size_t L = (size_t)(tab - buf);
+    // the first line is skipped only when it is the numeric count line; a k-mer line
+    // without a fraction counts as fraction 1 (as canu_amd/mhap.py reads it)
+    const size_t L = strcspn(buf, " \t\r\n");
+    const bool count_line = first && L > 0 && strspn(buf, "0123456789") == L &&
+                            buf[L] != '\t' && buf[L] != ' ';
+    first = false;
+    if (L == 0 || count_line) continue;
     if (L != k) continue;
     kmers.append(buf, L);
-    fr.push_back(strtod(tab + 1, nullptr));
+    const char *f = buf + L;
+    while (*f == ' ' || *f == '\t') f++;
+    fr.push_back((*f && *f != '\n' && *f != '\r') ? strtod(f, nullptr) : 1.0);
   }
   gzclose(G);
   return true;

@@ -851,9 +851,18 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = fals
     c->bloom_w = w;
   }
   uint32_t S = 1u << c->slice_bits;
-  uint32_t wpb = std::max<uint32_t>(1, std::min<uint32_t>(4, 65536u / (16u * S)));
-  size_t lds = (size_t)wpb * (16u * S + (bloom ? 8u << T.bloom_w : 0u));
-  if (lds > 65536) return fail(OVL_ERR_UNSUPPORTED, "k-mer slice too large (%u)", S);
+  // LDS per wave: its slice and, with the filter, its fine bucket's filter region.  A slice
+  // whose wave does not fit 64 KB with the filter is built without it (the filter is only a
+  // shortcut in front of the table); without it, it is refused
+  if (bloom && 16ull * S + (8ull << T.bloom_w) > 65536) {
+    bloom = false;
+    T.bloom = nullptr;
+    T.bloom_w = 0;
+  }
+  const uint64_t per_wave = 16ull * S + (bloom ? 8ull << T.bloom_w : 0ull);
+  if (per_wave > 65536) return fail(OVL_ERR_UNSUPPORTED, "k-mer slice too large (%u)", S);
+  uint32_t wpb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, 65536ull / per_wave));
+  size_t lds = (size_t)wpb * per_wave;
   hipLaunchKernelGGL(k_table, dim3((nfine + wpb - 1) / wpb), dim3(64 * wpb), lds, s, T);
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(c->ev[1], s));
@@ -941,6 +950,11 @@ static void release_find_buffers(ovl_ctx *c) {
   f.ok64a.release(); f.ok64b.release(); f.dkey.release(); f.oa.release(); f.ob.release();
   f.ucnt.release(); f.useg.release(); f.hcnt.release(); f.hbase.release(); f.hbuf.release();
   f.rows.release(); f.rowdir.release(); f.deltas.release();
+  // the extension accumulator's buffers, once nothing waits in them
+  if (c->acc.np == 0) {
+    c->acc.units.release(); c->acc.pnodes.release(); c->acc.pairs.release();
+    c->acc.nu = c->acc.nn = 0;
+  }
 }
 
 // HBM figures of the last index_window_cap call, for error messages
@@ -956,7 +970,9 @@ static uint64_t index_window_cap(ovl_ctx *c) {
                           (uint64_t)c->d_tab.n * sizeof(TabEntry) + f.probe.n * sizeof(Probe) +
                           (f.pool.n + f.pnodes[0].n + f.pnodes[1].n) * sizeof(Node) +
                           (f.pairs[0].n + f.pairs[1].n) * sizeof(PairRec) +
-                          4ull * (f.rows.n + f.rowdir.n + f.deltas.n);
+                          4ull * (f.rows.n + f.rowdir.n + f.deltas.n) +
+                          c->acc.units.n * sizeof(Unit) + c->acc.pnodes.n * sizeof(Node) +
+                          c->acc.pairs.n * sizeof(PairRec);
     // the search and extension buffers of the batch are sized by budget (up to ~64 GB on a
     // 288 GB part): keep that much aside, or a fifth of a smaller device
     const uint64_t avail = fr + held;

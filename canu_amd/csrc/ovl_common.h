@@ -269,7 +269,9 @@ struct PairRec {
   uint32_t node_off;     // first node (list order) in the pair-node array
   uint32_t node_cnt;
   int32_t  diag_ct, diag_bgn, diag_end;
-  uint32_t flags;        // bit0 consistent, bit1 unit left_end_screened, bit2 right
+  uint32_t flags;        // bit0 consistent, bit1 unit left_end_screened, bit2 right,
+                         // bit3 / bit4 the target's left / right end screened (as the
+                         // hash batch that found the pair left them)
 };
 
 // Match_Node_t (prefixEditDistance.H:60)

@@ -1510,7 +1510,9 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
   int32_t S_Len = S.len, t_len = T.len;
   Node *nodes = X.pnodes + P.node_off;
   int32_t nn = (int32_t)P.node_cnt;
-  uint32_t trf = X.R.flags[P.tgt];
+  // the target's screened-end bits as its hash batch set them (PairRec bits 3 / 4): the
+  // read flags themselves belong to whichever batch was built last
+  const uint32_t trf = (P.flags >> 2) & 6u;
   bool consistent = P.flags & 1u;
   bool lscr = P.flags & 2u, rscr = P.flags & 4u;
 

@@ -458,7 +458,11 @@ __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32
     pr2.diag_ct = s.diag_ct;
     pr2.diag_bgn = s.diag_bgn;
     pr2.diag_end = s.diag_end;
-    pr2.flags = (s.consistent ? 1u : 0u) | (uflags & 6u);
+    // the target's screened ends (bits 1 / 2 of its read flags, set by this hash batch's
+    // k_table) are copied here: the pair may be extended after a later batch's build has
+    // cleared them (the extension accumulator holds pairs across hash batches)
+    pr2.flags = (s.consistent ? 1u : 0u) | (uflags & 6u) |
+                ((A.R.flags[pr2.tgt] & 6u) << 2);
     A.pairs[pbase + rank] = pr2;
   }
 }

@@ -214,7 +214,7 @@ def read_frequency_file(path: str, k: int) -> tuple[list[str], np.ndarray]:
             parts = line.split()
             if not parts:
                 continue
-            if j == 0 and len(parts) == 1:
+            if j == 0 and len(parts) == 1 and parts[0].isdigit():
                 continue                                   # the count line
             if len(parts[0]) != k:
                 raise MhapError(-4, f"{path}:{j + 1}: k-mer of length {len(parts[0])}, not {k}")

@@ -173,6 +173,17 @@ def reference_available() -> bool:
     return os.path.exists(REF_BIN)
 
 
+def require_reference(mhap_convert: bool = False) -> None:
+    """The -m gpu parity tests compare with the reference itself (oic_ref, and mhapConvert
+    for the MHAP output format).  Both are built in the build container and travel to the
+    GPU box with the tree, so their absence there is a broken setup: fail, never skip."""
+    missing = [p for p in [REF_BIN] + ([MHAPCONVERT_BIN] if mhap_convert else [])
+               if not os.path.exists(p)]
+    if missing:
+        raise AssertionError(f"reference checker(s) not built: {missing} "
+                             "(run __graft_entry__.build() where /root/reference exists)")
+
+
 def read_ovb_reference(path: str) -> np.ndarray:
     """Records of an .ovb in FILE order, read by the reference's own ovFile reader
     (oic_ref --read-ovb, ref_harness.cpp)."""

@@ -93,13 +93,13 @@ def _frequent_mers(rs, k=22, n=40):
     return out
 
 
-@needs_ref
 @pytest.mark.gpu
 @pytest.mark.parametrize("job", ["utg", "partial_threads", "partial_limit"])
 def test_gpu_cli_canu_job(cli, job):
     """overlap.sh's command line on a reference-written gkpStore: the .ovb read back by the
     reference's ovFile reader equals the reference overlapInCore's records, the .counts
     file is byte-identical, the -s statistics line-identical."""
+    oracle.require_reference()
     rs = synth_reads(240, 6000, 150_000, 0.015, seed=33, n_repeats=4, repeat_len=300,
                      len_jitter=0.3)
     hb, he, rb, re_ = (1, 240, 1, 240) if job == "utg" else (31, 230, 11, 200)

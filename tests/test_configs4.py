@@ -94,11 +94,11 @@ def test_rank_jobs_union_and_reference():
     for j in _jobs(2):
         rec, st = _gpu_job(rs, j["h"], j["r"])
         assert st["hash_batches"] >= 2
-        if oracle.reference_available():
-            ref, ref_st = _ref_job(rs, j["h"], j["r"])
-            assert rec.shape == ref.shape and np.array_equal(rec, ref), j
-            for rk, mk in STAT_KEYS:
-                assert ref_st[rk] == st[mk], (j, rk)
+        oracle.require_reference()
+        ref, ref_st = _ref_job(rs, j["h"], j["r"])
+        assert rec.shape == ref.shape and np.array_equal(rec, ref), j
+        for rk, mk in STAT_KEYS:
+            assert ref_st[rk] == st[mk], (j, rk)
         parts.append(rec)
     union = oracle.sort_records(np.concatenate(parts))
     assert union.shape == whole.shape and np.array_equal(union, whole)

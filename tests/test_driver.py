@@ -119,10 +119,10 @@ def test_gpu_driver_vs_oracle_and_reference(built, case):
     assert got.shape == want.shape and np.array_equal(got, want)
     for _, ok in STAT_KEYS:
         assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
-    if oracle.reference_available():
-        ref, rst = _reference(rs, P, batch, threads, rr)
-        assert np.array_equal(got, ref)
-        assert st["total_overlaps"] == rst["total"]
+    oracle.require_reference()
+    ref, rst = _reference(rs, P, batch, threads, rr)
+    assert np.array_equal(got, ref)
+    assert st["total_overlaps"] == rst["total"]
 
 
 @pytest.mark.gpu
@@ -144,12 +144,12 @@ def test_gpu_driver_10kb_production_batches(built):
                                                   with_stats=True)
     assert batches[-1][1] == 300
     assert np.array_equal(got, want)
-    if oracle.reference_available():
-        ref, rst = oracle.run_reference(rs, P, threads=8, hash_bits=22,
-                                        batching={"hashdatalen": 1_000_000}, with_stats=True)
-        assert np.array_equal(got, ref)
-        for rk, ok in STAT_KEYS:
-            assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
+    oracle.require_reference()
+    ref, rst = oracle.run_reference(rs, P, threads=8, hash_bits=22,
+                                    batching={"hashdatalen": 1_000_000}, with_stats=True)
+    assert np.array_equal(got, ref)
+    for rk, ok in STAT_KEYS:
+        assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
 
 
 @pytest.mark.gpu
@@ -235,8 +235,7 @@ def test_gpu_driver_library_filters(built):
         st = oic.stats()
     finally:
         oic.close()
-    if not oracle.reference_available():
-        pytest.skip("oracle/_ref/oic_ref not built")
+    oracle.require_reference()
     ref, rst = oracle.run_reference(rs, P, threads=threads, hash_bits=22, batching=batch,
                                     libs=libs, extra=extra, with_stats=True)
     assert got.shape == ref.shape and np.array_equal(got, ref)
@@ -268,3 +267,47 @@ def test_gpu_bloom_filter_is_exact(built, monkeypatch, mode):
     assert got.shape == want.shape and np.array_equal(got, want)
     for _, ok in STAT_KEYS:
         assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
+
+
+def _end_skip_kmers(rs, k=22, step=23, span=110):
+    """Skip k-mers taken near both ends of every third read: Mark_Skip_Kmers then marks
+    those reads' ends screened (Build_Hash_Index.C:147-156), which the hopeless check of
+    Process_Matches reads for the TARGET of a single-match pair
+    (Process_String_Overlaps.C:445, :455)."""
+    out = set()
+    for r in range(0, rs.nreads, 3):
+        seq = rs.read(r).decode().upper()
+        for i in list(range(0, span, step)) + list(range(len(seq) - span, len(seq) - k, step)):
+            s = seq[i:i + k]
+            if len(s) == k and set(s) <= set("ACGT"):
+                out.add(s)
+    return sorted(out)
+
+
+@pytest.mark.gpu
+def test_gpu_driver_screened_ends_across_batches(built):
+    """Pairs found in one hash batch are extended after later batches have been built (the
+    extension accumulator).  The target's screened-end bits must be those of the batch
+    that found the pair, as in the reference, where every batch is extended before the
+    next is built: a multi-batch job with end skip k-mers, maxErate 0.06 (hopeless check
+    on) and noisy reads (many single-match pairs), bit-exact against the reference
+    overlapInCore and its -s counters."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    oracle.require_reference()
+    rs = synth_reads(n_reads=240, read_len=3000, genome_len=60_000, error_rate=0.035, seed=27,
+                     len_jitter=0.3)
+    skip = _end_skip_kmers(rs)
+    P = _params()
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=50, Num_PThreads=4).finalize()
+    oic = OverlapInCore(O, device=0)
+    got = oic.run_driver(rs, skip_kmers=skip)
+    st = oic.stats()
+    oic.close()
+    assert st["hash_batches"] >= 4
+    ref, rst = oracle.run_reference(rs, P, threads=4, hash_bits=22,
+                                    batching={"hashstrings": 50}, skip_kmers=skip,
+                                    with_stats=True)
+    assert got.shape == ref.shape and np.array_equal(got, ref)
+    for rk, ok in STAT_KEYS:
+        assert st[ok] == rst[rk], (rk, st[ok], rst[rk])

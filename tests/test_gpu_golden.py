@@ -96,7 +96,7 @@ def test_gpu_output_files(built, tmp_path):
     where built, else the test decoder) to the reference's records, the .counts file is
     byte-identical to the one the reference wrote, the stats text has the reference's lines."""
     import os
-    from test_ovb import GOLDEN, read_ovb_py
+    from test_ovb import GOLDEN
     rs, p, skip, want = load_golden("basic")
     oic = OverlapInCore(_P(p), device=0)
     oic.run(rs)
@@ -105,7 +105,8 @@ def test_gpu_output_files(built, tmp_path):
     oic.write_stats(str(tmp_path / "001.stats"))
     st = oic.stats()
     oic.close()
-    got = oracle.read_ovb_reference(path) if oracle.reference_available() else read_ovb_py(path)
+    oracle.require_reference()
+    got = oracle.read_ovb_reference(path)
     assert np.array_equal(got, want)
     assert open(str(tmp_path / "001.counts"), "rb").read() == \
         open(os.path.join(GOLDEN, "basic_ref.counts"), "rb").read()

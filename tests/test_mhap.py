@@ -284,8 +284,8 @@ def test_gpu_shards_and_text(built, small, small_oracle, tmp_path):
     _same(whole, small_oracle)
     want = "".join(mhap.format_line(r, 1, small.nreads, 1) + "\n" for r in small_oracle)
     assert open(path).read() == want
-    if oracle.mhap_convert_available():
-        assert len(oracle.mhap_convert(small, path)) == len(small_oracle)
+    oracle.require_reference(mhap_convert=True)
+    assert len(oracle.mhap_convert(small, path)) == len(small_oracle)
 
 
 @pytest.mark.gpu

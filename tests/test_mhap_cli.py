@@ -132,11 +132,11 @@ def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
     assert len(self_want) > 5 and len(cross_want) > 5
     _same(got[:len(self_want)], self_want)
     _same(got[len(self_want):], cross_want)
-    if oracle.mhap_convert_available():
-        out = tmp_path / "000001.mhap"
-        out.write_text(cp.stdout)
-        # canu's conversion arguments for an "(and self)" job: -h <block bgn> 0 -q <block bgn>
-        assert len(oracle.mhap_convert(rs, str(out), 1, 0, 1)) == len(got)
+    oracle.require_reference(mhap_convert=True)
+    out = tmp_path / "000001.mhap"
+    out.write_text(cp.stdout)
+    # canu's conversion arguments for an "(and self)" job: -h <block bgn> 0 -q <block bgn>
+    assert len(oracle.mhap_convert(rs, str(out), 1, 0, 1)) == len(got)
 
     # job 2: block 2 against block 3 only (--no-self); IDs are 1..30 (hash), 31..60 (query)
     cp = _run(cli, [*OPTS, "-s", "./blocks/000002.dat", "--no-self", "-q",
