@@ -177,7 +177,7 @@ def require_reference(mhap_convert: bool = False) -> None:
     """The -m gpu parity tests compare with the reference itself (oic_ref, and mhapConvert
     for the MHAP output format).  Both are built in the build container and travel to the
     GPU box with the tree, so their absence there is a broken setup: fail, never skip."""
-    missing = [p for p in [REF_BIN] + ([MHAPCONVERT_BIN] if mhap_convert else [])
+    missing = [p for p in [REF_BIN, OVS_BIN] + ([MHAPCONVERT_BIN] if mhap_convert else [])
                if not os.path.exists(p)]
     if missing:
         raise AssertionError(f"reference checker(s) not built: {missing} "
@@ -210,6 +210,37 @@ def build_gkpstore(rs, workdir: str) -> str:
     if cp.returncode != 0:
         raise RuntimeError(f"oic_ref --gkp-only failed: {cp.stderr[-2000:]}")
     return os.path.join(workdir, "w", "ref.gkpStore")
+
+
+OVS_BIN = os.path.join(HERE, "_ref", "ovs_ref")
+
+
+def store_available() -> bool:
+    return os.path.exists(OVS_BIN)
+
+
+def build_store(gkp: str, store: str, ovbs) -> int:
+    """The REFERENCE ovStore build (oracle/store_harness.cpp over the reference's
+    ovStoreFilter / ovStoreWriter, ovStoreBuild.C:473-655) of the given .ovb files into a
+    new store directory; returns the number of overlaps stored (forward + reverse copies)."""
+    if not store_available():
+        raise FileNotFoundError(OVS_BIN)
+    cp = subprocess.run([OVS_BIN, "--build", gkp, store, *ovbs], capture_output=True, text=True)
+    if cp.returncode != 0:
+        raise RuntimeError(f"ovs_ref --build failed: {cp.stderr[-2000:]}")
+    return int(cp.stdout.split("STORED")[1].split()[0])
+
+
+def dump_store(gkp: str, store: str) -> np.ndarray:
+    """Every overlap of a store, in store order, read by the reference's ovStore reader."""
+    if not store_available():
+        raise FileNotFoundError(OVS_BIN)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as wd:
+        out = os.path.join(wd, "store.bin")
+        cp = subprocess.run([OVS_BIN, "--dump", gkp, store, out], capture_output=True, text=True)
+        if cp.returncode != 0:
+            raise RuntimeError(f"ovs_ref --dump failed: {cp.stderr[-2000:]}")
+        return np.fromfile(out, dtype=RECORD_DTYPE)
 
 
 MHAPCONVERT_BIN = os.path.join(HERE, "_ref", "mhapConvert")
