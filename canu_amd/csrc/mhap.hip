@@ -308,7 +308,7 @@ struct WSketchArgs {
   int32_t k, H;
   const FreqSlot *ftab;         // -f k-mers and their multipliers m(c), or null
   uint64_t fmask;               // table slots - 1
-  double dmult;                 // m(c) of every other k-mer
+  double dmult;                 // m(c) of every other k-mer (< 0: it never enters a sketch)
   int32_t no_tf;
   int32_t *minhash;             // [read][H]
 };
@@ -370,13 +370,15 @@ __global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
               if (fs.code == FEMPTY) break;
             }
           }
-          const double tf = A.no_tf ? 1.0 : (double)(e - p);
-          const double wf = floor(tf * m + 0.5);
-          W[i] = wf < 1.0 ? 1 : (int32_t)wf;
-          const uint64_t x = splitmix64(c);
-          XL[i] = (uint32_t)x;
-          XH[i] = (uint32_t)(x >> 32);
-          vm |= 1u << i;
+          if (m >= 0.0) {                       // m < 0: removed (--supress-noise 1)
+            const double tf = A.no_tf ? 1.0 : (double)(e - p);
+            const double wf = floor(tf * m + 0.5);
+            W[i] = wf < 1.0 ? 1 : (int32_t)wf;
+            const uint64_t x = splitmix64(c);
+            XL[i] = (uint32_t)x;
+            XH[i] = (uint32_t)(x >> 32);
+            vm |= 1u << i;
+          }
         }
       }
     }
@@ -1086,6 +1088,7 @@ void mhap_weighting_init(mhap_weighting *w) {
   w->repeat_idf_scale = 10.0;
   w->filter_threshold = 1e-5;
   w->no_tf = 0;
+  w->supress_noise = 0;
 }
 
 static bool kmer_code(const char *km, uint32_t k, uint64_t *canon) {
@@ -1110,6 +1113,13 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   const uint32_t k = c->P.k;
   if (w->repeat_weight >= 0.0 && 2 * k > 56)
     return mfail(M_BAD_PARAM, "weighted sketches need k <= 28 (read index beside the code)");
+  if (w->supress_noise < 0 || w->supress_noise > 2)
+    return mfail(M_BAD_PARAM, "--supress-noise %d (0, 1 or 2)", w->supress_noise);
+  if (w->supress_noise && w->repeat_weight < 0.0)
+    return mfail(M_BAD_PARAM, "--supress-noise needs the weighted sketch (--repeat-weight >= 0)");
+  // --supress-noise: every -f k-mer is in the table (those below the threshold at the top
+  // multiplier), so that a k-mer NOT in the file can be told apart
+  const bool noise = w->supress_noise != 0 && n != 0;
   c->W = *w;
   c->weighted = w->repeat_weight >= 0.0;
   // the -f k-mers at or above the threshold, canonical (both strands are listed), the
@@ -1118,7 +1128,7 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   for (uint64_t i = 0; i < n; i++) {
     uint64_t cc;
     if (!kmer_code(kmers + i * k, k, &cc)) continue;
-    if (!(fractions[i] >= w->filter_threshold)) continue;
+    if (!(fractions[i] >= w->filter_threshold) && !noise) continue;
     F.emplace_back(cc, fractions[i]);
   }
   std::sort(F.begin(), F.end());
@@ -1148,7 +1158,8 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   double idf_min = idf_max;
   std::vector<double> idf(codes.size());
   for (size_t i = 0; i < codes.size(); i++) {
-    idf[i] = log(1.0 / fr[i]);
+    // below the threshold (only listed with --supress-noise): the top idf
+    idf[i] = fr[i] >= w->filter_threshold ? log(1.0 / fr[i]) : idf_max;
     idf_min = std::min(idf_min, idf[i]);
   }
   auto mult = [&](double v) {
@@ -1158,7 +1169,9 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   };
   std::vector<double> m(codes.size());
   for (size_t i = 0; i < codes.size(); i++) m[i] = mult(idf[i]);
-  c->dmult = mult(idf_max);
+  // a k-mer not in the table: the top multiplier; with --supress-noise 2 the most frequent
+  // k-mer's (suppressed like a repeat), with 1 none (-1: it never enters a sketch)
+  c->dmult = !noise ? mult(idf_max) : w->supress_noise == 2 ? mult(idf_min) : -1.0;
   // open addressing at load <= 1/2
   uint64_t slots = 16;
   while (slots < 2 * codes.size() + 1) slots <<= 1;

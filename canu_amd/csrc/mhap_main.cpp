@@ -21,7 +21,8 @@
 // 2.x algorithm in include/canu_mhap.h (mhap_weighting); parity with the jar itself is
 // unpinned.  Without --repeat-weight (or with a negative one) the sketch is
 // MHAP 1.x's unweighted one and -f k-mers at or above --filter-threshold are left out.
-// --supress-noise is rejected.
+// --supress-noise (canu: with mhapFilterUnique) is restated from the jar's option text in
+// include/canu_mhap.h (mhap_weighting.supress_noise); unpinned like the rest.
 #include <zlib.h>
 
 #include <algorithm>
@@ -59,6 +60,7 @@ int usage(const char *prog) {
           "  --ordered-sketch-size n  --ordered-kmer-size n  --min-olap-length n\n"
           "  --num-threads n (ignored: one GPU)   CANU_MHAP_DEVICE picks the GPU\n"
           "  --repeat-weight x  --repeat-idf-scale x  --filter-threshold x  --no-tf\n"
+          "  --supress-noise 0|1|2\n"
           "                                      (tf-idf repeat weighting, canu_mhap.h)\n",
           prog, prog);
   return 1;
@@ -220,10 +222,8 @@ int main(int argc, char **argv) {
     else if (a == "--repeat-weight") W.repeat_weight = atof(num("--repeat-weight"));
     else if (a == "--repeat-idf-scale") W.repeat_idf_scale = atof(num("--repeat-idf-scale"));
     else if (a == "--no-tf") W.no_tf = 1;
-    else if (a == "--supress-noise") {
-      fprintf(stderr, "mhap: %s: the jar's noise suppression is not implemented\n", a.c_str());
-      return 1;
-    } else if (a == "--no-self") no_self = true;
+    else if (a == "--supress-noise") W.supress_noise = atoi(num("--supress-noise"));
+    else if (a == "--no-self") no_self = true;
     else if (a == "-f") fpath = num("-f");
     else if (a == "-p") fasta = num("-p");
     else if (a == "-q") qpath = num("-q");

@@ -26,7 +26,7 @@ EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last
            "mhap_copy_sketches_host", "mhap_weighting_init", "mhap_set_kmer_frequencies",
            "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
 
-ABI_VERSION = 3          # MHAP_ABI_VERSION of include/canu_mhap.h
+ABI_VERSION = 4          # MHAP_ABI_VERSION of include/canu_mhap.h
 
 
 class MhapError(RuntimeError):
@@ -44,7 +44,8 @@ class _Params(ctypes.Structure):
 
 class _Weighting(ctypes.Structure):
     _fields_ = [("repeat_weight", ctypes.c_double), ("repeat_idf_scale", ctypes.c_double),
-                ("filter_threshold", ctypes.c_double), ("no_tf", ctypes.c_int32)]
+                ("filter_threshold", ctypes.c_double), ("no_tf", ctypes.c_int32),
+                ("supress_noise", ctypes.c_int32)]
 
 
 class _Stats(ctypes.Structure):
@@ -110,6 +111,9 @@ class MhapParameters:
     repeat_idf_scale: float = 10.0
     filter_threshold: float = 1e-5
     no_tf: bool = False
+    # --supress-noise (canu passes 2 with mhapFilterUnique, OverlapMhap.pm:383): k-mers not
+    # in the -f file removed (1) or weighted like the most frequent one (2); canu_mhap.h
+    supress_noise: int = 0
 
     @classmethod
     def sensitivity(cls, level: str, tag: str = "cor", nanopore: bool = False,
@@ -141,7 +145,7 @@ class MhapParameters:
 
     def weighting_c(self) -> _Weighting:
         return _Weighting(self.repeat_weight, self.repeat_idf_scale, self.filter_threshold,
-                          1 if self.no_tf else 0)
+                          1 if self.no_tf else 0, int(self.supress_noise))
 
     def canu_weighting(self, filter_threshold: float = 0.000005) -> "MhapParameters":
         """The weighting canu always asks the jar for (OverlapMhap.pm:382, :390;
@@ -155,7 +159,8 @@ class MhapParameters:
                     threshold=self.threshold, ordered_sketch=self.ordered_sketch_size,
                     ordered_k=self.ordered_kmer_size, min_olap=self.min_olap_length,
                     repeat_weight=self.repeat_weight, repeat_idf_scale=self.repeat_idf_scale,
-                    filter_threshold=self.filter_threshold, no_tf=bool(self.no_tf))
+                    filter_threshold=self.filter_threshold, no_tf=bool(self.no_tf),
+                    supress_noise=int(self.supress_noise))
 
 
 def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
@@ -195,8 +200,9 @@ def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
         elif a in ("--no-self",):
             io[a] = True
         elif a == "--supress-noise":
-            raise MhapError(-3, f"{a}: the jar's low-frequency noise suppression is not "
-                                "implemented (canu passes it only with mhapFilterUnique)")
+            p.supress_noise = int(val); i += 1
+            if p.supress_noise not in (0, 1, 2):
+                raise MhapError(-2, f"--supress-noise {val}: 0, 1 or 2")
         else:
             raise MhapError(-2, f"unknown MHAP option '{a}'")
         i += 1

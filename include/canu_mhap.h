@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHAP_ABI_VERSION 3
+#define MHAP_ABI_VERSION 4
 
 typedef struct {
   uint32_t k;               /* -k                      MinHash k-mer size, 1..32        */
@@ -106,15 +106,27 @@ int         mhap_set_filter_kmers(mhap_ctx *ctx, const char *kmers, uint64_t n);
  *   w(c)    max(1, floor(tf(c) * m(c) + 0.5)), m(c) = r + (1 - r) * scaled idf(c), where
  *           r = repeat_weight; r >= 1 or no -f k-mers: m = 1 (tf only)
  * repeat_weight < 0 is MHAP 1.x's unweighted sketch: -f k-mers with a fraction >=
- * filter_threshold are dropped, every other k-mer counts once. */
+ * filter_threshold are dropped, every other k-mer counts once.
+ * supress_noise (--supress-noise, OverlapMhap.pm:383 / :483, passed when
+ * mhapFilterUnique is set; the -f file then lists every k-mer at or above the unique-k-mer
+ * count, Meryl.pm:678-714) -- restated from MHAP 2.x's option text ("1) completely removes
+ * any k-mers not specified in the filter file, 2) supresses k-mers not specified in the
+ * filter file, similar to repeats"), parity unpinned:
+ *   0  as above;
+ *   1  k-mers not in the -f file never enter a sketch (weighted sketches only);
+ *   2  k-mers not in the -f file get the multiplier of the most frequent -f k-mer
+ *      (scaled idf 1, m = 1 for canu's r = 0.9); -f k-mers below filter_threshold keep the
+ *      top multiplier (scaled idf repeat_idf_scale) as before. */
 typedef struct {
   double  repeat_weight;      /* --repeat-weight     (canu: 0.9; < 0 unweighted)         */
   double  repeat_idf_scale;   /* --repeat-idf-scale  (canu: 10)                          */
   double  filter_threshold;   /* --filter-threshold  (canu: mhapFilterThreshold 5e-6)    */
   int32_t no_tf;              /* --no-tf                                                 */
+  int32_t supress_noise;      /* --supress-noise 0 / 1 / 2 (ABI 4)                       */
 } mhap_weighting;
 
-/* Unweighted defaults: repeat_weight -1, repeat_idf_scale 10, filter_threshold 1e-5, tf on. */
+/* Unweighted defaults: repeat_weight -1, repeat_idf_scale 10, filter_threshold 1e-5, tf on,
+ * supress_noise 0. */
 void        mhap_weighting_init(mhap_weighting *w);
 
 /* -f with its second column: n k-mers (n * k bytes) and the fraction of all k-mers each

@@ -70,7 +70,7 @@ def default_params(**kw) -> dict:
     """canu's 'normal' sensitivity for correction (OverlapMhap.pm:116-121, Defaults.pm)."""
     p = dict(k=16, num_hashes=512, min_matches=3, threshold=0.78, ordered_sketch=1536,
              ordered_k=12, min_olap=500, repeat_weight=-1.0, repeat_idf_scale=10.0,
-             filter_threshold=1e-5, no_tf=False)
+             filter_threshold=1e-5, no_tf=False, supress_noise=0)
     p.update(kw)
     return p
 
@@ -138,22 +138,26 @@ def kmer_multipliers(freq_kmers, fractions, p: dict):
       idf = ln(1 / fraction), idf_max = ln(1 / filter_threshold), idf_min over the table,
     r = repeat_weight, X = repeat_idf_scale (m = 1 when r >= 1 or the table is empty), and
     the multiplier of every other k-mer (idf = idf_max).  Logs and arithmetic in Python
-    floats (C doubles, libm log), in the library's order of operations."""
+    floats (C doubles, libm log), in the library's order of operations.
+    supress_noise (--supress-noise, canu_mhap.h): with a -f table, every listed k-mer is
+    kept (below the threshold: idf = idf_max) and an unlisted k-mer's multiplier is that of
+    the most frequent one (2) or -1, i.e. removed from the sketch (1)."""
     import math
     k, thr = p["k"], p["filter_threshold"]
     r, X = p["repeat_weight"], p["repeat_idf_scale"]
+    noise = int(p.get("supress_noise", 0)) != 0 and len(freq_kmers) > 0
     best = {}
     for km, f in zip(freq_kmers, fractions):
         f = float(f)
         c = _CODE[np.frombuffer(km.encode() if isinstance(km, str) else km, dtype=np.uint8)]
-        if c.shape[0] != k or (c == 255).any() or not (f >= thr):
+        if c.shape[0] != k or (c == 255).any() or (not (f >= thr) and not noise):
             continue
         _, can, _ = kmers(c, k)
         cc = int(can[0])
         best[cc] = max(best.get(cc, f), f)
     codes = sorted(best)
     idf_max = math.log(1.0 / thr)
-    idf = [math.log(1.0 / best[c]) for c in codes]
+    idf = [math.log(1.0 / best[c]) if best[c] >= thr else idf_max for c in codes]
     idf_min = min([idf_max] + idf)
 
     def mult(v):
@@ -162,8 +166,8 @@ def kmer_multipliers(freq_kmers, fractions, p: dict):
         sc = 1.0 + (X - 1.0) * (v - idf_min) / (idf_max - idf_min) if idf_max > idf_min else X
         return r + (1.0 - r) * sc
 
-    return (np.array(codes, dtype=U64), np.array([mult(v) for v in idf], dtype=np.float64),
-            mult(idf_max))
+    dm = mult(idf_max) if not noise else mult(idf_min) if int(p["supress_noise"]) == 2 else -1.0
+    return (np.array(codes, dtype=U64), np.array([mult(v) for v in idf], dtype=np.float64), dm)
 
 
 def sketch_weighted(rs, p: dict, freq=None) -> np.ndarray:
@@ -192,6 +196,10 @@ def sketch_weighted(rs, p: dict, freq=None) -> np.ndarray:
             q = np.searchsorted(fcodes, u)
             hit = (q < fcodes.size) & (fcodes[np.minimum(q, fcodes.size - 1)] == u)
             m[hit] = fmult[q[hit]]
+        keep = m >= 0.0                        # --supress-noise 1: unlisted k-mers removed
+        u, tf, m = u[keep], tf[keep], m[keep]
+        if u.size == 0:
+            continue
         w = np.array([max(1, int(math.floor(float(t) * float(mm) + 0.5)))
                       for t, mm in zip(tf.tolist(), m.tolist())], dtype=np.int64)
         x = splitmix64(u)

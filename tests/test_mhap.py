@@ -48,7 +48,7 @@ def test_header_declares_the_python_exports():
 def test_library_exports_every_declared_symbol(built):
     lib = mhap.load_library()
     assert [f for f in mhap.EXPORTS if not hasattr(lib, f)] == []
-    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 3
+    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 4
 
 
 def test_params_init_is_canu_normal(built):
@@ -88,8 +88,10 @@ def test_parse_canu_command_line():
     assert not p.no_tf
     assert io["-s"] == "./blocks/000001.dat" and io["--num-threads"] == "8"
     assert mhap.parse_mhap_args(["--no-tf"])[0].no_tf
+    assert p.supress_noise == 0
+    assert mhap.parse_mhap_args(["--supress-noise", "2"])[0].supress_noise == 2
     with pytest.raises(mhap.MhapError):
-        mhap.parse_mhap_args(["--supress-noise", "2"])
+        mhap.parse_mhap_args(["--supress-noise", "3"])
     with pytest.raises(mhap.MhapError):
         mhap.parse_mhap_args(["--bogus"])
 
@@ -147,6 +149,41 @@ def test_oracle_weighting_properties():
     # a read whose k-mers are all listed at one fraction gets a sketch unlike the tf one
     full = M.sketch_weighted(rs, _weighted_params(), (km, fr))
     assert not np.array_equal(full, tfo)
+
+
+def _noise_freq(rs, every=3):
+    """An mhapFilterUnique-style -f list (Meryl.pm:678-714: every k-mer at or above the
+    unique-count threshold, with its fraction): some of the reads' k-mers, most of them
+    below --filter-threshold, a few repeats above it."""
+    km, fr = _freq_for(rs, every=every)
+    fr = fr.copy()
+    fr[np.arange(fr.size) % 6 >= 2] = 2e-7        # solid but not repeated: below 5e-6
+    return km, fr
+
+
+def test_oracle_supress_noise():
+    """--supress-noise (canu_mhap.h, restated from the jar's option text; unpinned): every
+    -f k-mer is in the table (those below the threshold at the top multiplier); an unlisted
+    k-mer is weighted like the most frequent one (2) or never enters a sketch (1)."""
+    rs = _reads(n=6, L=3000, cov=10, seed=17)
+    km, fr = _noise_freq(rs)
+    p0 = _weighted_params()
+    c0, m0, d0 = M.kmer_multipliers(km, fr, p0)
+    for mode in (1, 2):
+        c, m, d = M.kmer_multipliers(km, fr, dict(p0, supress_noise=mode))
+        assert c.size > c0.size                   # the below-threshold k-mers are listed
+        assert abs(m.max() - d0) < 1e-12          # ... at the top multiplier
+        assert (abs(d - m.min()) < 1e-12) if mode == 2 else d == -1.0
+    s0 = M.sketch_weighted(rs, p0, (km, fr))
+    s1 = M.sketch_weighted(rs, dict(p0, supress_noise=1), (km, fr))
+    s2 = M.sketch_weighted(rs, dict(p0, supress_noise=2), (km, fr))
+    assert not np.array_equal(s0, s2) and not np.array_equal(s1, s2)
+    # mode 1 keeps only listed k-mers: every read's sketch values are >= mode 0's
+    assert (s1 >= s0).all() and (s1 != s0).any()
+    # nothing listed: with mode 1 no k-mer is left (empty sketches)
+    none = ([km[0]], np.array([fr[0]]))
+    c, m, d = M.kmer_multipliers(none[0], none[1], dict(p0, supress_noise=1))
+    assert c.size == 1 and d == -1.0
 
 
 def test_oracle_kmer_codes():
@@ -317,7 +354,8 @@ def test_gpu_sketch_rows_match_oracle(built, small):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "repeat_read", "k20"])
+@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "repeat_read", "k20", "noise1",
+                                     "noise2"])
 def test_gpu_weighted_sketch_rows_match_oracle(built, variant):
     """The weighted MinHash rows in HBM (distinct k-mers by a radix sort, tf as run lengths,
     the -f multipliers) equal the restatement's, bit for bit."""
@@ -336,6 +374,9 @@ def test_gpu_weighted_sketch_rows_match_oracle(built, variant):
     if variant == "k20":                 # 64-bit (read, code) keys: one sort per batch
         P.k = 20
         freq = ([x + "ACGT" for x in freq[0]], freq[1])
+    if variant in ("noise1", "noise2"):  # --supress-noise with an mhapFilterUnique -f list
+        P.supress_noise = int(variant[-1])
+        freq = _noise_freq(rs)
     m = mhap.Mhap(P, device=0)
     m.load_reads(rs)
     m.set_kmer_frequencies(*freq)

@@ -41,7 +41,7 @@ def _run(cli, args, cwd=None):
 def test_cli_usage_errors(cli):
     for args in ([], ["-p", "x.fasta"], ["-p", "x.fasta", "-s", "y.dat", "-q", "."],
                  ["--bogus"], ["-k"], ["--no-tf", "-s", "missing.dat"],
-                 ["--supress-noise", "2", "-s", "y.dat"]):
+                 ["--supress-noise", "5", "-s", "y.dat"]):
         cp = _run(cli, args)
         assert cp.returncode == 1, (args, cp.stderr)
 
@@ -85,8 +85,12 @@ def _same(got, want):
 
 
 @pytest.mark.gpu
-def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
+@pytest.mark.parametrize("noise", [0, 2])
+def test_gpu_cli_precompute_and_jobs(cli, tmp_path, noise):
+    """noise = 2: canu's mhapFilterUnique command line (--supress-noise 2, OverlapMhap.pm:383
+    / :483) with an -f list that also holds k-mers below --filter-threshold (Meryl.pm:678)."""
     import gzip
+    extra = CANU_EXTRA + (["--supress-noise", str(noise)] if noise else [])
     rs = _reads()
     blocks = [_block(rs, i, i + BLOCK) for i in range(0, N, BLOCK)]
     bdir = tmp_path / "blocks"
@@ -99,7 +103,7 @@ def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
     for j, i0 in enumerate(range(0, 3000, 9)):
         m = r0[i0:i0 + 16]
         km += [m, m.translate(comp)[::-1]]
-        fr += [5e-6 * 1.4 ** (j % 15)] * 2
+        fr += [5e-6 * 1.4 ** (j % 15) * (0.05 if noise and j % 3 == 0 else 1.0)] * 2
     fpath = tmp_path / "asm.ms16.frequentMers.ignore.gz"
     with gzip.open(fpath, "wt") as f:
         f.write(f"{len(km)}\n")
@@ -111,12 +115,13 @@ def test_gpu_cli_precompute_and_jobs(cli, tmp_path):
         with open(fa, "w") as f:
             for r in range(b.nreads):
                 f.write(f">{BLOCK * (i - 1) + r + 1}\n{b.read(r).decode()}\n")
-        cp = _run(cli, [*OPTS, *CANU_EXTRA, "-f", str(fpath), "-p", f"./{fa.name}", "-q", "."],
+        cp = _run(cli, [*OPTS, *extra, "-f", str(fpath), "-p", f"./{fa.name}", "-q", "."],
                   cwd=bdir)
         assert cp.returncode == 0, cp.stderr
         os.replace(bdir / f"{i:06d}.input.dat", bdir / f"{i:06d}.dat")
     # the sketches are canu's weighted ones (restated tf-idf, canu_mhap.h)
     P = mhap.MhapParameters().canu_weighting(0.000005).as_oracle()
+    P["supress_noise"] = noise
     freq = (km, np.array(fr_read))
 
     # job 1: block 1 against itself and blocks 2-3 (OverlapMhap.pm's "(and self)" case)
