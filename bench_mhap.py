@@ -213,6 +213,12 @@ def main() -> None:
             "gbp_vs_gbp_per_sec": round(gbp * gbp / 2.0 * args.steps / elapsed, 3),
             "breakdown_ms": {k: round(v / args.steps, 2) for k, v in ms.items()},
             "setup_s": round(setup_s, 1), "roofline": roof, "cpu_baseline": cpu,
+            "parity": {"checked": False, "pinned": False,
+                       "reason": "parity with the MHAP jar is unpinned (the reference ships "
+                                 "only the prebuilt jar, no fixtures; no JVM here): the GPU is "
+                                 "bit-exact to the restatement oracle/mhap_oracle.py "
+                                 "(tests/test_mhap.py), whose weighted sketch is restated from "
+                                 "the published MHAP 2.x algorithm (DESIGN.md)"},
         }
         print(json.dumps(line), flush=True)
     m.close()

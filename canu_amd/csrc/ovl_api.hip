@@ -289,6 +289,53 @@ void ovl_params_finalize(ovl_params *p) {
 
 void *ovl_ctx_stream(ovl_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+// ovl_probe_ceiling: Q independent random 16-B loads in flight per lane over the table's
+// 2^tab_bits slots (masked index, an LCG per lane: nothing in the loop but the loads)
+template <int Q>
+__global__ void __launch_bounds__(256) k_rand_lookup(const uint4 *t, uint64_t mask,
+                                                     uint32_t iters, uint32_t *sink) {
+  uint32_t acc = 0;
+  uint64_t x = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x + 1) * 0x9E3779B97F4A7C15ull;
+  for (uint32_t i = 0; i < iters; i++) {
+    uint4 v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      v[q] = t[(x >> 17) & mask];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++) acc ^= v[q].x ^ v[q].w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;       // keeps the loads live; (almost) never taken
+}
+
+int ovl_probe_ceiling(ovl_ctx *c, double *gloads_per_s, uint64_t *table_bytes) {
+  if (!c || !gloads_per_s || !table_bytes) return fail(OVL_ERR_STATE, "null argument");
+  if (!c->have_index || !c->d_tab.p) return fail(OVL_ERR_STATE, "no index table");
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const uint64_t slots = 1ull << c->tab_bits;
+  DBuf<uint32_t> sink;
+  if (sink.alloc(1)) return fail(OVL_ERR_OOM, "sink");
+  const uint32_t blocks = 8u * (uint32_t)c->n_cu, iters = 64;
+  hipLaunchKernelGGL(k_rand_lookup<8>, dim3(blocks), dim3(256), 0, s,
+                     (const uint4 *)c->d_tab.p, slots - 1, iters, sink.p);   // warm
+  HIPC(hipEventRecord(c->ev[6], s));
+  const int reps = 3;
+  for (int r = 0; r < reps; r++)
+    hipLaunchKernelGGL(k_rand_lookup<8>, dim3(blocks), dim3(256), 0, s,
+                       (const uint4 *)c->d_tab.p, slots - 1, iters, sink.p);
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(c->ev[7], s));
+  HIPC(hipEventSynchronize(c->ev[7]));
+  float ms = 0;
+  HIPC(hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
+  const double loads = (double)reps * blocks * 256.0 * iters * 8.0;
+  *gloads_per_s = ms > 0 ? loads / (ms * 1e-3) / 1e9 : 0.0;
+  *table_bytes = slots * sizeof(TabEntry);
+  return OVL_OK;
+}
+
 int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
   *out = nullptr;
   if (p->kmer_len == 0) return fail(OVL_ERR_BAD_PARAM, "kmer length (-k) needed");
@@ -2106,9 +2153,18 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
     HA.out = nullptr;
     hipLaunchKernelGGL(k_hitlist, dim3((nb + 3) / 4), dim3(256), 0, s, HA);
     HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev[3], s));
     std::vector<uint64_t> cnt(nb);
     HIPC(hipMemcpyAsync(cnt.data(), ucnt.p, 8ull * nb, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+    // ms_seed_hits is device time of the kernels alone: the probe + count pass here, each
+    // write pass below; the host's piece cuts, buffer growth, uploads, the hit copies to
+    // the host and the syncs between pieces are outside every event pair
+    {
+      float t = 0;
+      (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+      ms_tot += t;
+    }
     // write pass, in pieces of whole units that fit the hit buffer: every unit's base
     // within its piece is computed once (one host pass over the batch) and uploaded once;
     // the hit buffer only grows (one allocation at the largest piece)
@@ -2134,21 +2190,21 @@ int ovl_seed_hits(ovl_ctx *c, uint32_t bgn, uint32_t end, ovl_seed_hit *out, uin
       HA.rbase = fb.rbase.p + p0;
       HA.unit_base = ubase.p + p0;
       HA.nunits = p1 - p0;
+      HIPC(hipEventRecord(c->ev[4], s));
       hipLaunchKernelGGL(k_hitlist, dim3((p1 - p0 + 3) / 4), dim3(256), 0, s, HA);
       HIPC(hipGetLastError());
+      HIPC(hipEventRecord(c->ev[5], s));
       if (out && copied < max_hits && a2) {
         uint64_t n = std::min<uint64_t>(a2, max_hits - copied);
         HIPC(hipMemcpyAsync(out + copied, hbuf.p, 16ull * n, hipMemcpyDeviceToHost, s));
         copied += n;
       }
       HIPC(hipStreamSynchronize(s));
+      float t = 0;
+      (void)hipEventElapsedTime(&t, c->ev[4], c->ev[5]);
+      ms_tot += t;
       total += a2;
     }
-    HIPC(hipEventRecord(c->ev[3], s));
-    HIPC(hipStreamSynchronize(s));
-    float t = 0;
-    (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
-    ms_tot += t;
     u0 = u1;
   }
   c->stats.ms_seed_hits = ms_tot;

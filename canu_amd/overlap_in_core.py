@@ -86,12 +86,12 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
            "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream", "ovl_write_ovb",
            "ovl_ctx_write_ovb", "ovl_ctx_write_stats", "ovl_set_read_libraries",
            "ovl_hash_limits_init", "ovl_build_hash_batch", "ovl_driver_params_init",
-           "ovl_overlap_driver", "ovl_seed_hits"]
+           "ovl_overlap_driver", "ovl_seed_hits", "ovl_probe_ceiling"]
 
 _lib = None
 
 
-ABI_VERSION = 3          # OVL_ABI_VERSION of include/canu_ovl.h
+ABI_VERSION = 4          # OVL_ABI_VERSION of include/canu_ovl.h
 
 
 def load_library(path: str | None = None):
@@ -126,6 +126,7 @@ def load_library(path: str | None = None):
     lib.ovl_fetch_overlaps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                        P(ctypes.c_uint64)]
     lib.ovl_get_stats.argtypes = [ctypes.c_void_p, P(_Stats)]
+    lib.ovl_probe_ceiling.argtypes = [ctypes.c_void_p, P(ctypes.c_double), P(ctypes.c_uint64)]
     lib.ovl_ctx_stream.argtypes = [ctypes.c_void_p]
     lib.ovl_ctx_stream.restype = ctypes.c_void_p
     lib.ovl_write_ovb.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
@@ -381,6 +382,13 @@ class OverlapInCore:
 
     def stream(self) -> int:
         return self.lib.ovl_ctx_stream(self.ctx)
+
+    def probe_ceiling(self) -> tuple[float, int]:
+        """(G random 16-B loads/s over the current index table's allocation, its bytes):
+        the ceiling of one random lookup per query window here (ovl_probe_ceiling)."""
+        g, b = ctypes.c_double(), ctypes.c_uint64()
+        self._check(self.lib.ovl_probe_ceiling(self.ctx, ctypes.byref(g), ctypes.byref(b)))
+        return g.value, b.value
 
     def write_ovb(self, path: str) -> None:
         """overlapInCore's -o output: the last find's records as an .ovb + .counts."""

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 3
+#define OVL_ABI_VERSION 4
 
 typedef enum {
   OVL_OK               =  0,
@@ -257,6 +257,13 @@ int         ovl_ctx_write_stats(ovl_ctx *ctx, const char *path);
 /* HIP stream the context runs on (as void*, a hipStream_t), for callers that time or
  * order work around it. */
 void       *ovl_ctx_stream(ovl_ctx *ctx);
+
+/* Measurement only (bench.py's probe roofline; no reference counterpart, ABI 4): the rate
+ * of independent random 16-B loads over the CURRENT index table's own allocation
+ * (2^tab_bits slots, the table the hash probe looks each query window up in), in G loads/s,
+ * and the table's bytes -- the memory system's ceiling for one random lookup per window on
+ * this device at this table size.  Reads the table only; needs an index. */
+int         ovl_probe_ceiling(ovl_ctx *ctx, double *gloads_per_s, uint64_t *table_bytes);
 
 #ifdef __cplusplus
 }

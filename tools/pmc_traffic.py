@@ -3,7 +3,8 @@
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
   profiles/<tag>_traffic.csv        per kernel: launches, avg ns, HBM bytes per launch
   profiles/traffic.json             {kernel: {hbm_bytes_per_step, launches_per_step}} for
-                                    bench.py (the profiled run is one step, no warmup)
+                                    bench.py (the profiled run is one step, no warmup);
+                                    profiles/traffic_configs4.json for --workload configs4-rank
 HBM bytes = (r * FETCH_SIZE + WRITE_SIZE) * 1024 (counters in KiB).  r is the read
 correction of the kernel's dominant read pattern, measured on known byte counts by
 tools/calib_traffic.hip (profiles/calib_traffic.json): coalesced streaming reads are
@@ -125,13 +126,14 @@ def main():
     sys.path.insert(0, ROOT)
     import bench
     bargs = bench.parse_args(sys.argv[2:])
-    traffic["_method"] = {"workload": bench.Configs2(bargs, 0, 1, None, None).workload_key(),
+    jcls = bench.Configs4Rank if bargs.workload == "configs4-rank" else bench.Configs2
+    traffic["_method"] = {"workload": jcls(bargs, 0, 1, None, None).workload_key(),
                           "src_sha": bench.source_hash(),
                           "hbm_bytes": "(r * FETCH_SIZE + WRITE_SIZE) KiB",
                           "read_correction": {"default": 2.0, **READ_CORR},
                           "calibration": "profiles/calib_traffic.json (tools/calib_traffic.hip)",
                           "tag": tag}
-    with open(os.path.join(PROF, "traffic.json"), "w") as f:
+    with open(os.path.join(PROF, bench.TRAFFIC_FILES[bargs.workload]), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
     print(json.dumps(traffic, indent=1))
 

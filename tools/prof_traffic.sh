@@ -7,7 +7,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}; shift
-ARGS=${@:---steps 1 --warmup 0 --no-cpu-baseline --no-shard-timing --no-seed-only}
+ARGS=${@:---steps 1 --warmup 0 --no-cpu-baseline --no-shard-timing --no-seed-only --no-side}
 export TMPDIR=/tmp
 mkdir -p $R/gpurun_out
 cd /tmp
