@@ -262,6 +262,26 @@ struct ovl_ctx {
   }
 };
 
+// ovl_probe_ceiling: Q independent random 16-B loads in flight per lane over the table's
+// 2^tab_bits slots (masked index, an LCG per lane: nothing in the loop but the loads)
+template <int Q>
+__global__ void __launch_bounds__(256) k_rand_lookup(const uint4 *t, uint64_t mask,
+                                                     uint32_t iters, uint32_t *sink) {
+  uint32_t acc = 0;
+  uint64_t x = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x + 1) * 0x9E3779B97F4A7C15ull;
+  for (uint32_t i = 0; i < iters; i++) {
+    uint4 v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      v[q] = t[(x >> 17) & mask];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++) acc ^= v[q].x ^ v[q].w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;       // keeps the loads live; (almost) never taken
+}
+
 extern "C" {
 
 int ovl_abi_version(void) { return OVL_ABI_VERSION; }
@@ -288,26 +308,6 @@ void ovl_params_finalize(ovl_params *p) {
 }
 
 void *ovl_ctx_stream(ovl_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
-
-// ovl_probe_ceiling: Q independent random 16-B loads in flight per lane over the table's
-// 2^tab_bits slots (masked index, an LCG per lane: nothing in the loop but the loads)
-template <int Q>
-__global__ void __launch_bounds__(256) k_rand_lookup(const uint4 *t, uint64_t mask,
-                                                     uint32_t iters, uint32_t *sink) {
-  uint32_t acc = 0;
-  uint64_t x = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x + 1) * 0x9E3779B97F4A7C15ull;
-  for (uint32_t i = 0; i < iters; i++) {
-    uint4 v[Q];
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-      x = x * 6364136223846793005ull + 1442695040888963407ull;
-      v[q] = t[(x >> 17) & mask];
-    }
-#pragma unroll
-    for (int q = 0; q < Q; q++) acc ^= v[q].x ^ v[q].w;
-  }
-  if (acc == 0x9E3779B9u) sink[0] = acc;       // keeps the loads live; (almost) never taken
-}
 
 int ovl_probe_ceiling(ovl_ctx *c, double *gloads_per_s, uint64_t *table_bytes) {
   if (!c || !gloads_per_s || !table_bytes) return fail(OVL_ERR_STATE, "null argument");
