@@ -216,6 +216,9 @@ struct ovl_ctx {
     DBuf<uint64_t> hcnt, hbase;              // ovl_seed_hits: per-unit hit counts / bases
     DBuf<uint4> hbuf;                        // ovl_seed_hits: one piece of the hit list
     DBuf<uint32_t> oa, ob, ucnt, useg;
+    DBuf<uint64_t> shk[2];                   // shared-strand order: keys, sorted keys
+    DBuf<uint32_t> shi[2], shw, seg, nseg;   // pair indices (sorted), unit work, groups
+    DBuf<uint8_t> shf, shtmp;                // group-start flags, hipcub scratch
     DBuf<Node> pool, pnodes[2];
     DBuf<PairRec> pairs[2];
     DBuf<unsigned long long> stats;
@@ -462,6 +465,36 @@ static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const ui
 
 // Work-order keys for the extension queue: a pair's match-node count (its extension work
 // grows with it), so the longest pairs start first and the kernel's tail is short.
+// The shared-strand kernel's work order (k_extend<.., SH>): pairs grouped by unit, units by
+// descending work (their pairs' node counts summed), a unit's pairs by descending node count
+// -- one 64-bit key: [~work 20 | unit 28 | ~nodes 16] sorted ascending (work clamped: ties
+// only reorder units).
+__global__ void k_sh_unit_work(const PairRec *pairs, uint32_t n, uint32_t *uwork) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    atomicAdd(&uwork[pairs[i].unit], pairs[i].node_cnt);
+}
+
+__global__ void k_sh_keys(const PairRec *pairs, uint32_t n, const uint32_t *uwork,
+                          uint64_t *keys, uint32_t *idx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const PairRec P = pairs[i];
+    const uint64_t w = std::min<uint32_t>(uwork[P.unit], 0xFFFFFu);
+    const uint64_t nc = std::min<uint32_t>(P.node_cnt, 0xFFFFu);
+    keys[i] = ((0xFFFFFull - w) << 44) | ((uint64_t)P.unit << 16) | (0xFFFFull - nc);
+    idx[i] = i;
+  }
+}
+
+// first position of every unit group in the sorted keys (bits 16.. differ from the previous)
+__global__ void k_sh_flags(const uint64_t *keys, uint32_t n, uint8_t *flags) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    flags[i] = (i == 0 || (keys[i] >> 16) != (keys[i - 1] >> 16)) ? 1 : 0;
+}
+
+__global__ void k_sh_seg_end(uint32_t *seg, const uint32_t *nseg, uint32_t n) {
+  seg[*nseg] = n;
+}
+
 __global__ void k_pair_order_keys(const PairRec *pairs, uint32_t n, uint32_t *keys,
                                   uint32_t *idx) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -997,6 +1030,8 @@ static void release_find_buffers(ovl_ctx *c) {
   f.ok64a.release(); f.ok64b.release(); f.dkey.release(); f.oa.release(); f.ob.release();
   f.ucnt.release(); f.useg.release(); f.hcnt.release(); f.hbase.release(); f.hbuf.release();
   f.rows.release(); f.rowdir.release(); f.deltas.release();
+  for (int i = 0; i < 2; i++) { f.shk[i].release(); f.shi[i].release(); }
+  f.shw.release(); f.seg.release(); f.nseg.release(); f.shf.release(); f.shtmp.release();
   // the extension accumulator's buffers, once nothing waits in them
   if (c->acc.np == 0) {
     c->acc.units.release(); c->acc.pnodes.release(); c->acc.pairs.release();
@@ -1317,6 +1352,12 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   auto fits = [&](uint64_t L, uint32_t wpb, size_t cap) {
     return stg_lds_of(L) * wpb + ml_of(ecap_of(L)) <= cap;
   };
+  // the shared-strand block: Edit_Match_Limit table, slot control, OVL_SH_SLOTS query
+  // strands, then per wave its target strand and scratch (k_extend<.., SH>)
+  auto sh_lds_of = [&](uint64_t L, uint32_t wpb) -> size_t {
+    return ml_of(ecap_of(L)) + OVL_SH_SLOTS * sizeof(ShSlot) + 16 +
+           8ull * OVL_SH_SLOTS * (uint64_t)sw_of(L) + wpb * (8ull * (uint64_t)sw_of(L) + 4ull * OVL_SCR);
+  };
   auto longest_fitting = [&](uint32_t wpb, size_t cap) -> uint32_t {
     uint64_t lo = 0, hi = c->max_len;
     if (fits(hi, wpb, cap)) return (uint32_t)hi;
@@ -1333,9 +1374,12 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     bool l16 = false;
     uint64_t stride = 0;
     bool wide = false;             // the 2 x OVL_RJ-chunk register window (wide bands)
+    bool sh = false;               // the block-shared query strand (first class only)
   };
   // the staged kernel instance of a class
-  auto stage_kernel = [](bool l16, bool wide) -> const void * {
+  auto stage_kernel = [](bool l16, bool wide, bool sh = false) -> const void * {
+    if (sh) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, OVL_RJ, true>)
+                       : reinterpret_cast<const void *>(k_extend<true, false, false, OVL_RJ, true>);
     if (wide) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, 2 * OVL_RJ>)
                          : reinterpret_cast<const void *>(k_extend<true, false, false, 2 * OVL_RJ>);
     return l16 ? reinterpret_cast<const void *>(k_extend<true, true>)
@@ -1346,16 +1390,24 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   auto per_wave_bytes = [](const ExtClass &g) {
     return g.stride * 4 + 16ull * (g.ecap + 2) + 28ull * (g.ecap + 8);
   };
-  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob, bool wide = false) -> int {
+  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob, bool wide = false,
+                        bool sh = false) -> int {
     ExtClass g;
     g.len = L;
     g.wide = wide;
+    g.sh = sh;
     g.ecap = ecap_of(L);
     g.sw = sw_of(L);
     g.l16 = L < 16384;
-    g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, ml_of(g.ecap))) / stg_lds_of(L));
-    if (g.wpb < 1) return -1;
-    g.lds = stg_lds_of(L) * g.wpb + ml_of(g.ecap);
+    if (sh) {
+      g.wpb = 8;
+      g.lds = sh_lds_of(L, g.wpb);
+      if (g.lds > cap) return -1;
+    } else {
+      g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, ml_of(g.ecap))) / stg_lds_of(L));
+      if (g.wpb < 1) return -1;
+      g.lds = stg_lds_of(L) * g.wpb + ml_of(g.ecap);
+    }
     // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the LDS so that at most that many blocks
     // fit on a CU (occupancy studies); unset = natural occupancy
     if (allow_knob)
@@ -1367,13 +1419,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     uint64_t st = (uint64_t)(g.ecap + 2) * lw / (g.l16 ? 2 : 1);   // the row log
     if (window) st = std::max<uint64_t>(st, 3ull * (g.ecap + 9) + 2ull * L + 64);
     g.stride = (st + 63) & ~63ull;
-    const void *kfn = stage_kernel(g.l16, wide);
+    const void *kfn = stage_kernel(g.l16, wide, sh);
     if (g.lds > 64 * 1024)
       if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess)
         return -1;
     // persistent grid: as many blocks as are resident at once (registers and LDS), so no
     // block starts only after the work queue has drained; within the scratch budget
-    uint32_t waves = 4u * OVL_EXT_OCC * c->n_cu;
+    uint32_t waves = 4u * (sh ? OVL_SH_OCC : OVL_EXT_OCC) * c->n_cu;
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kfn, 64 * g.wpb, g.lds) == hipSuccess &&
         bpc > 0)
@@ -1390,9 +1442,31 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // longest loaded read inside its tier, so its scratch (and a short-read job's launch) is
   // exactly what a job without the longer reads would get.
   {
+    uint32_t prev = 0;
+    // the shared-strand class (OVL_SHARED=0 turns it off): 4 blocks of 8 waves per CU within
+    // 40 KB each (32 waves: the reads <= ~11 kb), or 3 within 52 KB (24 waves, <= ~15 kb)
+    // when every read fits that and not the first; the -l kernel has its own order
+    const char *she = getenv("OVL_SHARED");
+    if (!ordered && !(she && atoi(she) == 0)) {
+      auto longest_sh = [&](size_t cap) -> uint32_t {
+        uint32_t L = 0;
+        for (uint32_t x : c->h_len)
+          if (x > L && sh_lds_of(x, 8) <= cap) L = x;
+        return L;
+      };
+      uint32_t L = longest_sh(40 * 1024);
+      size_t cap = 40 * 1024;
+      if (L < c->max_len && longest_sh(52 * 1024) == c->max_len) {
+        L = c->max_len;
+        cap = 52 * 1024;
+      }
+      if (L >= 64) {
+        if (make_stage(L, cap, true, false, true)) return fail(OVL_ERR_HIP, "shared staged kernel setup");
+        prev = L;
+      }
+    }
     const size_t tier_cap[3] = {OVL_EXT_OCC == 8 ? 40 * 1024 : 52 * 1024, 52 * 1024, 160 * 1024};
     const uint32_t tier_wpb[3] = {8, 6, 1};
-    uint32_t prev = 0;
     for (int t = 0; t < 3; t++) {
       const uint32_t T = longest_fitting(tier_wpb[t], tier_cap[t]);
       uint32_t L = 0;
@@ -1577,6 +1651,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       EA.ord_slot = nullptr;
       EA.ord_diag = nullptr;
       EA.dkey = nullptr;
+      EA.seg = nullptr;
+      EA.nseg_dev = nullptr;
+      EA.seg_next = x_ctr.p + 6;
       slot_pairs[slot] = npairs;
       HIPC(hipMemsetAsync(x_ctr.p, 0, 64, xs));
       if (npairs && ordered) {
@@ -1650,7 +1727,47 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
               fb.otmp.grow(std::max<size_t>(tmp, 1)))
             return fail(OVL_ERR_OOM, "work order");
         }
-        if (npairs > 1) {
+        const bool sh = !ext_stage.empty() && ext_stage[0].sh;
+        if (sh) {
+          // the shared-strand class's order: pairs grouped by unit (k_sh_keys), the groups'
+          // first positions selected (hipcub), the end appended
+          const int n = (int)npairs;
+          size_t t1 = 0, t2 = 0;
+          if (nc >= (1u << 28))
+            return fail(OVL_ERR_UNSUPPORTED, "%u units in one extension launch: past the shared-"
+                        "strand order's 28-bit unit field (OVL_SHARED=0 runs without it)", nc);
+          HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, fb.shk[0].p, fb.shk[1].p,
+                                                  fb.shi[0].p, fb.shi[1].p, n, 0, 64, xs));
+          hipcub::CountingInputIterator<uint32_t> it(0);
+          HIPC(hipcub::DeviceSelect::Flagged(nullptr, t2, it, fb.shf.p, fb.seg.p, fb.nseg.p, n, xs));
+          const size_t t = std::max(t1, t2);
+          if (fb.shk[0].n < npairs || fb.shk[1].n < npairs || fb.shi[0].n < npairs ||
+              fb.shi[1].n < npairs || fb.shw.n < nc || fb.seg.n < (size_t)npairs + 1 ||
+              fb.shf.n < npairs || fb.shtmp.n < t || !fb.nseg.p) {
+            HIPC(hipStreamSynchronize(xs));
+            if (fb.shk[0].grow(npairs) || fb.shk[1].grow(npairs) || fb.shi[0].grow(npairs) ||
+                fb.shi[1].grow(npairs) || fb.shw.grow(std::max<uint32_t>(nc, 1)) ||
+                fb.seg.grow((size_t)npairs + 1) || fb.shf.grow(npairs) ||
+                fb.shtmp.grow(std::max<size_t>(t, 1)) || fb.nseg.grow(1))
+              return fail(OVL_ERR_OOM, "shared-strand work order");
+          }
+          const dim3 grid(std::min<uint32_t>((npairs + 255) / 256, 4096)), blk(256);
+          HIPC(hipMemsetAsync(fb.shw.p, 0, 4ull * std::max<uint32_t>(nc, 1), xs));
+          hipLaunchKernelGGL(k_sh_unit_work, grid, blk, 0, xs, ext_pairs, npairs, fb.shw.p);
+          hipLaunchKernelGGL(k_sh_keys, grid, blk, 0, xs, ext_pairs, npairs, fb.shw.p, fb.shk[0].p,
+                             fb.shi[0].p);
+          size_t tt = t1;
+          HIPC(hipcub::DeviceRadixSort::SortPairs(fb.shtmp.p, tt, fb.shk[0].p, fb.shk[1].p,
+                                                  fb.shi[0].p, fb.shi[1].p, n, 0, 64, xs));
+          hipLaunchKernelGGL(k_sh_flags, grid, blk, 0, xs, fb.shk[1].p, npairs, fb.shf.p);
+          tt = t2;
+          HIPC(hipcub::DeviceSelect::Flagged(fb.shtmp.p, tt, it, fb.shf.p, fb.seg.p, fb.nseg.p, n, xs));
+          hipLaunchKernelGGL(k_sh_seg_end, dim3(1), dim3(1), 0, xs, fb.seg.p, fb.nseg.p, npairs);
+          HIPC(hipGetLastError());
+          EA.list = fb.shi[1].p;
+          EA.seg = fb.seg.p;
+          EA.nseg_dev = fb.nseg.p;
+        } else if (npairs > 1) {
           // longest-first work order (node count descending; ties keep pair order)
           hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
                              dim3(256), 0, xs, ext_pairs, npairs, fb.okey.p, fb.oidx.p);
@@ -1704,7 +1821,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
             // an empty class defers nothing: its counter stays 0 for the next one
           } else {
           n_ext_launch++;
-          if (g.wide && g.l16)
+          if (g.sh && g.l16)
+            hipLaunchKernelGGL((k_extend<true, true, false, OVL_RJ, true>), dim3(g.waves / g.wpb),
+                               dim3(64 * g.wpb), g.lds, xs, EA);
+          else if (g.sh)
+            hipLaunchKernelGGL((k_extend<true, false, false, OVL_RJ, true>), dim3(g.waves / g.wpb),
+                               dim3(64 * g.wpb), g.lds, xs, EA);
+          else if (g.wide && g.l16)
             hipLaunchKernelGGL((k_extend<true, true, false, 2 * OVL_RJ>), dim3(g.waves / g.wpb),
                                dim3(64 * g.wpb), g.lds, xs, EA);
           else if (g.wide)

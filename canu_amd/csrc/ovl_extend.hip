@@ -66,6 +66,12 @@ struct ExtendArgs {
   const uint32_t *ord_slot;     // String_Olap_Space order (Add_Ref's hash slots)
   const uint32_t *ord_diag;     // By_Diag_Sum order, ties in String_Olap_Space order (stable)
   const uint64_t *dkey;         // per pair: its average diagonal as an order-preserving key
+  // SH (the staged kernel with a block-shared query strand): list[] holds the pairs grouped
+  // by unit (units by descending work, a unit's pairs by descending node count); unit group
+  // g is list[seg[g] .. seg[g+1]); a block's waves share the query strand of each group
+  const uint32_t *seg;
+  const uint32_t *nseg_dev;
+  uint32_t *seg_next;           // global cursor over the groups
 };
 
 // debug counters (dbg != null): 0 ped calls 1 rows 2 chunks 3 slide words 4 tb steps
@@ -445,6 +451,9 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #define OVL_RJ 8
 #endif
 #define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
+#ifndef OVL_INPLACE
+#define OVL_INPLACE 1            // the row loop updates its row registers in place (A/B: 0)
+#endif
 static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 
 #ifdef OVL_PROFILE
@@ -775,7 +784,16 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     // ---- A+B per chunk: neighbours from row e-1 (DPP, no LDS), then the first 32-base
     // slide step of every lane, branch-free (one pass: each unrolled chunk costs a scalar
     // compare-and-branch on jr) --------------------------------------------------------
+#if OVL_INPLACE
+    // Row e is computed in place of row e-1 (R[j]); chunk j's lower neighbour is chunk j-1's
+    // OLD value, kept in prev_old.  The bases left before the end are recomputed where they
+    // are needed (the rare continued slides, the end row), and the end test is one mask of
+    // lanes whose slide reached its limit: 16 VGPRs fewer than keeping NR[] / RM[] arrays.
+    int32_t prev_old = -2;
+    uint64_t endm = 0;
+#else
     int32_t NR[J], RM[J];   // row value; lanes: bases left before the end (0 = end)
+#endif
     uint64_t need[J];
     uint64_t any = 0;
 #pragma unroll
@@ -784,7 +802,11 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t p0 = R[j];
       // row e-1 at d-1 and d+1 (diagonal B-1 and B+64J are outside the band: -2)
+#if OVL_INPLACE
+      const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, prev_old);
+#else
       const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, R[j > 0 ? j - 1 : 0]);
+#endif
       const int32_t pp = (j + 1 < J) ? dpp_upper_across(p0, R[j + 1 < J ? j + 1 : j])
                                      : dpp_from_upper(p0, -2);
       // q = Row - 1 = max(pm - 1, p0, pp): the +1 of the max3 folds into the constants
@@ -815,8 +837,15 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
                                     : (int32_t)__builtin_clz(mm | 1u);
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
+#if OVL_INPLACE
+      prev_old = p0;
+      R[j] = q + 1 + k;                        // lim >= 0 inside the band
+      // the slide reached its limit (no bases left): outside the band k = lim < lmin
+      endm |= __builtin_amdgcn_ballot_w64(k >= lmin);
+#else
       NR[j] = q + 1 + k;                       // lim >= 0 inside the band
       RM[j] = lmin - k;                        // inside: lim - k >= 0; outside: > 0
+#endif
       // run == 31 && lim > 31  <=>  min(run, lim - 1) == 31 (run <= 31): one ballot, no
       // scalar AND of two
       need[j] = __builtin_amdgcn_ballot_w64((run < lim - 1 ? run : lim - 1) == 31);
@@ -834,12 +863,28 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
         if (need[j]) {
+#if OVL_INPLACE
+          // the lane's end flag is set inside the divergent branch and balloted after it: a
+          // ballot merged out of a divergent region makes the mask (and every branch on it)
+          // divergent
+          bool fend = false;
+#endif
           if (need[j] & (1ull << lane)) {
             const int32_t d = B + 64 * j + (int32_t)lane;
+#if OVL_INPLACE
+            const int32_t rm = (m - R[j]) < (n - d - R[j]) ? (m - R[j]) : (n - d - R[j]);
+            const int32_t sl = slide_any<DIR>(A, a0, T, t0, R[j], d, rm);
+            R[j] += sl;
+            fend = sl >= rm;
+#else
             const int32_t sl = slide_any<DIR>(A, a0, T, t0, NR[j], d, RM[j]);
             NR[j] += sl;
             RM[j] -= sl;
+#endif
           }
+#if OVL_INPLACE
+          endm |= __builtin_amdgcn_ballot_w64(fend);
+#endif
 #ifdef OVL_PROFILE
           pc_slide++;
 #endif
@@ -857,6 +902,19 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     // first or last chunk, or the whole band) every chunk is rescanned below.  The end test
     // is a per-lane min of the bases left, one ballot per row.  (The per-chunk s_ff1 /
     // s_flbit / min reduction was 6 scalar instructions per chunk.)
+#if OVL_INPLACE
+#define NRJ(j) R[j]
+    uint64_t km0 = 0, kml = 0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      if (j >= JU && j > jr) break;
+      const int32_t d = B + 64 * j + (int32_t)lane;
+      kml = __builtin_amdgcn_ballot_w64(R[j] + (d > 0 ? d : 0) >= ML);
+      if (j == 0) km0 = kml;
+    }
+    const uint64_t endany = endm;
+#else
+#define NRJ(j) NR[j]
     int32_t rmin = RM[0];
     uint64_t km0 = 0, kml = 0;
 #pragma unroll
@@ -868,6 +926,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       if (j == 0) km0 = kml;
     }
     const uint64_t endany = __builtin_amdgcn_ballot_w64(rmin == 0);
+#endif
     uint32_t nlo, nhi;                         // min window offset of a kept lane; min
                                                // reversed offset (64J-1 - o) of one
     // s_ff1 / s_flbit give ~0u on an empty mask: one signed test of their OR sends the row
@@ -884,7 +943,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
         const int32_t d = B + 64 * j + (int32_t)lane;
-        const uint64_t km = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
+        const uint64_t km = __builtin_amdgcn_ballot_w64(NRJ(j) + (d > 0 ? d : 0) >= ML);
         uint32_t f1, fb;
         asm("s_ff1_i32_b64 %0, %1" : "=s"(f1) : "s"(km));
         asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(km));
@@ -913,6 +972,16 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
 #pragma unroll
       for (int j = J - 1; j >= 0; j--) {
         if (j >= JU && j > jr) continue;
+#if OVL_INPLACE
+        const int32_t d = B + 64 * j + (int32_t)lane;
+        const int32_t rm = (m - R[j]) < (n - d - R[j]) ? (m - R[j]) : (n - d - R[j]);
+        const uint64_t em = __builtin_amdgcn_ballot_w64(rm == 0);
+        if (em) {
+          const int32_t l = (int32_t)__builtin_ctzll(em);
+          end_d = B + 64 * j + l;
+          end_row = __builtin_amdgcn_readlane(R[j], l);
+        }
+#else
         const uint64_t em = __builtin_amdgcn_ballot_w64(RM[j] == 0);
         if (em) {
           const int32_t l = (int32_t)__builtin_ctzll(em);
@@ -922,7 +991,17 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
           end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
                  : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
         }
+#endif
       }
+#if OVL_INPLACE
+      // row e-1 at end_d+1, from the row log (R holds row e now); the forward rule below
+      // needs it only when the end is A's end: one load, once per extension
+      if (DIR > 0) {
+        vm_sync();
+        const int32_t c = (end_d + 1) & (LW - 1);
+        end_pp = (int32_t)clog[(size_t)(e - 1) * LW + c];
+      }
+#endif
       ended = true;
       end_e = e;
       e = limit + 1;
@@ -946,7 +1025,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jrs) break;
         const int32_t d = B + 64 * j + (int32_t)lane;
-        const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
+        const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NRJ(j) : -2;
         R[j] = v;
         const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
         kmx = key > kmx ? key : kmx;
@@ -1019,6 +1098,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   }
   // stopped with rows left to compute: the window overflowed (every other stop sets e
   // past the limit)
+#undef NRJ
   if (e <= limit) out.ovf = 1;
   if (out.ovf) return out;
   const int32_t max_score_best_d = ms_B + ((1 << WB) - 1) - (ms_key & ((1 << WB) - 1));
@@ -1794,8 +1874,31 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
 #endif
 // RJ: register chunks of the staged kernel's row window (OVL_RJ; the wide class that takes
 // the pairs whose band outgrows it runs 2 x OVL_RJ at lower occupancy)
-template <bool STAGE, bool L16, bool ORD = false, int RJ = OVL_RJ>
-__global__ void __launch_bounds__(512, RJ > OVL_RJ ? 3 : OVL_EXT_OCC) k_extend(ExtendArgs X) {
+#define OVL_SH_SLOTS 3           // SH: query strands a block holds at once (LDS slots)
+
+// SH: block-shared query strands.  At 10 kb each wave's two staged strands (2 x 2.5 KB) plus
+// its scratch cap a CU at 24 waves by LDS alone; the pairs of one (query, orientation) unit
+// share the query strand (12.6 pairs per unit in the 50k x 10 kb job), so a block keeps
+// OVL_SH_SLOTS query strands and each wave stages only its target.  Slot protocol (LDS
+// atomics, no block barrier after the start): ctl = (end << 32) | next over the sorted pair
+// list; a wave takes pair `next` of a slot after incrementing the slot's users; a slot whose
+// pairs are all taken and that no wave is using is reloaded with the next unit group by the
+// wave that claims it (loading flag) -- no wave can be reading its old strand then, since a
+// reader holds a valid pair and so a user count.
+struct ShSlot {
+  unsigned long long ctl;       // (end << 32) | next
+  int32_t users;                // waves holding a pair of this slot
+  int32_t loading;              // a wave is reloading the slot
+  int32_t bad;                  // the unit's query strand cannot be staged: defer its pairs
+  int32_t pad[3];
+};
+
+#ifndef OVL_SH_OCC
+#define OVL_SH_OCC 8             // waves per SIMD the shared-strand kernel is compiled for
+#endif
+template <bool STAGE, bool L16, bool ORD = false, int RJ = OVL_RJ, bool SH = false>
+__global__ void __launch_bounds__(512, SH ? OVL_SH_OCC : RJ > OVL_RJ ? 3 : OVL_EXT_OCC)
+k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -1813,7 +1916,30 @@ __global__ void __launch_bounds__(512, RJ > OVL_RJ ? 3 : OVL_EXT_OCC) k_extend(E
   WM.rowdir = X.rowdir + (size_t)gw * 4 * (X.e_cap + 2);
   WM.mlim = l_ext0;
   lds_u64 *sw = nullptr, *tw = nullptr;
-  if constexpr (STAGE) {
+  ShSlot *slots = nullptr;
+  lds_u64 *sstr = nullptr;
+  if constexpr (SH) {
+    // block: [slot control][query strand slots] then per wave [T words | scratch]
+    slots = (ShSlot *)s_ext;
+    sstr = (lds_u64 *)(s_ext + (OVL_SH_SLOTS * sizeof(ShSlot) + 16) / 4);
+    lds_i32 *wbase = (lds_i32 *)(sstr + OVL_SH_SLOTS * X.sw_words);
+    uint32_t wave_ints = 2 * (uint32_t)X.sw_words + OVL_SCR;
+    lds_i32 *wlds = wbase + wave * wave_ints;
+    tw = (lds_u64 *)wlds;
+    WM.lrow = nullptr;
+    WM.wcap = 0;
+    WM.tbw = wlds + 2 * X.sw_words;
+    WM.ldc = WM.tbw;
+    WM.ldcap = OVL_SCR;
+    if (threadIdx.x < OVL_SH_SLOTS) {
+      slots[threadIdx.x].ctl = 0;                     // next = end = 0: exhausted, unused
+      slots[threadIdx.x].users = 0;
+      slots[threadIdx.x].loading = 0;
+      slots[threadIdx.x].bad = 0;
+    }
+    if (threadIdx.x == 0) *(int32_t *)(slots + OVL_SH_SLOTS) = 0;   // no more groups
+    __syncthreads();
+  } else if constexpr (STAGE) {
     // per wave: [S words | T words] (u64) then the scratch
     uint32_t wave_ints = 4 * (uint32_t)X.sw_words + OVL_SCR;
     lds_i32 *wlds = s_ext + wave * wave_ints;
@@ -1842,7 +1968,96 @@ __global__ void __launch_bounds__(512, RJ > OVL_RJ ? 3 : OVL_EXT_OCC) k_extend(E
   unsigned long long st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t npairs = X.npairs_dev ? __builtin_amdgcn_readfirstlane(*X.npairs_dev) : X.npairs;
 
-  if constexpr (ORD) {
+  if constexpr (SH) {
+    static_assert(STAGE, "SH is a staged kernel");
+    volatile int32_t *done = (volatile int32_t *)(slots + OVL_SH_SLOTS);
+    const uint32_t nseg = __builtin_amdgcn_readfirstlane(*X.nseg_dev);
+    int32_t last = (int32_t)(wave % OVL_SH_SLOTS);
+    for (;;) {
+      // a pair from a loaded slot (the wave's last slot first)
+      int32_t slot = -1;
+      uint32_t li = 0;
+      for (int32_t kk = 0; kk < OVL_SH_SLOTS; kk++) {
+        const int32_t sl = (last + kk) % OVL_SH_SLOTS;
+        unsigned long long c = 0;
+        if (lane == 0) {
+          atomicAdd(&slots[sl].users, 1);
+          c = atomicAdd(&slots[sl].ctl, 1ull);
+        }
+        const uint32_t idx = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)c);
+        const uint32_t end = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(c >> 32));
+        if (idx < end) { slot = sl; li = idx; break; }
+        if (lane == 0) atomicSub(&slots[sl].users, 1);
+      }
+      if (slot < 0) {
+        // none: reload a slot whose pairs are all taken and that no wave uses
+        bool loaded = false, finished = false;
+        for (int32_t sl = 0; sl < OVL_SH_SLOTS && !loaded && !finished; sl++) {
+          int32_t claim = 0;
+          if (lane == 0) {
+            const unsigned long long c = __hip_atomic_load(&slots[sl].ctl, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int32_t us = __hip_atomic_load(&slots[sl].users, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((uint32_t)c >= (uint32_t)(c >> 32) && us == 0 &&
+                atomicCAS(&slots[sl].loading, 0, 1) == 0)
+              claim = 1;
+          }
+          claim = __builtin_amdgcn_readfirstlane(claim);
+          if (!claim) continue;
+          uint32_t g = 0;
+          if (lane == 0) g = atomicAdd(X.seg_next, 1u);
+          g = __builtin_amdgcn_readfirstlane(g);
+          if (g >= nseg) {
+            if (lane == 0) { *done = 1; atomicExch(&slots[sl].loading, 0); }
+            finished = true;
+            break;
+          }
+          const uint32_t b = X.seg[g], e = X.seg[g + 1];
+          const PairRec P0 = X.pairs[X.list[b]];
+          const Unit un0 = X.units[P0.unit];
+          const Strand S0 = un0.dir ? strand_rc(X.R, un0.r) : strand_fwd(X.R, un0.r);
+          const bool ok = !(S0.ex_wild || S0.ex_nul) && S0.len <= X.stage_len;
+          if (ok) (void)stage_strand(S0, sstr + sl * X.sw_words, lane);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          lds_sync();
+          if (lane == 0) {
+            slots[sl].bad = ok ? 0 : 1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            atomicExch(&slots[sl].ctl, ((unsigned long long)e << 32) | b);
+            atomicExch(&slots[sl].loading, 0);
+          }
+          loaded = true;
+          last = sl;
+        }
+        if (loaded) continue;
+        if (finished || *done) break;        // no unit group left: the slots hold the rest
+        __builtin_amdgcn_s_sleep(2);         // a slot is still in use: wait for it
+        continue;
+      }
+      last = slot;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const uint32_t pi = X.list[li];
+      PairRec P = X.pairs[pi];
+      Unit un = X.units[P.unit];
+      Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
+      Strand T = strand_fwd(X.R, P.tgt);
+      bool ok = false;
+      const int32_t bad = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&slots[slot].bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (!bad && !T.ex_wild && T.len <= X.stage_len) {
+        StrandLP SL;
+        SL.w = sstr + slot * X.sw_words;
+        SL.len = S.len;
+        StrandLP TL = stage_strand(T, tw, lane);
+        lds_sync();
+        ok = process_pair<true, L16, false, RJ>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
+      }
+      if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
+      lds_sync();
+      if (lane == 0) atomicSub(&slots[slot].users, 1);
+    }
+  } else if constexpr (ORD) {
     static_assert(!STAGE, "the -l kernel is the generic one");
     for (;;) {
       uint32_t ui = 0;
