@@ -242,6 +242,34 @@ struct ovl_ctx {
     uint64_t nu = 0, nn = 0, np = 0;
   } acc;
 
+  // OverlapDriver jobs: the query windows sorted by k-mer once per job (k_sq_keys,
+  // k_probe_sorted in ovl_seed.hip; sq_prepare below).  sq_request: the driver asks find_impl
+  // to use them from its second hash batch on (OVL_SQ=0 never, =1 from the first).
+  bool sq_request = false;
+  struct SqRun {
+    uint32_t u0, u1;             // the run's units [u0, u1) of sq.units
+    uint64_t e0, n;              // its windows: entries [e0, e0 + n) of key / wid
+    uint64_t wb0, ub0;           // offsets of its unit bases (n units + 1) and 512-window blocks
+  };
+  struct {
+    bool on = false;
+    uint32_t ref_bgn = 0, ref_end = 0, lib_lo = 0, lib_hi = 0, hash_lo = 0;
+    std::vector<Unit> units;     // the job's query units, read order
+    std::vector<uint32_t> ureadiid;
+    std::vector<uint64_t> uwin;  // windows per unit
+    std::vector<uint64_t> wb;    // per unit + one per run: run-local first window (as dwbase)
+    std::vector<SqRun> runs;
+    DBuf<uint64_t> key, key2;
+    DBuf<uint32_t> wid, wid2, ublk;
+    DBuf<uint64_t> dwbase;
+    DBuf<Unit> dunits;
+    DBuf<uint8_t> tmp;
+    DBuf<uint32_t> uhits, uflags;
+    int probed = -1;             // the run whose records fb.probe holds for this batch
+    uint32_t probed_nu = 0;      // ... for this many of its units
+    double ms_sort = 0;
+  } sq;
+
   // results
   DBuf<Rec> d_out;
   uint64_t nout = 0;
@@ -1018,6 +1046,7 @@ static const uint64_t MAX_STRING_NUM = (1ull << 31) - 1; // overlapInCore.C:57-6
 // previous search hold (released when a build needs it), less 64 GB kept for the seed and
 // extension buffers (whose budgets shrink to fit).  OVL_TEST_INDEX_WINDOW_CAP lowers
 // it (tests of the capped path).
+static void sq_release(ovl_ctx *c);
 static void release_find_buffers(ovl_ctx *c) {
   auto &f = c->fb;
   for (int i = 0; i < 2; i++) {
@@ -1031,6 +1060,7 @@ static void release_find_buffers(ovl_ctx *c) {
   f.ucnt.release(); f.useg.release(); f.hcnt.release(); f.hbase.release(); f.hbuf.release();
   f.rows.release(); f.rowdir.release(); f.deltas.release();
   for (int i = 0; i < 2; i++) { f.shk[i].release(); f.shi[i].release(); }
+  sq_release(c);
   f.shw.release(); f.seg.release(); f.nseg.release(); f.shf.release(); f.shtmp.release();
   // the extension accumulator's buffers, once nothing waits in them
   if (c->acc.np == 0) {
@@ -1161,10 +1191,10 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
         eb = id;
       }
     }
-    if ((rc = build_index(c, bgn, eb, true)) == OVL_ERR_OOM) {
+    if ((rc = build_index(c, bgn, eb, !c->sq.on)) == OVL_ERR_OOM) {
       // the previous batch's search buffers make room (the next search grows them again)
       release_find_buffers(c);
-      rc = build_index(c, bgn, eb, true);
+      rc = build_index(c, bgn, eb, !c->sq.on);
     }
     if (rc) return rc;
     if (!load_may_cut) break;
@@ -1192,7 +1222,7 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
       if (entries >= entry_limit) { el = bgn + i; reached = true; break; }
     }
     if (reached) {
-      if (el < eb && (rc = build_index(c, bgn, el, true))) return rc;
+      if (el < eb && (rc = build_index(c, bgn, el, !c->sq.on))) return rc;
       e = el;
       uint64_t cw = 0;
       for (uint32_t id = bgn; id <= el; id++) {
@@ -1247,6 +1277,116 @@ static bool use_bloom(const ovl_ctx *c, uint32_t bgn, uint32_t end) {
   return 4 * (q - inside) >= 3 * q;
 }
 
+// The sorted query windows of an OverlapDriver job (k_sq_keys / k_probe_sorted): the units
+// find_impl searches (ref reads bgn..end of libraries [lib_lo, lib_hi] at least --minlength
+// and k long, both orientations, read order), their windows keyed by mix64(k-mer) and
+// radix-sorted once, in runs of <= 2^30 windows.  A batch searches the units of the reads
+// below its last hash read: a prefix of them, so per run a window-id bound.  Off (and the
+// random-lookup probe used) when the keys would take more than a third of the free HBM.
+static void sq_release(ovl_ctx *c) {
+  auto &Q = c->sq;
+  Q.on = false;
+  Q.key.release(); Q.key2.release(); Q.wid.release(); Q.wid2.release(); Q.ublk.release();
+  Q.dwbase.release(); Q.dunits.release(); Q.tmp.release(); Q.uhits.release(); Q.uflags.release();
+  Q.units.clear(); Q.ureadiid.clear(); Q.uwin.clear(); Q.wb.clear(); Q.runs.clear();
+  Q.probed = -1;
+}
+
+static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, uint32_t lib_hi) {
+  auto &Q = c->sq;
+  if (Q.on && Q.ref_bgn == bgn && Q.ref_end == end && Q.lib_lo == lib_lo && Q.lib_hi == lib_hi)
+    return OVL_OK;
+  sq_release(c);
+  const uint32_t k = c->P.kmer_len;
+  for (uint32_t a = bgn; a <= end && a >= bgn; a++) {         // find_impl's unit rule
+    const uint32_t r = a - c->first_iid;
+    const int32_t L = (int32_t)c->h_len[r];
+    const uint32_t lib = read_lib(c, r);
+    if (lib < lib_lo || lib > lib_hi || L < c->P.min_olap_len || L < (int32_t)k) continue;
+    for (uint32_t dir = 0; dir < 2; dir++) {
+      Q.units.push_back(Unit{r, dir});
+      Q.ureadiid.push_back(a);
+      Q.uwin.push_back((uint64_t)(L - (int32_t)k + 1));
+    }
+  }
+  const uint32_t nu = (uint32_t)Q.units.size();
+  if (nu == 0) return OVL_OK;
+  // runs of <= 2^30 windows (hipcub sorts index with int)
+  const uint64_t RUN = 1ull << 30;
+  uint64_t total = 0, maxrun = 0;
+  for (uint32_t u = 0; u < nu;) {
+    ovl_ctx::SqRun R;
+    R.u0 = u;
+    R.e0 = total;
+    R.n = 0;
+    while (u < nu && (R.n + Q.uwin[u] <= RUN || u == R.u0)) R.n += Q.uwin[u++];
+    R.u1 = u;
+    R.wb0 = Q.wb.size();
+    uint64_t acc = 0;
+    for (uint32_t x = R.u0; x < R.u1; x++) { Q.wb.push_back(acc); acc += Q.uwin[x]; }
+    Q.wb.push_back(acc);
+    total += R.n;
+    maxrun = std::max(maxrun, R.n);
+    Q.runs.push_back(R);
+  }
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return OVL_OK;
+  const uint64_t need = 12ull * total + 20ull * maxrun + 8ull * (maxrun >> 9) + 64ull * nu;
+  if (need > fr / 3) { sq_release(c); return OVL_OK; }
+  hipStream_t s = c->stream;
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t tmpb = 0;
+  HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, Q.key2.p, Q.key.p, Q.wid2.p, Q.wid.p,
+                                          (int)std::min<uint64_t>(maxrun, RUN), 0, 64, s));
+  std::vector<uint32_t> ublk;
+  for (auto &R : Q.runs) {
+    R.ub0 = ublk.size();
+    uint32_t x = 0;
+    for (uint64_t w = 0; w < R.n; w += 512) {
+      while (Q.wb[R.wb0 + x + 1] <= w) x++;
+      ublk.push_back(x);
+    }
+  }
+  if (Q.key.alloc(total) || Q.wid.alloc(total) || Q.key2.alloc(maxrun) || Q.wid2.alloc(maxrun) ||
+      Q.tmp.alloc(std::max<size_t>(tmpb, 1)) || Q.dwbase.alloc(Q.wb.size()) ||
+      Q.dunits.alloc(nu) || Q.ublk.alloc(std::max<size_t>(ublk.size(), 1)) ||
+      Q.uhits.alloc(nu) || Q.uflags.alloc(nu)) {
+    sq_release(c);
+    return OVL_OK;                                 // no room: the random-lookup probe
+  }
+  HIPC(hipMemcpyAsync(Q.dwbase.p, Q.wb.data(), 8ull * Q.wb.size(), hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(Q.dunits.p, Q.units.data(), sizeof(Unit) * nu, hipMemcpyHostToDevice, s));
+  if (!ublk.empty())
+    HIPC(hipMemcpyAsync(Q.ublk.p, ublk.data(), 4ull * ublk.size(), hipMemcpyHostToDevice, s));
+  for (const auto &R : Q.runs) {
+    SqKeyArgs KA;
+    KA.R = c->reads();
+    KA.units = Q.dunits.p + R.u0;
+    KA.wbase = Q.dwbase.p + R.wb0;
+    KA.nunits = R.u1 - R.u0;
+    KA.k = k;
+    KA.kmask = (1ull << (2 * k)) - 1;
+    KA.key = Q.key2.p;
+    KA.wid = Q.wid2.p;
+    hipLaunchKernelGGL(k_sq_keys, dim3((KA.nunits + 3) / 4), dim3(256), 0, s, KA);
+    HIPC(hipGetLastError());
+    size_t tb = tmpb;
+    HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
+                                            Q.wid.p + R.e0, (int)R.n, 0, 64, s));
+  }
+  HIPC(hipStreamSynchronize(s));
+  // the sort buffers go: only the sorted runs stay for the job
+  Q.key2.release();
+  Q.wid2.release();
+  Q.tmp.release();
+  Q.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->stats.ms_seed += Q.ms_sort;
+  Q.ref_bgn = bgn; Q.ref_end = end; Q.lib_lo = lib_lo; Q.lib_hi = lib_hi;
+  Q.on = true;
+  Q.probed = -1;
+  return OVL_OK;
+}
+
 // Process_Overlaps (overlapInCore-Process_Overlaps.C:101-137) over ref reads bgn..end of
 // libraries [lib_lo, lib_hi] against the current index.  append: keep the records and
 // counters already held (the driver's later hash batches).
@@ -1289,6 +1429,21 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     c->nout = 0;
   }
   c->stats.ref_reads += nref;
+
+  // OverlapDriver batches: the job's query windows sorted once (sq_prepare); this batch's
+  // units are the first nu of the job's (the reads below its last hash read)
+  if (c->sq_request && !units.empty())
+    if (int rc = sq_prepare(c, bgn, end, lib_lo, lib_hi)) return rc;
+  const bool sqm = c->sq_request && c->sq.on && !units.empty();
+  if (sqm) {
+    auto &Q = c->sq;
+    if (units.size() > Q.units.size() ||
+        memcmp(units.data(), Q.units.data(), sizeof(Unit) * units.size()) != 0)
+      return fail(OVL_ERR_HIP, "sorted query windows: unit list mismatch");
+    Q.probed = -1;                                  // a new index: no run probed against it
+  }
+  std::vector<uint32_t> sq_uh;                      // the probed run's unit hit counts
+  size_t sq_run = 0;
 
   // per-context device buffers, sized per batch
   // A batch is sized by seed hits (node pool + list-ordered copy: 32 B per hit); the probe
@@ -1937,12 +2092,69 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     auto &d_units = c->fb.units[slot];
     auto &d_pnodes = c->fb.pnodes[slot];
     auto &d_pairs = c->fb.pairs[slot];
+    uint32_t nb = 0;
+    std::vector<uint64_t> rbase;
+    std::vector<uint32_t> uh;
+    uint32_t *chain_uflags = nullptr;
+    if (sqm) {
+      // the run of sorted windows holding unit u0: probed once per batch (k_probe_sorted),
+      // its records then chained in hit-budget chunks
+      auto &Q = c->sq;
+      while (Q.runs[sq_run].u1 <= u0) sq_run++;
+      const auto &R = Q.runs[sq_run];
+      const uint32_t ue = std::min<uint32_t>(R.u1, nu);
+      if (Q.probed != (int)sq_run) {
+        const uint64_t wlim = Q.wb[R.wb0 + (ue - R.u0)];
+        if (d_probe.grow(R.n)) return fail(OVL_ERR_OOM, "probe records (%llu)", (unsigned long long)R.n);
+        HIPC(hipEventRecord(c->ev[2], s));
+        HIPC(hipMemsetAsync(d_probe.p, 0, 8ull * wlim, s));
+        HIPC(hipMemsetAsync(Q.uhits.p + R.u0, 0, 4ull * (ue - R.u0), s));
+        HIPC(hipMemsetAsync(Q.uflags.p + R.u0, 0, 4ull * (ue - R.u0), s));
+        SqProbeArgs SA;
+        SA.X = index_dev(c);
+        SA.R = c->reads();
+        SA.key = Q.key.p + R.e0;
+        SA.wid = Q.wid.p + R.e0;
+        SA.n = R.n;
+        SA.wlim = (uint32_t)wlim;
+        SA.units = Q.dunits.p + R.u0;
+        SA.wbase = Q.dwbase.p + R.wb0;
+        SA.ublk = Q.ublk.p + R.ub0;
+        SA.k = k;
+        SA.out = d_probe.p;
+        SA.unit_hits = Q.uhits.p + R.u0;
+        SA.unit_flags = Q.uflags.p + R.u0;
+        hipLaunchKernelGGL(k_probe_sorted, dim3(8 * c->n_cu), dim3(256), 0, s, SA);
+        n_probe_launch++;
+        HIPC(hipGetLastError());
+        HIPC(hipEventRecord(c->ev[3], s));
+        sq_uh.resize(ue - R.u0);
+        HIPC(hipMemcpyAsync(sq_uh.data(), Q.uhits.p + R.u0, 4ull * (ue - R.u0),
+                            hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        float t = 0;
+        (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+        ms_probe += t;
+        // algorithmic bytes: the sorted windows (8-B key + 4-B id), the table read once, a
+        // record written for every searched window (the zeroing and the hits)
+        probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) + 8ull * wlim;
+        Q.probed = (int)sq_run;
+      }
+      nb = ue - u0;
+      rbase.assign(Q.wb.begin() + R.wb0 + (u0 - R.u0), Q.wb.begin() + R.wb0 + (ue - R.u0) + 1);
+      uh.assign(sq_uh.begin() + (u0 - R.u0), sq_uh.begin() + (ue - R.u0));
+      chain_uflags = Q.uflags.p + u0;
+      if (d_units.grow(nb) || d_rbase.grow(nb + 1))
+        return fail(OVL_ERR_OOM, "unit buffers");
+      HIPC(hipMemcpyAsync(d_units.p, units.data() + u0, sizeof(Unit) * nb, hipMemcpyHostToDevice, s));
+      HIPC(hipMemcpyAsync(d_rbase.p, rbase.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
+    } else {
     // batch by probe slots
     uint32_t u1 = u0;
     uint64_t wsum = 0;
     while (u1 < nu && (wsum + uwin[u1] <= WIN_BUDGET || u1 == u0)) wsum += uwin[u1++];
-    uint32_t nb = u1 - u0;
-    std::vector<uint64_t> rbase(nb + 1);
+    nb = u1 - u0;
+    rbase.resize(nb + 1);
     uint64_t acc = 0;
     for (uint32_t i = 0; i < nb; i++) { rbase[i] = acc; acc += uwin[u0 + i]; }
     rbase[nb] = acc;
@@ -1974,7 +2186,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     n_probe_launch++;
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev[3], s));
-    std::vector<uint32_t> uh(nb);
+    uh.resize(nb);
     HIPC(hipMemcpyAsync(uh.data(), d_uhits.p, 4ull * nb, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     float t = 0;
@@ -1986,6 +2198,8 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     // algorithmic bytes: per window one 16-B table entry and one 8-B Probe record, plus the
     // packed query (2 bits per base); see DESIGN.md
     probe_bytes += acc * 24 + acc / 4;
+    chain_uflags = d_uflags.p;
+    }
     // shrink the batch to the hit budget (probe results stay valid for the prefix)
     uint64_t hsum = 0;
     uint32_t nc = 0;
@@ -2051,7 +2265,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       CA.units = d_units.p;
       CA.rbase = d_rbase.p;
       CA.probes = d_probe.p;
-      CA.unit_flags = d_uflags.p;
+      CA.unit_flags = chain_uflags;
       CA.nunits = nc;
       CA.k = k;
       CA.unit_next = d_ctr.p + 0;
@@ -2120,8 +2334,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       }
       chain_retries++;
     }
-    (void)hipEventElapsedTime(&t, c->ev[4], c->ev[5]);
-    ms_chain += t;
+    {
+      float t = 0;
+      (void)hipEventElapsedTime(&t, c->ev[4], c->ev[5]);
+      ms_chain += t;
+    }
     {
       unsigned long long h = 0;
       HIPC(hipMemcpy(&h, c->fb.chits.p, 8, hipMemcpyDeviceToHost));
@@ -2379,6 +2596,15 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   uint32_t bgn = g_bgn_hash;
   uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
   uint64_t batches = 0;
+  // the query windows sorted once for the job's batches (sq_prepare) from its second batch
+  // on -- a one-batch job probes at random as ovl_find_overlaps does; OVL_SQ=0: never,
+  // OVL_SQ=1: from the first batch.  They are the job's own work: released at its end.
+  int sq_mode = 2;
+  if (const char *e = getenv("OVL_SQ")) sq_mode = atoi(e);
+  struct SqOff {
+    ovl_ctx *c;
+    ~SqOff() { c->sq_request = false; sq_release(c); }
+  } sq_off{c};
   while (bgn < g_end_hash) {                                             // :222
     if (end > g_end_hash) end = g_end_hash;
     uint32_t loaded = 0;
@@ -2392,6 +2618,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
       // the batches' pairs are extended together: the last batch flushes what is pending
       uint64_t n = 0;
       const bool last_batch = !(end + 1 < g_end_hash);
+      c->sq_request = sq_mode == 1 || (sq_mode == 2 && batches >= 2);
       if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n,
                           last_batch)))
         return rc;

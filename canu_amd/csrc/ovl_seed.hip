@@ -175,6 +175,102 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------
+// OverlapDriver jobs: the query windows sorted by k-mer once per job.
+// Every hash batch of a driver job is searched by the same query reads (every read of the
+// -r range below the batch's end; Process_Overlaps.C:101-137), and most of their windows
+// miss the batch, so k_probe's one random table lookup per window per batch runs at the
+// memory system's random-access rate (~40 G lookups/s, whatever the table's size).  Here the
+// job's query windows are keyed by their k-mer's mix64 and radix-sorted ONCE (k_sq_keys, in
+// runs of <= 2^30 windows); each batch then streams a run in key order, which is table-slot
+// order (a slot is the top tab_bits of the same mix64): consecutive windows read consecutive
+// slots, the table and the windows are both read as streams, and only the windows whose
+// k-mer the batch holds write a Probe record back to window order (k_probe_sorted).  The
+// records, unit hit counts and screened-end flags are exactly k_probe's.
+
+struct SqKeyArgs {
+  ReadsDev R;
+  const Unit *units;            // the run's units
+  const uint64_t *wbase;        // per unit: first window (run-local)
+  uint32_t nunits, k;
+  uint64_t kmask;
+  uint64_t *key;                // run-local window id -> mix64(k-mer)
+  uint32_t *wid;                // -> the window id; 0xFFFFFFFF: no k-mer there (an N, a NUL)
+};
+
+// one wave per unit: its windows' keys, k_probe's window rule (unit_windows, the N / NUL masks)
+__global__ void __launch_bounds__(256) k_sq_keys(SqKeyArgs A) {
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t u = blockIdx.x * 4 + wave;
+  if (u >= A.nunits) return;
+  const Unit un = A.units[u];
+  const Strand S = un.dir ? strand_rc(A.R, un.r) : strand_fwd(A.R, un.r);
+  const uint32_t *bad = un.dir ? S.ex_nul : S.ex_wild;
+  const uint32_t nw = unit_windows(A.R, un, A.k);
+  const int32_t L = S.len;
+  const uint32_t kbits = (1u << A.k) - 1u;
+  const uint64_t b = A.wbase[u];
+  for (uint32_t o = lane; o < nw; o += 64) {
+    bool ok = (int32_t)(o + A.k) <= L;
+    if (ok && bad) ok = (mask_at(bad, (int32_t)o) & kbits) == 0;
+    A.key[b + o] = ok ? mix64(bases_at(S.w, (int32_t)o) & A.kmask) : ~0ull;
+    A.wid[b + o] = ok ? (uint32_t)(b + o) : 0xFFFFFFFFu;
+  }
+}
+
+struct SqProbeArgs {
+  IndexDev X;
+  ReadsDev R;
+  const uint64_t *key;          // the run's windows, sorted by key
+  const uint32_t *wid;
+  uint64_t n;
+  uint32_t wlim;                // this batch searches the run's windows below wlim
+  const Unit *units;            // the run's units
+  const uint64_t *wbase;        // per run unit: first window; [nunits] = the run's windows
+  const uint32_t *ublk;         // per 512 windows: the unit holding the block's first window
+  uint32_t k;
+  Probe *out;                   // run-local window id -> its record (zeroed up to wlim)
+  uint32_t *unit_hits, *unit_flags;   // per run unit (zeroed)
+};
+
+__global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
+  const uint64_t smask = (1ull << A.X.slice_bits) - 1;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < A.n; i += stride) {
+    const uint32_t w = A.wid[i];
+    if (w >= A.wlim) continue;                   // no k-mer, or a unit this batch skips
+    const uint64_t M = A.key[i];
+    const uint64_t s0 = M >> (64 - A.X.tab_bits), base = s0 & ~smask;
+    TabEntry t = A.X.tab[s0];
+    bool found = false;
+    for (uint64_t j = 1;; j++) {                 // index_find's linear probe (k_probe)
+      if (t.cnt == 0) break;
+      if (t.key == M) { found = true; break; }
+      if (j > smask) break;
+      t = A.X.tab[base | ((s0 + j) & smask)];
+    }
+    if (!found) continue;
+    uint32_t u = A.ublk[w >> 9];
+    while (A.wbase[u + 1] <= w) u++;
+    const uint32_t c = t.cnt;
+    if (c & OVL_FLAG_SKIP) {
+      // Hash_Find found an Empty entry: hi_hits (Find_Overlaps.C:321-366)
+      const uint32_t o = w - (uint32_t)A.wbase[u];
+      const int32_t L = (int32_t)A.R.len[A.units[u].r];
+      uint32_t f = 0;
+      if (o < 90) f |= 2u;
+      if (o > 0 && L - (int32_t)o - (int32_t)A.k + 1 < 90) f |= 4u;
+      if (f) atomicOr(&A.unit_flags[u], f);
+    } else {
+      Probe pr;
+      pr.off = t.off;
+      pr.cnt = c & OVL_CNT_MASK;
+      A.out[w] = pr;
+      atomicAdd(&A.unit_hits[u], pr.cnt);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // The seed-hit list (ovl_seed_hits): every Add_Ref call of Find_Overlaps (:328-370) as
 // {query, target, window | dir << 31, target offset}, in the reference's order -- window
 // ascending, then the k-mer's chain order (target iid, offset descending).  One wave per

@@ -311,3 +311,33 @@ def test_gpu_driver_screened_ends_across_batches(built):
     assert got.shape == ref.shape and np.array_equal(got, ref)
     for rk, ok in STAT_KEYS:
         assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_gpu_sorted_query_windows_are_exact(built, monkeypatch, mode):
+    """OverlapDriver batches searched through the job's query windows sorted once by k-mer
+    (k_probe_sorted; OVL_SQ=1 from the first batch) and by one random table lookup per
+    window (k_probe; OVL_SQ=0): the same records and -s counters, the reference's -- with
+    N bases (windows without a k-mer, NUL-ended reverse strands), ragged lengths and end
+    skip k-mers (screened ends set from the sorted windows)."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    oracle.require_reference()
+    monkeypatch.setenv("OVL_SQ", mode)
+    rs = synth_reads(n_reads=240, read_len=3000, genome_len=60_000, error_rate=0.03, seed=28,
+                     len_jitter=0.4, n_rate=0.001)
+    skip = _end_skip_kmers(rs)
+    P = _params()
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=45, Num_PThreads=4).finalize()
+    oic = OverlapInCore(O, device=0)
+    got = oic.run_driver(rs, skip_kmers=skip)
+    st = oic.stats()
+    oic.close()
+    assert st["hash_batches"] >= 5
+    ref, rst = oracle.run_reference(rs, P, threads=4, hash_bits=22,
+                                    batching={"hashstrings": 45}, skip_kmers=skip,
+                                    with_stats=True)
+    assert got.shape == ref.shape and np.array_equal(got, ref)
+    for rk, ok in STAT_KEYS:
+        assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
