@@ -1336,8 +1336,12 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   hipStream_t s = c->stream;
   const auto t0 = std::chrono::steady_clock::now();
   size_t tmpb = 0;
+  // only the top SQ_BITS of a key order the windows: a table slot is the key's top tab_bits,
+  // so windows sorted by the top 24 bits reach the table in runs of 2^(tab_bits - 24) slots
+  // (the order within a run does not matter): 3 radix passes instead of 8
+  const int SQ_BITS = 24;
   HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, Q.key2.p, Q.key.p, Q.wid2.p, Q.wid.p,
-                                          (int)std::min<uint64_t>(maxrun, RUN), 0, 64, s));
+                                          (int)std::min<uint64_t>(maxrun, RUN), 64 - SQ_BITS, 64, s));
   std::vector<uint32_t> ublk;
   for (auto &R : Q.runs) {
     R.ub0 = ublk.size();
@@ -1372,7 +1376,7 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
     HIPC(hipGetLastError());
     size_t tb = tmpb;
     HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
-                                            Q.wid.p + R.e0, (int)R.n, 0, 64, s));
+                                            Q.wid.p + R.e0, (int)R.n, 64 - SQ_BITS, 64, s));
   }
   HIPC(hipStreamSynchronize(s));
   // the sort buffers go: only the sorted runs stay for the job
@@ -1598,11 +1602,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // exactly what a job without the longer reads would get.
   {
     uint32_t prev = 0;
-    // the shared-strand class (OVL_SHARED=0 turns it off): 4 blocks of 8 waves per CU within
+    // the shared-strand class (OVL_SHARED=1 turns it on): 4 blocks of 8 waves per CU within
     // 40 KB each (32 waves: the reads <= ~11 kb), or 3 within 52 KB (24 waves, <= ~15 kb)
     // when every read fits that and not the first; the -l kernel has its own order
     const char *she = getenv("OVL_SHARED");
-    if (!ordered && !(she && atoi(she) == 0)) {
+    if (!ordered && she && atoi(she) != 0) {
       auto longest_sh = [&](size_t cap) -> uint32_t {
         uint32_t L = 0;
         for (uint32_t x : c->h_len)
@@ -2108,7 +2112,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         if (d_probe.grow(R.n)) return fail(OVL_ERR_OOM, "probe records (%llu)", (unsigned long long)R.n);
         HIPC(hipEventRecord(c->ev[2], s));
         HIPC(hipMemsetAsync(d_probe.p, 0, 8ull * wlim, s));
-        HIPC(hipMemsetAsync(Q.uhits.p + R.u0, 0, 4ull * (ue - R.u0), s));
         HIPC(hipMemsetAsync(Q.uflags.p + R.u0, 0, 4ull * (ue - R.u0), s));
         SqProbeArgs SA;
         SA.X = index_dev(c);
@@ -2122,10 +2125,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         SA.ublk = Q.ublk.p + R.ub0;
         SA.k = k;
         SA.out = d_probe.p;
-        SA.unit_hits = Q.uhits.p + R.u0;
         SA.unit_flags = Q.uflags.p + R.u0;
         hipLaunchKernelGGL(k_probe_sorted, dim3(8 * c->n_cu), dim3(256), 0, s, SA);
         n_probe_launch++;
+        hipLaunchKernelGGL(k_sq_unit_hits, dim3((ue - R.u0 + 3) / 4), dim3(256), 0, s, d_probe.p,
+                           Q.dwbase.p + R.wb0, ue - R.u0, Q.uhits.p + R.u0);
         HIPC(hipGetLastError());
         HIPC(hipEventRecord(c->ev[3], s));
         sq_uh.resize(ue - R.u0);

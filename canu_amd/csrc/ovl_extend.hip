@@ -1981,27 +1981,35 @@ k_extend(ExtendArgs X) {
         const int32_t sl = (last + kk) % OVL_SH_SLOTS;
         unsigned long long c = 0;
         if (lane == 0) {
-          atomicAdd(&slots[sl].users, 1);
-          c = atomicAdd(&slots[sl].ctl, 1ull);
+          // counted before the pair is taken (seq_cst: the two are not reordered)
+          __hip_atomic_fetch_add(&slots[sl].users, 1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+          c = __hip_atomic_fetch_add(&slots[sl].ctl, 1ull, __ATOMIC_SEQ_CST,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         const uint32_t idx = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)c);
         const uint32_t end = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(c >> 32));
         if (idx < end) { slot = sl; li = idx; break; }
-        if (lane == 0) atomicSub(&slots[sl].users, 1);
+        if (lane == 0)
+          __hip_atomic_fetch_add(&slots[sl].users, -1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (slot < 0) {
         // none: reload a slot whose pairs are all taken and that no wave uses
         bool loaded = false, finished = false;
         for (int32_t sl = 0; sl < OVL_SH_SLOTS && !loaded && !finished; sl++) {
+          // claim the slot first, then check it: only the claimant may publish a new group,
+          // so once claimed an exhausted ctl stays exhausted, and a zero user count then
+          // means no wave holds one of its pairs (a holder counts itself before it takes
+          // a pair).  Checking before claiming raced with another loader's publish.
           int32_t claim = 0;
           if (lane == 0) {
-            const unsigned long long c = __hip_atomic_load(&slots[sl].ctl, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int32_t us = __hip_atomic_load(&slots[sl].users, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if ((uint32_t)c >= (uint32_t)(c >> 32) && us == 0 &&
-                atomicCAS(&slots[sl].loading, 0, 1) == 0)
-              claim = 1;
+            if (atomicCAS(&slots[sl].loading, 0, 1) == 0) {
+              const unsigned long long c = __hip_atomic_load(&slots[sl].ctl, __ATOMIC_SEQ_CST,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+              const int32_t us = __hip_atomic_load(&slots[sl].users, __ATOMIC_SEQ_CST,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+              if ((uint32_t)c >= (uint32_t)(c >> 32) && us == 0) claim = 1;
+              else atomicExch(&slots[sl].loading, 0);
+            }
           }
           claim = __builtin_amdgcn_readfirstlane(claim);
           if (!claim) continue;
@@ -2055,7 +2063,8 @@ k_extend(ExtendArgs X) {
       }
       if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
       lds_sync();
-      if (lane == 0) atomicSub(&slots[slot].users, 1);
+      if (lane == 0)      // release: every read of the slot's strand is done
+        __hip_atomic_fetch_add(&slots[slot].users, -1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   } else if constexpr (ORD) {
     static_assert(!STAGE, "the -l kernel is the generic one");

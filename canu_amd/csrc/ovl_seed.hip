@@ -229,7 +229,7 @@ struct SqProbeArgs {
   const uint32_t *ublk;         // per 512 windows: the unit holding the block's first window
   uint32_t k;
   Probe *out;                   // run-local window id -> its record (zeroed up to wlim)
-  uint32_t *unit_hits, *unit_flags;   // per run unit (zeroed)
+  uint32_t *unit_flags;         // per run unit (zeroed)
 };
 
 __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
@@ -265,9 +265,21 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
       pr.off = t.off;
       pr.cnt = c & OVL_CNT_MASK;
       A.out[w] = pr;
-      atomicAdd(&A.unit_hits[u], pr.cnt);
     }
   }
+}
+
+// the units' hit counts (k_probe's unit_hits) from the records: one wave per unit, its
+// windows' records read once (a random atomic per hit would cost more)
+__global__ void __launch_bounds__(256) k_sq_unit_hits(const Probe *rec, const uint64_t *wbase,
+                                                      uint32_t nunits, uint32_t *unit_hits) {
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t u = blockIdx.x * 4 + wave;
+  if (u >= nunits) return;
+  uint32_t h = 0;
+  for (uint64_t w = wbase[u] + lane; w < wbase[u + 1]; w += 64) h += rec[w].cnt;
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  if (lane == 0) unit_hits[u] = h;
 }
 
 // ---------------------------------------------------------------------------------------
