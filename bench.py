@@ -456,8 +456,48 @@ class Configs4Rank(Configs2):
                 "dist_backend": backend if world > 1 else None}
 
     def parity(self, st, reduce, SUM, torch):
-        return {"checked": False, "reason": "no reference digest at this size; the rank-job "
-                "union and oic_ref parity are tests/test_configs4.py (-m gpu)"}
+        """Each rank's job vs the reference's digest of the same plan job
+        (tests/golden/c4rank<reads/1000>k.json, tools/make_c4_digest.py), when one was made
+        for this read set; the 1/8-scale default has none (the reference would take hours)."""
+        from canu_amd import digest
+        a = self.args
+        path = os.path.join(ROOT, "tests", "golden", f"c4rank{a.reads // 1000}k.json")
+        g = None
+        try:
+            with open(path) as f:
+                g = json.load(f)
+        except (OSError, ValueError):
+            pass
+        mine = self.workload_key()
+        same = g is not None and all(
+            np.isclose(float(g["workload"][k]), float(mine[k])) for k in
+            ("reads", "read_len", "coverage", "read_error", "seed", "k", "maxerate",
+             "minlength"))
+        gj = None
+        if same:
+            for j in g["jobs"]:
+                if tuple(j["h"]) == tuple(self.job["h"]) and tuple(j["r"]) == tuple(self.job["r"]):
+                    gj = j
+        # every rank must agree on whether the check runs (the reduces below are collective)
+        have = int(reduce(1 if gj is not None else 0, SUM, torch.int64))
+        if have != self.world:
+            return {"checked": False, "reason": "no reference digest for this plan job "
+                    "(tools/make_c4_digest.py pins the 20k-read plan; the rank-job union and "
+                    "oic_ref parity are tests/test_configs4.py, -m gpu)"}
+        t0 = time.time()
+        rec = self.oic.fetch()
+        names = {"kmer_hits_without_olap": "kmer_hits_without_olap",
+                 "kmer_hits_with_olap": "kmer_hits_with_olap", "multi_overlaps": "multi",
+                 "total_overlaps": "total", "contained_overlaps": "contained",
+                 "dovetail_overlaps": "dovetail"}
+        ok = (rec.shape[0] == gj["records"] and
+              digest.sha256_sorted(rec) == gj["sha256_sorted"] and
+              f"{digest.multiset_hash(rec):016x}" == gj["multiset_hash"] and
+              all(int(st[m]) == int(gj["stats"][r]) for m, r in names.items()))
+        n_ok = int(reduce(1 if ok else 0, SUM, torch.int64))
+        return {"checked": True, "ok": n_ok == self.world, "jobs_ok": n_ok,
+                "records": int(reduce(int(rec.shape[0]), SUM, torch.int64)),
+                "golden": os.path.relpath(path, ROOT), "check_s": round(time.time() - t0, 2)}
 
     def seed_only(self):
         return None
