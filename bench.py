@@ -621,7 +621,16 @@ def rooflines(args, job, st, world):
                          "source": "live: ovl_probe_ceiling over this run's index table"})
             if g > 0 and wps / 1e9 > g:
                 ceil["note"] = ("the probe beats uniform random loads here: its lookups are not "
-                                "uniform over the table (repeated k-mers hit cached lines)")
+                                "uniform over the table (repeated k-mers hit cached lines); "
+                                "the replay below is the ceiling for its own lookups")
+            # the probe's own lookup stream (the job's query windows, first 2^28) replayed as
+            # pure loads over the same table (ovl_probe_replay): the rate the memory system
+            # gives these exact lookups, so frac_of_replay is the probe's overhead over them
+            if getattr(job, "q_lo", None) is not None:
+                gr, nw = job.oic.probe_replay(job.q_lo, job.q_hi)
+                ceil.update({"replay_gloads_per_s": round(gr, 2), "replay_windows": int(nw),
+                             "frac_of_replay": round(wps / 1e9 / gr, 3) if gr > 0 else None,
+                             "replay_source": "live: ovl_probe_replay, the probe's own slots"})
         except Exception as e:        # a side figure: never lose the bench line to it
             ceil["error"] = f"{type(e).__name__}: {e}"[:200]
         probe_roof["random_lookup_ceiling"] = ceil

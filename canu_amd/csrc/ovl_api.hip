@@ -313,6 +313,47 @@ __global__ void __launch_bounds__(256) k_rand_lookup(const uint4 *t, uint64_t ma
   if (acc == 0x9E3779B9u) sink[0] = acc;       // keeps the loads live; (almost) never taken
 }
 
+// ovl_probe_replay: the table slot of every query window (k_probe's window rule and hash),
+// written as a 32-bit slot list (0xFFFFFFFF: no k-mer), one wave per unit
+__global__ void __launch_bounds__(256) k_slot_list(ReadsDev R, const Unit *units,
+                                                   const uint64_t *wbase, uint32_t nunits,
+                                                   uint32_t k, uint64_t kmask, uint32_t tab_bits,
+                                                   uint32_t *slot) {
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t u = blockIdx.x * 4 + wave;
+  if (u >= nunits) return;
+  const Unit un = units[u];
+  const Strand S = un.dir ? strand_rc(R, un.r) : strand_fwd(R, un.r);
+  const uint32_t *bad = un.dir ? S.ex_nul : S.ex_wild;
+  const uint32_t nw = (uint32_t)(wbase[u + 1] - wbase[u]);
+  const uint32_t kbits = (1u << k) - 1u;
+  for (uint32_t o = lane; o < nw; o += 64) {
+    bool ok = (int32_t)(o + k) <= S.len;
+    if (ok && bad) ok = (mask_at(bad, (int32_t)o) & kbits) == 0;
+    slot[wbase[u] + o] =
+        ok ? (uint32_t)(mix64(bases_at(S.w, (int32_t)o) & kmask) >> (64 - tab_bits)) : 0xFFFFFFFFu;
+  }
+}
+
+// the same lookups as pure loads: 8 slots per lane in flight, nothing else in the loop
+__global__ void __launch_bounds__(256) k_slot_replay(const uint4 *t, const uint32_t *slot,
+                                                     uint64_t n, uint32_t *sink) {
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i0 < n; i0 += 8 * stride) {
+    uint4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint64_t i = i0 + q * stride;
+      const uint32_t sl = i < n ? slot[i] : 0xFFFFFFFFu;
+      v[q] = sl != 0xFFFFFFFFu ? t[sl] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) acc ^= v[q].x ^ v[q].w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" {
 
 int ovl_abi_version(void) { return OVL_ABI_VERSION; }
@@ -367,6 +408,61 @@ int ovl_probe_ceiling(ovl_ctx *c, double *gloads_per_s, uint64_t *table_bytes) {
   return OVL_OK;
 }
 
+int ovl_probe_replay(ovl_ctx *c, uint32_t bgn, uint32_t end, double *gloads_per_s,
+                     uint64_t *n_windows) {
+  if (!c || !gloads_per_s || !n_windows) return fail(OVL_ERR_STATE, "null argument");
+  if (!c->have_index || !c->d_tab.p) return fail(OVL_ERR_STATE, "no index table");
+  if (c->tab_bits > 32) return fail(OVL_ERR_UNSUPPORTED, "table of 2^%u slots", c->tab_bits);
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (bgn < c->first_iid) bgn = c->first_iid;
+  const uint32_t last = c->first_iid + c->nreads - 1;
+  if (end > last) end = last;
+  // the query units of find_impl's rule (both orientations, --minlength, k), up to 2^28
+  // windows: a sample of the same lookup stream k_probe runs over these reads
+  std::vector<Unit> units;
+  std::vector<uint64_t> wb(1, 0);
+  const uint32_t k = c->P.kmer_len;
+  for (uint32_t a = bgn; a <= end && a >= bgn && wb.back() < (1ull << 28); a++) {
+    const uint32_t r = a - c->first_iid;
+    const int32_t L = (int32_t)c->h_len[r];
+    if (L < c->P.min_olap_len || L < (int32_t)k) continue;
+    for (uint32_t dir = 0; dir < 2; dir++) {
+      units.push_back(Unit{r, dir});
+      wb.push_back(wb.back() + (uint64_t)(L - (int32_t)k + 1));
+    }
+  }
+  const uint64_t n = wb.back();
+  *n_windows = n;
+  *gloads_per_s = 0.0;
+  if (n == 0) return OVL_OK;
+  DBuf<uint32_t> slot, sink;
+  DBuf<Unit> du;
+  DBuf<uint64_t> dwb;
+  if (slot.alloc(n) || sink.alloc(1) || du.alloc(units.size()) || dwb.alloc(wb.size()))
+    return fail(OVL_ERR_OOM, "probe replay (%llu windows)", (unsigned long long)n);
+  HIPC(hipMemcpyAsync(du.p, units.data(), sizeof(Unit) * units.size(), hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(dwb.p, wb.data(), 8ull * wb.size(), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_slot_list, dim3(((uint32_t)units.size() + 3) / 4), dim3(256), 0, s,
+                     c->reads(), du.p, dwb.p, (uint32_t)units.size(), k,
+                     (1ull << (2 * k)) - 1, c->tab_bits, slot.p);
+  const uint32_t blocks = 8u * (uint32_t)c->n_cu;
+  hipLaunchKernelGGL(k_slot_replay, dim3(blocks), dim3(256), 0, s, (const uint4 *)c->d_tab.p,
+                     slot.p, n, sink.p);                                       // warm
+  HIPC(hipEventRecord(c->ev[6], s));
+  const int reps = 3;
+  for (int r = 0; r < reps; r++)
+    hipLaunchKernelGGL(k_slot_replay, dim3(blocks), dim3(256), 0, s, (const uint4 *)c->d_tab.p,
+                       slot.p, n, sink.p);
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(c->ev[7], s));
+  HIPC(hipEventSynchronize(c->ev[7]));
+  float ms = 0;
+  HIPC(hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
+  *gloads_per_s = ms > 0 ? (double)reps * (double)n / (ms * 1e-3) / 1e9 : 0.0;
+  return OVL_OK;
+}
+
 int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
   *out = nullptr;
   if (p->kmer_len == 0) return fail(OVL_ERR_BAD_PARAM, "kmer length (-k) needed");
@@ -407,6 +503,9 @@ int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
     c->h_error_bound[i] = (int32_t)ceil(i * er);
   std::vector<int32_t> ml;
   init_match_limit(ml, er, c->max_errors);
+  // padded past max_errors: the staged kernel may read its rows' limits straight from here
+  // (OVL_GML), where a block's LDS copy held 0x7fffffff beyond max_errors
+  ml.resize(ml.size() + 64, 0x7fffffff);
   if (c->d_error_bound.alloc(AS_MAX_READLEN + 1) != hipSuccess ||
       c->d_match_limit.alloc(ml.size()) != hipSuccess) {
     ovl_ctx_destroy(c);
@@ -1506,10 +1605,12 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     return c->h_error_bound[std::min<uint64_t>(L, AS_MAX_READLEN)] + 2;
   };
   auto sw_of = [](uint64_t L) { return (int32_t)(((L + 31) / 32 + 2) & ~1ull); };
-  auto stg_lds_of = [&](uint64_t L) { return 4ull * (4ull * (uint64_t)sw_of(L) + OVL_SCR); };
+  auto stg_lds_of = [&](uint64_t L) { return 4ull * (4ull * (uint64_t)sw_of(L) + OVL_SCR_STAGE); };
   auto ml_of = [](int32_t ec) { return 4ull * (((uint64_t)(ec + 2) + 3) & ~3ull); };
+  // the staged kernel's block-shared Edit_Match_Limit table (none with OVL_GML)
+  auto sml_of = [&](int32_t ec) { return OVL_GML ? 0ull : ml_of(ec); };
   auto fits = [&](uint64_t L, uint32_t wpb, size_t cap) {
-    return stg_lds_of(L) * wpb + ml_of(ecap_of(L)) <= cap;
+    return stg_lds_of(L) * wpb + sml_of(ecap_of(L)) <= cap;
   };
   // the shared-strand block: Edit_Match_Limit table, slot control, OVL_SH_SLOTS query
   // strands, then per wave its target strand and scratch (k_extend<.., SH>)
@@ -1563,9 +1664,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       g.lds = sh_lds_of(L, g.wpb);
       if (g.lds > cap) return -1;
     } else {
-      g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, ml_of(g.ecap))) / stg_lds_of(L));
+      g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, sml_of(g.ecap))) / stg_lds_of(L));
       if (g.wpb < 1) return -1;
-      g.lds = stg_lds_of(L) * g.wpb + ml_of(g.ecap);
+      g.lds = stg_lds_of(L) * g.wpb + sml_of(g.ecap);
     }
     // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the LDS so that at most that many blocks
     // fit on a CU (occupancy studies); unset = natural occupancy
@@ -2143,6 +2244,62 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         // record written for every searched window (the zeroing and the hits)
         probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) + 8ull * wlim;
         Q.probed = (int)sq_run;
+        if (getenv("OVL_SQ_CHECK")) {
+          // debugging: the random-lookup probe of the same windows, compared record by record
+          const uint32_t ncu = ue - R.u0;
+          DBuf<Probe> ref;
+          DBuf<uint32_t> rh, rf;
+          if (ref.alloc(std::max<uint64_t>(wlim, 1)) || rh.alloc(ncu) || rf.alloc(ncu))
+            return fail(OVL_ERR_OOM, "sq check");
+          HIPC(hipMemsetAsync(ref.p, 0, 8ull * wlim, s));
+          ProbeArgs PA;
+          PA.R = c->reads();
+          PA.X = index_dev(c);
+          PA.units = Q.dunits.p + R.u0;
+          PA.rbase = Q.dwbase.p + R.wb0;
+          PA.nunits = ncu;
+          PA.out = ref.p;
+          PA.unit_hits = rh.p;
+          PA.unit_flags = rf.p;
+          PA.k = k;
+          hipLaunchKernelGGL(k_probe<false>, dim3((ncu + 3) / 4), dim3(256), 0, s, PA);
+          HIPC(hipGetLastError());
+          std::vector<Probe> a(wlim), b(wlim);
+          std::vector<uint32_t> hf(ncu), sf(ncu), hh(ncu);
+          HIPC(hipMemcpyAsync(a.data(), d_probe.p, 8ull * wlim, hipMemcpyDeviceToHost, s));
+          HIPC(hipMemcpyAsync(b.data(), ref.p, 8ull * wlim, hipMemcpyDeviceToHost, s));
+          HIPC(hipMemcpyAsync(hf.data(), rf.p, 4ull * ncu, hipMemcpyDeviceToHost, s));
+          HIPC(hipMemcpyAsync(sf.data(), Q.uflags.p + R.u0, 4ull * ncu, hipMemcpyDeviceToHost, s));
+          HIPC(hipMemcpyAsync(hh.data(), rh.p, 4ull * ncu, hipMemcpyDeviceToHost, s));
+          HIPC(hipStreamSynchronize(s));
+          uint64_t bad = 0, ha = 0, hb = 0, fbad = 0, hbad = 0;
+          for (uint64_t w = 0; w < wlim; w++) {
+            ha += a[w].cnt;
+            hb += b[w].cnt;
+            if (a[w].off != b[w].off || a[w].cnt != b[w].cnt) {
+              if (bad < 5) {
+                uint32_t u = 0;
+                while (Q.wb[R.wb0 + u + 1] <= w) u++;
+                fprintf(stderr, "OVL_SQ_CHECK window %llu (unit %u read %u dir %u o %llu): "
+                        "sorted {%u,%u} random {%u,%u}\n", (unsigned long long)w, u,
+                        Q.units[R.u0 + u].r, Q.units[R.u0 + u].dir,
+                        (unsigned long long)(w - Q.wb[R.wb0 + u]), a[w].off, a[w].cnt,
+                        b[w].off, b[w].cnt);
+              }
+              bad++;
+            }
+          }
+          for (uint32_t u = 0; u < ncu; u++) {
+            fbad += (hf[u] != sf[u]);
+            hbad += (hh[u] != sq_uh[u]);
+          }
+          fprintf(stderr, "OVL_SQ_CHECK run %zu: %u units, %llu windows (of %llu), tab_bits %u "
+                  "slice_bits %u: %llu records differ, hits sorted %llu random %llu, flags "
+                  "differ %llu, unit hits differ %llu\n", sq_run, ncu,
+                  (unsigned long long)wlim, (unsigned long long)R.n, c->tab_bits,
+                  c->slice_bits, (unsigned long long)bad, (unsigned long long)ha,
+                  (unsigned long long)hb, (unsigned long long)fbad, (unsigned long long)hbad);
+        }
       }
       nb = ue - u0;
       rbase.assign(Q.wb.begin() + R.wb0 + (u0 - R.u0), Q.wb.begin() + R.wb0 + (ue - R.u0) + 1);

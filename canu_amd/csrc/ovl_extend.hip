@@ -103,6 +103,23 @@ __device__ __forceinline__ void wave_argmax(int32_t &v, int32_t &d) {
   }
 }
 
+// OVL_GML: the staged kernel reads Edit_Match_Limit from global memory through the constant
+// address space (one scalar load per row, scalar-cache resident) instead of a block-shared LDS
+// copy; with OVL_SCR_STAGE = 0 its waves hold no LDS scratch either (the removal pass keeps
+// its thresholds in the wave's global scratch), so a 10 kb pair's wave needs only its two
+// strands in LDS -- 32 waves per CU at 8 waves per SIMD (OVL_EXT_OCC = 8)
+#ifndef OVL_GML
+#define OVL_GML 0
+#endif
+#ifndef OVL_SCR_STAGE
+#define OVL_SCR_STAGE 256
+#endif
+#if OVL_GML
+typedef const __attribute__((address_space(4))) int32_t ml_t;
+#else
+typedef const __attribute__((address_space(3))) int32_t ml_t;
+#endif
+
 struct WaveMem {
   int32_t *rows;      // global: band-compact log of every row (read by the traceback)
   int32_t *rowdir;    // global: (offset, lo) per row
@@ -112,6 +129,7 @@ struct WaveMem {
   lds_i32 *ldc;       // LDS: Left_Delta cache for Lies_On_Alignment
   int32_t  ldcap;
   const lds_i32 *mlim;  // LDS: Edit_Match_Limit[0 .. e_cap+1], shared by the block
+  ml_t    *rmlim;       // the register kernel's Edit_Match_Limit (LDS copy, or global: OVL_GML)
 };
 
 __device__ __forceinline__ void lds_sync() {
@@ -688,7 +706,7 @@ template <int DIR, typename SS, bool L16, int RJ = OVL_RJ>
 __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     const ExtendArgs &X, int32_t e_cap, int32_t partial_i, int32_t mbed, double bmv_in,
     double mbts, const lds_u64 *aw, int32_t a0, int32_t m, const lds_u64 *tw, int32_t t0,
-    int32_t n, int32_t limit, int32_t *rows, const lds_i32 *mlim, int32_t *dst,
+    int32_t n, int32_t limit, int32_t *rows, ml_t *mlim, int32_t *dst,
     uint32_t lane) {
   SS A, T;
   A.w = aw; A.len = 0;
@@ -1228,7 +1246,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     if constexpr (FAST)
       po = wave_ped_reg<1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
                                         X.branch_match_value, X.min_branch_tail_slope, A.w, a0,
-                                        am, B.w, b0, bn, error_limit, WM.rows, WM.mlim, stk,
+                                        am, B.w, b0, bn, error_limit, WM.rows, WM.rmlim, stk,
                                         lane);
     else
       po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
@@ -1275,7 +1293,7 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     if constexpr (FAST)
       po = wave_ped_reg<-1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
                                          X.branch_match_value, X.min_branch_tail_slope, A.w,
-                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.mlim, LD,
+                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.rmlim, LD,
                                          lane);
     else
       po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
@@ -1700,11 +1718,12 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     typedef typename std::conditional<T16, __attribute__((address_space(3))) int16_t,
                                       lds_i32>::type lds_t;
     constexpr int32_t per = T16 ? 1 : 2;               // ints per (thr, diag) pair
-    if (on_aln && per * (ld_len + 1) <= WM.ldcap) {
-      // Lies_On_Alignment (:307) by binary search: walking the deltas, delta i is reached
-      // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
-      // and compares with diag_i (or with the final diag).  thr is non-decreasing.
-      lds_t *thr = (lds_t *)WM.ldc, *dgl = thr + ld_len + 1;
+    // Lies_On_Alignment (:307) by binary search: walking the deltas, delta i is reached
+    // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
+    // and compares with diag_i (or with the final diag).  thr is non-decreasing.  The
+    // thresholds live in the wave's LDS scratch, or (OVL_SCR_STAGE = 0) in the spare slot of
+    // its global delta scratch.
+    auto by_search = [&](auto *thr, auto *dgl, auto sync) {
       int32_t cs = S_Lo, cd = T_Lo - S_Lo;
       for (int32_t i0 = 0; i0 < ld_len; i0 += 64) {
         const int32_t i = i0 + (int32_t)lane;
@@ -1722,7 +1741,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
         cd += __builtin_amdgcn_readlane(sd, 63);
       }
       if (lane == 0) { thr[ld_len] = T16 ? 32767 : 0x7fffffff; dgl[ld_len] = cd; }
-      lds_sync();
+      sync();
       for (int32_t i = lane; i < nn; i += 64) {
         Node nd = nodes[i];
         if (nd.Len < 0) continue;
@@ -1740,7 +1759,16 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
         }
         if (rm) { nodes[i].Len = ~nd.Len; removed++; }
       }
-      lds_sync();
+      sync();
+    };
+    typedef typename std::conditional<T16, __attribute__((address_space(1))) int16_t,
+                                      __attribute__((address_space(1))) int32_t>::type g_t;
+    if (on_aln && per * (ld_len + 1) <= WM.ldcap) {
+      lds_t *thr = (lds_t *)WM.ldc;
+      by_search(thr, thr + ld_len + 1, [] { lds_sync(); });
+    } else if (FAST && OVL_SCR_STAGE == 0 && on_aln && per * (ld_len + 1) <= X.e_cap + 8) {
+      g_t *thr = (g_t *)(LD + (X.e_cap + 8));
+      by_search(thr, thr + ld_len + 1, [] { vm_sync(); });
     } else {
       const int32_t *ldp = LD;
       if (ld_len <= WM.ldcap) {
@@ -1859,8 +1887,9 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
   return L;
 }
 
-#define OVL_SCR 256              // staged kernel: per-wave LDS scratch ints (Lies_On_Alignment
-                                 // thresholds, Left_Delta cache)
+#define OVL_SCR 256              // shared-strand kernel: per-wave LDS scratch ints
+                                 // (Lies_On_Alignment thresholds, Left_Delta cache)
+// OVL_SCR_STAGE: the staged kernel's per-wave LDS scratch ints (defined with OVL_GML above)
 
 // STAGE = true: exception-free pairs, strands staged in LDS, rows in registers; pairs with
 // 'n' bases or a band wider than the register window are deferred to the generic kernel.
@@ -1903,8 +1932,9 @@ k_extend(ExtendArgs X) {
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
   constexpr bool GR = !STAGE && L16;
-  int32_t mlsz = GR ? 0 : ((X.e_cap + 2) + 3) & ~3;
-  if constexpr (!GR) {
+  constexpr bool NOML = GR || (STAGE && OVL_GML);   // no LDS Edit_Match_Limit table
+  int32_t mlsz = NOML ? 0 : ((X.e_cap + 2) + 3) & ~3;
+  if constexpr (!NOML) {
     for (int32_t i = threadIdx.x; i < X.e_cap + 2; i += blockDim.x)
       s_ext0[i] = (i <= X.max_errors) ? X.match_limit[i] : 0x7fffffff;
   }
@@ -1915,6 +1945,11 @@ k_extend(ExtendArgs X) {
   WM.rows = X.rows + (size_t)gw * X.rows_cap;
   WM.rowdir = X.rowdir + (size_t)gw * 4 * (X.e_cap + 2);
   WM.mlim = l_ext0;
+#if OVL_GML
+  WM.rmlim = (ml_t *)X.match_limit;           // padded past max_errors on the host
+#else
+  WM.rmlim = l_ext0;
+#endif
   lds_u64 *sw = nullptr, *tw = nullptr;
   ShSlot *slots = nullptr;
   lds_u64 *sstr = nullptr;
@@ -1941,7 +1976,7 @@ k_extend(ExtendArgs X) {
     __syncthreads();
   } else if constexpr (STAGE) {
     // per wave: [S words | T words] (u64) then the scratch
-    uint32_t wave_ints = 4 * (uint32_t)X.sw_words + OVL_SCR;
+    uint32_t wave_ints = 4 * (uint32_t)X.sw_words + OVL_SCR_STAGE;
     lds_i32 *wlds = s_ext + wave * wave_ints;
     sw = (lds_u64 *)wlds;
     tw = sw + X.sw_words;
@@ -1949,7 +1984,7 @@ k_extend(ExtendArgs X) {
     WM.wcap = 0;
     WM.tbw = wlds + 4 * X.sw_words;
     WM.ldc = WM.tbw;
-    WM.ldcap = OVL_SCR;
+    WM.ldcap = OVL_SCR_STAGE;
   } else {
     // per wave: row buffers (not with GR), traceback window, delta cache
     int32_t wcap = GR ? 0 : 2 * X.e_cap + 8;

@@ -504,27 +504,6 @@ __device__ __forceinline__ uint32_t thash(uint32_t t) {
   return t >> 25;                 // 7 bits -> 0..127
 }
 
-// Replay the occurrences of target s.t found in window j's staged segment [lo0, hi0).
-__device__ __forceinline__ void replay_window(SlotState &s, const uint64_t *hb, uint32_t lo0,
-                                              uint32_t hi0, int32_t o_j, int32_t k,
-                                              WaveAlloc &W, const ChainArgs &A,
-                                              uint32_t lane) {
-  if (s.t == 0) return;
-  uint32_t lo = lo0, hi = hi0;           // entries are iid-descending: first iid <= t
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if ((uint32_t)(hb[mid] >> 32) > s.t) lo = mid + 1; else hi = mid;
-  }
-  while (lo < hi0 && (uint32_t)(hb[lo] >> 32) == s.t) {
-    int32_t pp = (int32_t)(uint32_t)hb[lo];
-    s.diag_ct++;                                        // Add_Ref (:203-206)
-    if (s.diag_bgn > o_j) s.diag_bgn = o_j;
-    if (s.diag_end < o_j) s.diag_end = o_j;
-    add_match(s, pp, o_j, k, A.pool, W, A, lane);
-    lo++;
-  }
-}
-
 // Walk the slot's list and store it in list order; write its PairRec.
 __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32_t uflags,
                                           const ChainArgs &A, uint32_t lane) {
@@ -583,10 +562,13 @@ __device__ __forceinline__ void emit_slot(const SlotState &s, uint32_t u, uint32
   } while (0)
 
 __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
-  __shared__ uint64_t s_hb[4][OVL_HCAP];
-  __shared__ uint8_t  s_hw[4][OVL_HCAP];      // window (0..63) of each staged occurrence
+  // a staged occurrence is its target iid (s_ht) and its payload (s_hp: window << 21 |
+  // offset in the target, which is < 2^21, AS_MAX_READLEN); the scatter copies payloads into
+  // per-target lists (s_sv), so the replay reads one independent LDS word per occurrence
+  __shared__ uint32_t s_ht[4][OVL_HCAP];
+  __shared__ uint32_t s_hp[4][OVL_HCAP];
   __shared__ uint8_t  s_hs[4][OVL_HCAP];      // its target slot (0..127), 0xFF: none
-  __shared__ uint16_t s_sx[4][OVL_HCAP];      // staged indices sorted by (slot, order)
+  __shared__ uint32_t s_sv[4][OVL_HCAP];      // payloads sorted by (slot, staged order)
   __shared__ uint32_t s_cnt[4][2 * OVL_MAXT]; // per slot: base, running count
   __shared__ uint32_t s_seg[4][65];
   __shared__ uint32_t s_off[4][64];
@@ -595,10 +577,10 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   __shared__ uint64_t s_lmask[4][OVL_MAXT];   // stable scatter: lanes of each slot
   __shared__ uint32_t s_over[4];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint64_t *hb = s_hb[wave];
-  uint8_t *hw = s_hw[wave];
+  uint32_t *ht = s_ht[wave];
+  uint32_t *hp = s_hp[wave];
   uint8_t *hs = s_hs[wave];
-  uint16_t *sx = s_sx[wave];
+  uint32_t *sv = s_sv[wave];
   uint32_t *cnt = s_cnt[wave];
   uint32_t *seg = s_seg[wave];
   uint32_t *soff = s_off[wave];
@@ -668,15 +650,16 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
               uint32_t mid = (lo + hi) >> 1;
               if (seg[mid] <= idx) lo = mid; else hi = mid;
             }
-            hb[idx - p0] = A.occ[soff[lo] + (idx - seg[lo])];
-            hw[idx - p0] = (uint8_t)lo;
+            const uint64_t oc = A.occ[soff[lo] + (idx - seg[lo])];
+            ht[idx - p0] = (uint32_t)(oc >> 32);
+            hp[idx - p0] = (lo << 21) | (uint32_t)oc;
           }
           for (uint32_t i = lane; i < 2 * OVL_MAXT; i += 64) cnt[i] = 0;
           WAVE_SYNC();
           // discover targets (LDS open-addressing set, 128 slots); remember each staged
           // occurrence's slot and count occurrences per slot
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
-            uint32_t t = (uint32_t)(hb[idx - p0] >> 32);
+            uint32_t t = ht[idx - p0];
             uint8_t slot = 0xFF;
             if (t > a_iid) {                     // Find_Overlaps.C:328
               if (pass == 0 && first_launch) nhits++;
@@ -729,7 +712,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             if (has) {
               mk = lmask[slot];
               uint32_t rank = __builtin_popcountll(mk & ((1ull << lane) - 1));
-              sx[cnt[slot] + cnt[OVL_MAXT + slot] + rank] = (uint16_t)(idx - p0);
+              sv[cnt[slot] + cnt[OVL_MAXT + slot] + rank] = hp[idx - p0];
             }
             WAVE_SYNC();
             if (has && lane == (uint32_t)__builtin_ctzll(mk)) {   // the slot's first lane
@@ -742,29 +725,25 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
           if (t0 != s0.t) { slot_reset(s0); s0.t = t0; }
           if (t1 != s1.t) { slot_reset(s1); s1.t = t1; }
-          // replay Add_Ref / Add_Match per target over its own occurrences, in order
+          // replay Add_Ref / Add_Match per target over its own occurrences, in order; the
+          // next payload is loaded before the current one is applied (no LDS round trip on
+          // the loop's dependency chain)
           {
-            uint32_t b = cnt[lane], n = cnt[OVL_MAXT + lane];
-            for (uint32_t i = 0; i < n; i++) {
-              uint32_t x = sx[b + i];
-              int32_t pp = (int32_t)(uint32_t)hb[x];
-              int32_t o_j = (int32_t)(base + hw[x]);
-              s0.diag_ct++;                                   // Add_Ref (:203-206)
-              if (s0.diag_bgn > o_j) s0.diag_bgn = o_j;
-              if (s0.diag_end < o_j) s0.diag_end = o_j;
-              add_match(s0, pp, o_j, k, A.pool, W, A, lane);
-            }
-            b = cnt[lane + 64];
-            n = cnt[OVL_MAXT + lane + 64];
-            for (uint32_t i = 0; i < n; i++) {
-              uint32_t x = sx[b + i];
-              int32_t pp = (int32_t)(uint32_t)hb[x];
-              int32_t o_j = (int32_t)(base + hw[x]);
-              s1.diag_ct++;
-              if (s1.diag_bgn > o_j) s1.diag_bgn = o_j;
-              if (s1.diag_end < o_j) s1.diag_end = o_j;
-              add_match(s1, pp, o_j, k, A.pool, W, A, lane);
-            }
+            auto replay = [&](SlotState &ss, uint32_t b, uint32_t n) {
+              uint32_t v = n ? sv[b] : 0u;
+              for (uint32_t i = 0; i < n; i++) {
+                const uint32_t cur = v;
+                if (i + 1 < n) v = sv[b + i + 1];
+                const int32_t pp = (int32_t)(cur & 0x1FFFFFu);
+                const int32_t o_j = (int32_t)(base + (cur >> 21));
+                ss.diag_ct++;                                 // Add_Ref (:203-206)
+                if (ss.diag_bgn > o_j) ss.diag_bgn = o_j;
+                if (ss.diag_end < o_j) ss.diag_end = o_j;
+                add_match(ss, pp, o_j, k, A.pool, W, A, lane);
+              }
+            };
+            replay(s0, cnt[lane], cnt[OVL_MAXT + lane]);
+            replay(s1, cnt[lane + 64], cnt[OVL_MAXT + lane + 64]);
           }
           WAVE_SYNC();
         }

@@ -86,12 +86,12 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
            "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream", "ovl_write_ovb",
            "ovl_ctx_write_ovb", "ovl_ctx_write_stats", "ovl_set_read_libraries",
            "ovl_hash_limits_init", "ovl_build_hash_batch", "ovl_driver_params_init",
-           "ovl_overlap_driver", "ovl_seed_hits", "ovl_probe_ceiling"]
+           "ovl_overlap_driver", "ovl_seed_hits", "ovl_probe_ceiling", "ovl_probe_replay"]
 
 _lib = None
 
 
-ABI_VERSION = 4          # OVL_ABI_VERSION of include/canu_ovl.h
+ABI_VERSION = 5          # OVL_ABI_VERSION of include/canu_ovl.h
 
 
 def load_library(path: str | None = None):
@@ -127,6 +127,8 @@ def load_library(path: str | None = None):
                                        P(ctypes.c_uint64)]
     lib.ovl_get_stats.argtypes = [ctypes.c_void_p, P(_Stats)]
     lib.ovl_probe_ceiling.argtypes = [ctypes.c_void_p, P(ctypes.c_double), P(ctypes.c_uint64)]
+    lib.ovl_probe_replay.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                     P(ctypes.c_double), P(ctypes.c_uint64)]
     lib.ovl_ctx_stream.argtypes = [ctypes.c_void_p]
     lib.ovl_ctx_stream.restype = ctypes.c_void_p
     lib.ovl_write_ovb.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
@@ -389,6 +391,14 @@ class OverlapInCore:
         g, b = ctypes.c_double(), ctypes.c_uint64()
         self._check(self.lib.ovl_probe_ceiling(self.ctx, ctypes.byref(g), ctypes.byref(b)))
         return g.value, b.value
+
+    def probe_replay(self, bgn: int, end: int) -> tuple[float, int]:
+        """(G loads/s, windows): the probe's own table lookups for the query windows of reads
+        bgn..end (first 2^28) replayed as pure loads (ovl_probe_replay)."""
+        g, n = ctypes.c_double(), ctypes.c_uint64()
+        self._check(self.lib.ovl_probe_replay(self.ctx, bgn, end, ctypes.byref(g),
+                                              ctypes.byref(n)))
+        return g.value, n.value
 
     def write_ovb(self, path: str) -> None:
         """overlapInCore's -o output: the last find's records as an .ovb + .counts."""

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 4
+#define OVL_ABI_VERSION 5
 
 typedef enum {
   OVL_OK               =  0,
@@ -264,6 +264,14 @@ void       *ovl_ctx_stream(ovl_ctx *ctx);
  * and the table's bytes -- the memory system's ceiling for one random lookup per window on
  * this device at this table size.  Reads the table only; needs an index. */
 int         ovl_probe_ceiling(ovl_ctx *ctx, double *gloads_per_s, uint64_t *table_bytes);
+
+/* Measurement only (ABI 5): the table lookups k_probe makes for the query windows of reads
+ * bgn..end (both orientations, the search's window rule; the first 2^28 windows), replayed
+ * as pure 16-B loads with nothing else in the loop, in G loads/s -- the memory system's rate
+ * for that exact lookup stream (the uniform ceiling above ignores that overlapping reads
+ * share k-mers, so the probe can beat it).  Reads the table only; needs an index. */
+int         ovl_probe_replay(ovl_ctx *ctx, uint32_t bgn, uint32_t end, double *gloads_per_s,
+                             uint64_t *n_windows);
 
 #ifdef __cplusplus
 }

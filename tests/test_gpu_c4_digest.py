@@ -7,9 +7,9 @@ the record count, SHA-256 of the sorted records, multiset hash and -s counters o
 reference overlapInCore (oracle/_ref/oic_ref) run with the same arguments
 (tools/make_c4_digest.py).  The digest is data, so this runs without the reference build.
 
-Every job runs here through the drop-in OverlapInCore.overlap_driver -- with the sorted query
-windows from the second batch on (the default) and, for the widest job, once more with the
-random-lookup probe only (OVL_SQ=0).
+Every job runs here through the drop-in OverlapInCore.overlap_driver (one hash batch each at
+this size, probed at random), and the last job -- searched by every read -- once more through
+the job's sorted query windows (OVL_SQ=1, k_probe_sorted).
 """
 import json
 import os
@@ -79,13 +79,11 @@ def test_gpu_c4_plan_jobs_match_reference_digest(monkeypatch):
                               w["read_error"], seed=w["seed"], len_jitter=0.2,
                               read_range=(0, n), workers=8)
     assert rs.total_bases() == w["total_bases"]
-    batches = []
     for gj in g["jobs"]:
         rec, st = _run_job(rs, gj, w)
         _check(rec, st, gj)
-        batches.append(st["hash_batches"])
-    assert max(batches) >= 2                  # the sorted query windows ran
-    widest = int(np.argmax(batches))
-    monkeypatch.setenv("OVL_SQ", "0")
-    rec, st = _run_job(rs, g["jobs"][widest], w)
-    _check(rec, st, g["jobs"][widest])
+    # the plan's jobs are one hash batch each at this size (the default probes at random
+    # then); the last job (searched by every read) once more through the sorted query windows
+    monkeypatch.setenv("OVL_SQ", "1")
+    rec, st = _run_job(rs, g["jobs"][-1], w)
+    _check(rec, st, g["jobs"][-1])

@@ -31,7 +31,11 @@ def main():
           f"total {wst['total_overlaps']} hits_with {wst['kmer_hits_with_olap']}", flush=True)
     d = _driver_kw(batch)
     for m in modes:
-        os.environ["OVL_SQ"] = m
+        os.environ["OVL_SQ"] = m.rstrip("c")
+        if m.endswith("c"):
+            os.environ["OVL_SQ_CHECK"] = "1"
+        else:
+            os.environ.pop("OVL_SQ_CHECK", None)
         O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
                           Max_Hash_Strings=d["hashstrings"], Max_Hash_Data_Len=d["hashdatalen"],
                           Hash_Mask_Bits=d["hashbits"], Max_Hash_Load=d["hashload"],

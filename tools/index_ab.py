@@ -53,12 +53,14 @@ def main():
               f"wall min {wall[0]:.2f} med {wall[len(wall) // 2]:.2f}, events med "
               f"{ev[len(ev) // 2]:.2f}", flush=True)
         return
-    ext = []
+    ext, seed = [], []
     for _ in range(args.finds):
         novl = oic.find_overlaps(1, n)
         st = oic.stats()
         ext.append(st.get("ms_extend", 0.0))
+        seed.append(st.get("ms_seed", 0.0))
     st["ms_extend"] = sorted(ext)[len(ext) // 2]
+    st["ms_seed"] = sorted(seed)[len(seed) // 2]
     import zlib
     crc = zlib.crc32(np.ascontiguousarray(oic.fetch()).tobytes())
     wall = sorted(x[0] for x in ms[1:])
