@@ -1435,10 +1435,12 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   hipStream_t s = c->stream;
   const auto t0 = std::chrono::steady_clock::now();
   size_t tmpb = 0;
-  // only the top SQ_BITS of a key order the windows: a table slot is the key's top tab_bits,
-  // so windows sorted by the top 24 bits reach the table in runs of 2^(tab_bits - 24) slots
-  // (the order within a run does not matter): 3 radix passes instead of 8
-  const int SQ_BITS = 24;
+  // the whole 64-bit key orders the windows (a table slot is the key's top tab_bits).
+  // Sorting only the top 24 bits would do (3 radix passes instead of 8), but this ROCm's
+  // hipcub / rocPRIM radix sort over bits [40, 64) of 64-bit keys returned duplicated ids
+  // and an unsorted order on an 882,524-window run (the full range sorted it exactly; the
+  // OVL_SQ_CHECK compare in git history, profiles/r04i_sq_sort.txt)
+  const int SQ_BITS = 64;
   HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, Q.key2.p, Q.key.p, Q.wid2.p, Q.wid.p,
                                           (int)std::min<uint64_t>(maxrun, RUN), 64 - SQ_BITS, 64, s));
   std::vector<uint32_t> ublk;
@@ -2244,62 +2246,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         // record written for every searched window (the zeroing and the hits)
         probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) + 8ull * wlim;
         Q.probed = (int)sq_run;
-        if (getenv("OVL_SQ_CHECK")) {
-          // debugging: the random-lookup probe of the same windows, compared record by record
-          const uint32_t ncu = ue - R.u0;
-          DBuf<Probe> ref;
-          DBuf<uint32_t> rh, rf;
-          if (ref.alloc(std::max<uint64_t>(wlim, 1)) || rh.alloc(ncu) || rf.alloc(ncu))
-            return fail(OVL_ERR_OOM, "sq check");
-          HIPC(hipMemsetAsync(ref.p, 0, 8ull * wlim, s));
-          ProbeArgs PA;
-          PA.R = c->reads();
-          PA.X = index_dev(c);
-          PA.units = Q.dunits.p + R.u0;
-          PA.rbase = Q.dwbase.p + R.wb0;
-          PA.nunits = ncu;
-          PA.out = ref.p;
-          PA.unit_hits = rh.p;
-          PA.unit_flags = rf.p;
-          PA.k = k;
-          hipLaunchKernelGGL(k_probe<false>, dim3((ncu + 3) / 4), dim3(256), 0, s, PA);
-          HIPC(hipGetLastError());
-          std::vector<Probe> a(wlim), b(wlim);
-          std::vector<uint32_t> hf(ncu), sf(ncu), hh(ncu);
-          HIPC(hipMemcpyAsync(a.data(), d_probe.p, 8ull * wlim, hipMemcpyDeviceToHost, s));
-          HIPC(hipMemcpyAsync(b.data(), ref.p, 8ull * wlim, hipMemcpyDeviceToHost, s));
-          HIPC(hipMemcpyAsync(hf.data(), rf.p, 4ull * ncu, hipMemcpyDeviceToHost, s));
-          HIPC(hipMemcpyAsync(sf.data(), Q.uflags.p + R.u0, 4ull * ncu, hipMemcpyDeviceToHost, s));
-          HIPC(hipMemcpyAsync(hh.data(), rh.p, 4ull * ncu, hipMemcpyDeviceToHost, s));
-          HIPC(hipStreamSynchronize(s));
-          uint64_t bad = 0, ha = 0, hb = 0, fbad = 0, hbad = 0;
-          for (uint64_t w = 0; w < wlim; w++) {
-            ha += a[w].cnt;
-            hb += b[w].cnt;
-            if (a[w].off != b[w].off || a[w].cnt != b[w].cnt) {
-              if (bad < 5) {
-                uint32_t u = 0;
-                while (Q.wb[R.wb0 + u + 1] <= w) u++;
-                fprintf(stderr, "OVL_SQ_CHECK window %llu (unit %u read %u dir %u o %llu): "
-                        "sorted {%u,%u} random {%u,%u}\n", (unsigned long long)w, u,
-                        Q.units[R.u0 + u].r, Q.units[R.u0 + u].dir,
-                        (unsigned long long)(w - Q.wb[R.wb0 + u]), a[w].off, a[w].cnt,
-                        b[w].off, b[w].cnt);
-              }
-              bad++;
-            }
-          }
-          for (uint32_t u = 0; u < ncu; u++) {
-            fbad += (hf[u] != sf[u]);
-            hbad += (hh[u] != sq_uh[u]);
-          }
-          fprintf(stderr, "OVL_SQ_CHECK run %zu: %u units, %llu windows (of %llu), tab_bits %u "
-                  "slice_bits %u: %llu records differ, hits sorted %llu random %llu, flags "
-                  "differ %llu, unit hits differ %llu\n", sq_run, ncu,
-                  (unsigned long long)wlim, (unsigned long long)R.n, c->tab_bits,
-                  c->slice_bits, (unsigned long long)bad, (unsigned long long)ha,
-                  (unsigned long long)hb, (unsigned long long)fbad, (unsigned long long)hbad);
-        }
       }
       nb = ue - u0;
       rbase.assign(Q.wb.begin() + R.wb0 + (u0 - R.u0), Q.wb.begin() + R.wb0 + (ue - R.u0) + 1);
@@ -2448,6 +2394,14 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       CA.done_cap = 0;
       CA.set_mask = 0;
       CA.seed_hits = c->fb.chits.p;
+      CA.prof = nullptr;
+#ifdef OVL_CHAIN_PROF
+      if (!c->dbg.p) {
+        if (c->dbg.alloc(32)) return fail(OVL_ERR_OOM, "debug counters");
+        HIPC(hipMemsetAsync(c->dbg.p, 0, 256, s));
+      }
+      CA.prof = c->dbg.p + 24;
+#endif
       HIPC(hipEventRecord(c->ev[4], s));
       hipLaunchKernelGGL(k_chain, dim3(chain_waves / 4), dim3(256), 0, s, CA);
       HIPC(hipGetLastError());
@@ -2538,6 +2492,18 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   }
   unsigned long long hs[16];
   HIPC(hipMemcpy(hs, d_stats.p, 128, hipMemcpyDeviceToHost));
+#ifdef OVL_CHAIN_PROF
+  if (c->dbg.p) {
+    unsigned long long cp[8];
+    (void)hipMemcpy(cp, c->dbg.p + 24, 64, hipMemcpyDeviceToHost);
+    const double tot = (double)(cp[0] + cp[1] + cp[2] + cp[3] + cp[4] + cp[5]) + 1e-9;
+    fprintf(stderr, "OVL_CHAIN_PROF wave-cycles (cumulative): probe+qualify %.3f stage %.3f "
+            "discover %.3f scatter %.3f replay %.3f emit %.3f (shares); %llu chunks, %llu "
+            "staged occurrences, %.0f cycles per chunk\n", cp[0] / tot, cp[1] / tot,
+            cp[2] / tot, cp[3] / tot, cp[4] / tot, cp[5] / tot, cp[6], cp[7],
+            tot / (double)(cp[6] ? cp[6] : 1));
+  }
+#endif
   if (c->dbg.p) {
     unsigned long long dd[32];
     (void)hipMemcpy(dd, c->dbg.p, 256, hipMemcpyDeviceToHost);

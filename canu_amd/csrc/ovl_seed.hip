@@ -45,8 +45,24 @@ __device__ __forceinline__ uint32_t unit_windows(const ReadsDev &R, const Unit &
 }
 
 // Number of leading entries of a descending occurrence list whose read iid > a.
+#ifndef OVL_QUAL_UNROLL
+#define OVL_QUAL_UNROLL 0
+#endif
 __device__ __forceinline__ uint32_t qualifying(const uint64_t *occ, uint32_t off, uint32_t cnt,
                                                uint32_t a_iid) {
+#if OVL_QUAL_UNROLL
+  if (cnt <= 8) {
+    // the (at most two) lines of a short list read by independent loads issued together,
+    // instead of a scan whose every load waits for the previous compare
+    uint32_t iid[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) iid[q] = (uint32_t)q < cnt ? (uint32_t)(occ[off + q] >> 32) : 0u;
+    uint32_t n = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) n += (iid[q] > a_iid) ? 1u : 0u;   // a descending prefix
+    return n;
+  }
+#endif
   if (cnt <= 8) {
     uint32_t q = 0;
     while (q < cnt && (uint32_t)(occ[off + q] >> 32) > a_iid) q++;
@@ -373,7 +389,16 @@ struct ChainArgs {
   uint32_t done_cap;            // targets per wave (>= any listed unit's distinct targets)
   uint32_t set_mask;            // set size - 1 (power of two >= 2 done_cap)
   unsigned long long *seed_hits; // qualifying occurrences (Add_Ref calls)
+  unsigned long long *prof;     // OVL_CHAIN_PROF builds: wave-cycles per phase (8 counters)
 };
+
+#ifdef OVL_CHAIN_PROF
+#define CPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define CPROF_ADD(i, a, b) cp[i] += (b) - (a)
+#else
+#define CPROF_T(v)
+#define CPROF_ADD(i, a, b)
+#endif
 
 __device__ __forceinline__ uint32_t done_hash(uint32_t t, uint32_t mask) {
   return (t * 0x85EBCA6Bu) & mask;
@@ -597,6 +622,11 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   uint32_t *done_list = first_launch ? nullptr : A.done_slots + (size_t)gw * A.done_cap;
   uint32_t *done_set = first_launch ? nullptr : A.done_set + (size_t)gw * (A.set_mask + 1);
   unsigned long long nhits = 0;
+#ifdef OVL_CHAIN_PROF
+  // 0 probe records + qualifying + scan, 1 staging, 2 target discovery, 3 slot scan +
+  // scatter, 4 replay, 5 emit, 6 chunks, 7 staged occurrences
+  unsigned long long cp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
   for (;;) {
     uint32_t ui = 0;
@@ -620,6 +650,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
       WAVE_SYNC();
 
       for (uint32_t base = 0; base < nw; base += 64) {
+        CPROF_T(t_a);
         uint32_t o = base + lane;
         Probe p;
         p.off = 0; p.cnt = 0;
@@ -635,6 +666,12 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           if ((int)lane >= d) incl += v;
         }
         uint32_t total = __shfl(incl, 63);
+        CPROF_T(t_b);
+        CPROF_ADD(0, t_a, t_b);
+#ifdef OVL_CHAIN_PROF
+        cp[6]++;
+        cp[7] += total;
+#endif
         if (total == 0) continue;
         seg[lane] = incl - p.cnt;
         soff[lane] = p.off;
@@ -642,6 +679,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
         WAVE_SYNC();
 
         for (uint32_t p0 = 0; p0 < total; p0 += OVL_HCAP) {
+          CPROF_T(t_c);
           uint32_t p1 = p0 + OVL_HCAP < total ? p0 + OVL_HCAP : total;
           // stage occurrences p0..p1 of this chunk, in order (ordered compaction)
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
@@ -656,6 +694,8 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           }
           for (uint32_t i = lane; i < 2 * OVL_MAXT; i += 64) cnt[i] = 0;
           WAVE_SYNC();
+          CPROF_T(t_d);
+          CPROF_ADD(1, t_c, t_d);
           // discover targets (LDS open-addressing set, 128 slots); remember each staged
           // occurrence's slot and count occurrences per slot
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
@@ -683,6 +723,8 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             hs[idx - p0] = slot;
           }
           WAVE_SYNC();
+          CPROF_T(t_e);
+          CPROF_ADD(2, t_d, t_e);
           // slot bases: exclusive scan over the 128 counts (two per lane)
           {
             uint32_t c0 = cnt[2 * lane], c1 = cnt[2 * lane + 1];
@@ -722,6 +764,8 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             WAVE_SYNC();
           }
           WAVE_SYNC();
+          CPROF_T(t_f);
+          CPROF_ADD(3, t_e, t_f);
           uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
           if (t0 != s0.t) { slot_reset(s0); s0.t = t0; }
           if (t1 != s1.t) { slot_reset(s1); s1.t = t1; }
@@ -745,6 +789,10 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             replay(s0, cnt[lane], cnt[OVL_MAXT + lane]);
             replay(s1, cnt[lane + 64], cnt[OVL_MAXT + lane + 64]);
           }
+          {
+            CPROF_T(t_g);
+            CPROF_ADD(4, t_f, t_g);
+          }
           WAVE_SYNC();
         }
       }
@@ -756,8 +804,13 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
         if (lane == 0) A.big_units[atomicAdd(A.n_big, 1u)] = u;
         break;
       }
+      CPROF_T(t_h);
       emit_slot(s0, u, uflags, A, lane);
       emit_slot(s1, u, uflags, A, lane);
+      {
+        CPROF_T(t_i);
+        CPROF_ADD(5, t_h, t_i);
+      }
       if (!over) break;
       // targets the 128-slot table could not hold: another pass over the unit, skipping
       // the targets emitted so far (done set)
@@ -783,6 +836,10 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   }
   for (int d = 32; d > 0; d >>= 1) nhits += __shfl_xor(nhits, d);
   if (lane == 0 && nhits) atomicAdd(A.seed_hits, nhits);
+#ifdef OVL_CHAIN_PROF
+  if (lane == 0 && A.prof)
+    for (int i = 0; i < 8; i++) atomicAdd(&A.prof[i], cp[i]);
+#endif
 }
 
 }  // namespace ovl
