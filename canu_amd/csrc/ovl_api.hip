@@ -1381,7 +1381,7 @@ static bool use_bloom(const ovl_ctx *c, uint32_t bgn, uint32_t end) {
 // and k long, both orientations, read order), their windows keyed by mix64(k-mer) and
 // radix-sorted once, in runs of <= 2^30 windows.  A batch searches the units of the reads
 // below its last hash read: a prefix of them, so per run a window-id bound.  Off (and the
-// random-lookup probe used) when the keys would take more than a third of the free HBM.
+// random-lookup probe used) when the keys would take more than half the free HBM.
 static void sq_release(ovl_ctx *c) {
   auto &Q = c->sq;
   Q.on = false;
@@ -1431,7 +1431,12 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return OVL_OK;
   const uint64_t need = 12ull * total + 20ull * maxrun + 8ull * (maxrun >> 9) + 64ull * nu;
-  if (need > fr / 3) { sq_release(c); return OVL_OK; }
+  if (getenv("OVL_TIMING"))
+    fprintf(stderr, "OVL_TIMING sorted query windows: %u units, %llu windows in %zu runs, "
+            "%.1f GB needed, %.1f GB free\n", nu, (unsigned long long)total, Q.runs.size(),
+            need / 1e9, fr / 1e9);
+  // up to half the free HBM (the configs[4] rank-0 job at 1/8 scale: 3.8 G windows, 67 GB)
+  if (need > fr / 2) { sq_release(c); return OVL_OK; }
   hipStream_t s = c->stream;
   const auto t0 = std::chrono::steady_clock::now();
   size_t tmpb = 0;
@@ -1640,8 +1645,12 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   };
   // the staged kernel instance of a class
   auto stage_kernel = [](bool l16, bool wide, bool sh = false) -> const void * {
+#if OVL_SH_BUILD
     if (sh) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, OVL_RJ, true>)
                        : reinterpret_cast<const void *>(k_extend<true, false, false, OVL_RJ, true>);
+#else
+    (void)sh;
+#endif
     if (wide) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, 2 * OVL_RJ>)
                          : reinterpret_cast<const void *>(k_extend<true, false, false, 2 * OVL_RJ>);
     return l16 ? reinterpret_cast<const void *>(k_extend<true, true>)
@@ -1708,7 +1717,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     // the shared-strand class (OVL_SHARED=1 turns it on): 4 blocks of 8 waves per CU within
     // 40 KB each (32 waves: the reads <= ~11 kb), or 3 within 52 KB (24 waves, <= ~15 kb)
     // when every read fits that and not the first; the -l kernel has its own order
-    const char *she = getenv("OVL_SHARED");
+    const char *she = OVL_SH_BUILD ? getenv("OVL_SHARED") : nullptr;
     if (!ordered && she && atoi(she) != 0) {
       auto longest_sh = [&](size_t cap) -> uint32_t {
         uint32_t L = 0;
@@ -2083,13 +2092,16 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
             // an empty class defers nothing: its counter stays 0 for the next one
           } else {
           n_ext_launch++;
-          if (g.sh && g.l16)
+          if (false) {
+#if OVL_SH_BUILD
+          } else if (g.sh && g.l16) {
             hipLaunchKernelGGL((k_extend<true, true, false, OVL_RJ, true>), dim3(g.waves / g.wpb),
                                dim3(64 * g.wpb), g.lds, xs, EA);
-          else if (g.sh)
+          } else if (g.sh) {
             hipLaunchKernelGGL((k_extend<true, false, false, OVL_RJ, true>), dim3(g.waves / g.wpb),
                                dim3(64 * g.wpb), g.lds, xs, EA);
-          else if (g.wide && g.l16)
+#endif
+          } else if (g.wide && g.l16)
             hipLaunchKernelGGL((k_extend<true, true, false, 2 * OVL_RJ>), dim3(g.waves / g.wpb),
                                dim3(64 * g.wpb), g.lds, xs, EA);
           else if (g.wide)

@@ -1922,6 +1922,13 @@ struct ShSlot {
   int32_t pad[3];
 };
 
+// The shared-strand kernel is built only with OVL_SH_BUILD=1 (measured slower, DESIGN.md
+// round 4): its 8-wave instance shares the row-loop functions with the 6-wave kernel, and a
+// callee takes the tightest register budget of its callers (64 VGPRs), which made the
+// previous row loop spill 96 B per lane in every kernel
+#ifndef OVL_SH_BUILD
+#define OVL_SH_BUILD 0
+#endif
 #ifndef OVL_SH_OCC
 #define OVL_SH_OCC 8             // waves per SIMD the shared-strand kernel is compiled for
 #endif

@@ -352,6 +352,9 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 }
 
 #define OVL_HCAP   256           // staged occurrences per wave
+#ifndef OVL_CHAIN_RUNS
+#define OVL_CHAIN_RUNS 1         // replay runs of head extensions at once (A/B: 0)
+#endif
 #define OVL_MAXT   128           // targets per pass (2 per lane)
 #define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
 #ifndef OVL_CHAIN_OCC
@@ -594,6 +597,9 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   __shared__ uint32_t s_hp[4][OVL_HCAP];
   __shared__ uint8_t  s_hs[4][OVL_HCAP];      // its target slot (0..127), 0xFF: none
   __shared__ uint32_t s_sv[4][OVL_HCAP];      // payloads sorted by (slot, staged order)
+#if OVL_CHAIN_RUNS
+  __shared__ uint64_t s_lst[4][OVL_HCAP / 64]; // bit i: sorted entry i starts a target's list
+#endif
   __shared__ uint32_t s_cnt[4][2 * OVL_MAXT]; // per slot: base, running count
   __shared__ uint32_t s_seg[4][65];
   __shared__ uint32_t s_off[4][64];
@@ -606,6 +612,9 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   uint32_t *hp = s_hp[wave];
   uint8_t *hs = s_hs[wave];
   uint32_t *sv = s_sv[wave];
+#if OVL_CHAIN_RUNS
+  uint64_t *lst = s_lst[wave];
+#endif
   uint32_t *cnt = s_cnt[wave];
   uint32_t *seg = s_seg[wave];
   uint32_t *soff = s_off[wave];
@@ -693,6 +702,9 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             hp[idx - p0] = (lo << 21) | (uint32_t)oc;
           }
           for (uint32_t i = lane; i < 2 * OVL_MAXT; i += 64) cnt[i] = 0;
+#if OVL_CHAIN_RUNS
+          if (lane < OVL_HCAP / 64) lst[lane] = 0;
+#endif
           WAVE_SYNC();
           CPROF_T(t_d);
           CPROF_ADD(1, t_c, t_d);
@@ -737,6 +749,10 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             WAVE_SYNC();
             cnt[2 * lane] = ex;                    // base of slot 2*lane
             cnt[2 * lane + 1] = ex + c0;           // base of slot 2*lane+1
+#if OVL_CHAIN_RUNS
+            if (c0) atomicOr((unsigned long long *)&lst[ex >> 6], 1ull << (ex & 63));
+            if (c1) atomicOr((unsigned long long *)&lst[(ex + c0) >> 6], 1ull << ((ex + c0) & 63));
+#endif
             cnt[OVL_MAXT + 2 * lane] = 0;          // running counts
             cnt[OVL_MAXT + 2 * lane + 1] = 0;
           }
@@ -764,6 +780,48 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             WAVE_SYNC();
           }
           WAVE_SYNC();
+#if OVL_CHAIN_RUNS
+          // Runs (see replay below): entry i of a target's list only extends the head node
+          // when the list's previous entry is the window before on the same diagonal and
+          // both are their windows' only occurrence of the target.  The number of such
+          // entries following entry i goes into the payload's top 5 bits (saturating: a
+          // longer run continues from its 31st entry); found per 64-entry block by a ballot
+          // of the run breaks, blocks from the last, carrying the next break.  A block
+          // reads its neighbours before any lane writes, and the block after it is done.
+          {
+            const uint32_t tn = p1 - p0;
+            auto start = [&](uint32_t i) -> bool { return (lst[i >> 6] >> (i & 63)) & 1ull; };
+            uint32_t next_break = tn;                  // first break at or after the block
+            for (int32_t b0 = (int32_t)((tn - 1) & ~63u); b0 >= 0; b0 -= 64) {
+              const uint32_t i = (uint32_t)b0 + lane;
+              bool cont = false;
+              uint32_t v = 0;
+              if (i < tn) {
+                v = sv[i] & 0x7FFFFFFu;
+                if (i > 0 && !start(i)) {
+                  const uint32_t w = sv[i - 1] & 0x7FFFFFFu;
+                  const uint32_t o = v >> 21, ow = w >> 21;
+                  const int32_t dg = (int32_t)(v & 0x1FFFFFu) - (int32_t)o;
+                  const int32_t dw = (int32_t)(w & 0x1FFFFFu) - (int32_t)ow;
+                  cont = ow + 1 == o && dg == dw &&
+                         (i + 1 >= tn || start(i + 1) || ((sv[i + 1] & 0x7FFFFFFu) >> 21) != o) &&
+                         (i < 2 || start(i - 1) || ((sv[i - 2] & 0x7FFFFFFu) >> 21) != ow);
+                }
+              }
+              const uint64_t brk = __builtin_amdgcn_ballot_w64(!cont);   // lanes past tn break
+              const uint64_t above = brk & ~((2ull << lane) - 1ull);
+              const uint32_t nb = above ? (uint32_t)b0 + (uint32_t)__builtin_ctzll(above) : next_break;
+              WAVE_SYNC();
+              if (i < tn) {
+                const uint32_t r = nb - i - 1;
+                sv[i] = v | ((r < 31 ? r : 31u) << 27);
+              }
+              if (brk) next_break = (uint32_t)b0 + (uint32_t)__builtin_ctzll(brk);
+              WAVE_SYNC();
+            }
+          }
+          WAVE_SYNC();
+#endif
           CPROF_T(t_f);
           CPROF_ADD(3, t_e, t_f);
           uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
@@ -773,6 +831,34 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           // next payload is loaded before the current one is applied (no LDS round trip on
           // the loop's dependency chain)
           {
+#if OVL_CHAIN_RUNS
+            // An entry followed by rl run entries: once it is applied, if the head node is
+            // the one holding it (expected next window o + 1 on its diagonal), each run entry
+            // would take Add_Match's first branch -- Len++ -- so the run is applied at once:
+            // Len += rl, diag_ct += rl, diag_end = the run's last window (windows ascend).
+            // Otherwise the next entry is applied one by one as before.
+            auto replay = [&](SlotState &st, uint32_t b, uint32_t n) {
+              for (uint32_t i = 0; i < n;) {
+                const uint32_t cur = sv[b + i];
+                const uint32_t r = cur >> 27;
+                const int32_t pp = (int32_t)(cur & 0x1FFFFFu);
+                const int32_t o_j = (int32_t)(base + ((cur >> 21) & 63u));
+                st.diag_ct++;                                 // Add_Ref (:203-206)
+                if (st.diag_bgn > o_j) st.diag_bgn = o_j;
+                if (st.diag_end < o_j) st.diag_end = o_j;
+                add_match(st, pp, o_j, k, A.pool, W, A, lane);
+                i++;
+                if (r && st.head != 0 && st.hd.Start + st.hd.Len - k == o_j &&
+                    st.hd.Offset - st.hd.Start == pp - o_j) {
+                  st.hd.Len += (int32_t)r;
+                  st.diag_ct += (int32_t)r;
+                  const int32_t o_l = (int32_t)(base + ((sv[b + i + r - 1] >> 21) & 63u));
+                  if (st.diag_end < o_l) st.diag_end = o_l;
+                  i += r;
+                }
+              }
+            };
+#else
             auto replay = [&](SlotState &ss, uint32_t b, uint32_t n) {
               uint32_t v = n ? sv[b] : 0u;
               for (uint32_t i = 0; i < n; i++) {
@@ -786,6 +872,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
                 add_match(ss, pp, o_j, k, A.pool, W, A, lane);
               }
             };
+#endif
             replay(s0, cnt[lane], cnt[OVL_MAXT + lane]);
             replay(s1, cnt[lane + 64], cnt[OVL_MAXT + lane + 64]);
           }
