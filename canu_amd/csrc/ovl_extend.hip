@@ -470,7 +470,7 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #endif
 #define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
 #ifndef OVL_INPLACE
-#define OVL_INPLACE 1            // the row loop updates its row registers in place (A/B: 0)
+#define OVL_INPLACE 0            // 1: the row loop updates its row registers in place (A/B)
 #endif
 static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 

@@ -251,12 +251,12 @@ struct SqProbeArgs {
 __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
   const uint64_t smask = (1ull << A.X.slice_bits) - 1;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < A.n; i += stride) {
-    const uint32_t w = A.wid[i];
-    if (w >= A.wlim) continue;                   // no k-mer, or a unit this batch skips
-    const uint64_t M = A.key[i];
-    const uint64_t s0 = M >> (64 - A.X.tab_bits), base = s0 & ~smask;
-    TabEntry t = A.X.tab[s0];
+  const uint32_t shift = 64 - A.X.tab_bits;
+  // a window whose k-mer the table holds: its record, or (a skip k-mer) its unit's
+  // screened-end flags; the table entry first loaded is passed in
+  auto finish = [&](uint32_t w, uint64_t M, TabEntry t) {
+    if (w >= A.wlim) return;                     // no k-mer, or a unit this batch skips
+    const uint64_t s0 = M >> shift, base = s0 & ~smask;
     bool found = false;
     for (uint64_t j = 1;; j++) {                 // index_find's linear probe (k_probe)
       if (t.cnt == 0) break;
@@ -264,12 +264,12 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
       if (j > smask) break;
       t = A.X.tab[base | ((s0 + j) & smask)];
     }
-    if (!found) continue;
-    uint32_t u = A.ublk[w >> 9];
-    while (A.wbase[u + 1] <= w) u++;
+    if (!found) return;
     const uint32_t c = t.cnt;
     if (c & OVL_FLAG_SKIP) {
       // Hash_Find found an Empty entry: hi_hits (Find_Overlaps.C:321-366)
+      uint32_t u = A.ublk[w >> 9];
+      while (A.wbase[u + 1] <= w) u++;
       const uint32_t o = w - (uint32_t)A.wbase[u];
       const int32_t L = (int32_t)A.R.len[A.units[u].r];
       uint32_t f = 0;
@@ -282,6 +282,29 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
       pr.cnt = c & OVL_CNT_MASK;
       A.out[w] = pr;
     }
+  };
+  // 4 sorted windows per thread per step: their ids, keys and first table entries are
+  // loaded together (the loop is latency-bound: id -> key -> entry -> record)
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i0 < A.n;
+       i0 += 4 * stride) {
+    uint32_t w[4];
+    uint64_t M[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint64_t i = i0 + q * stride;
+      w[q] = i < A.n ? A.wid[i] : 0xFFFFFFFFu;
+      M[q] = i < A.n ? A.key[i] : 0ull;
+    }
+    TabEntry t[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      t[q].key = 0; t[q].off = 0; t[q].cnt = 0;
+      if (w[q] < A.wlim) t[q] = A.X.tab[M[q] >> shift];
+    }
+    finish(w[0], M[0], t[0]);
+    finish(w[1], M[1], t[1]);
+    finish(w[2], M[2], t[2]);
+    finish(w[3], M[3], t[3]);
   }
 }
 
@@ -352,6 +375,9 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 }
 
 #define OVL_HCAP   256           // staged occurrences per wave
+#ifndef OVL_STAGE_BATCH
+#define OVL_STAGE_BATCH 0        // stage a chunk's 4 x 64 occurrences with their loads together
+#endif
 #ifndef OVL_CHAIN_RUNS
 #define OVL_CHAIN_RUNS 1         // replay runs of head extensions at once (A/B: 0)
 #endif
@@ -691,6 +717,36 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           CPROF_T(t_c);
           uint32_t p1 = p0 + OVL_HCAP < total ? p0 + OVL_HCAP : total;
           // stage occurrences p0..p1 of this chunk, in order (ordered compaction)
+#if OVL_STAGE_BATCH
+          {
+            // the 4 x 64 entries' windows first (independent LDS searches), then their
+            // occurrence loads issued together: one memory round trip instead of four
+            constexpr int NB = OVL_HCAP / 64;
+            uint32_t lw[NB], src[NB];
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+              const uint32_t idx = p0 + 64 * q + lane;
+              uint32_t lo = 0, hi = 64;          // last j with seg[j] <= idx
+              while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (seg[mid] <= idx) lo = mid; else hi = mid;
+              }
+              lw[q] = lo;
+              src[q] = idx < p1 ? soff[lo] + (idx - seg[lo]) : 0xFFFFFFFFu;
+            }
+            uint64_t oc[NB];
+#pragma unroll
+            for (int q = 0; q < NB; q++) oc[q] = src[q] != 0xFFFFFFFFu ? A.occ[src[q]] : 0ull;
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+              const uint32_t idx = p0 + 64 * q + lane;
+              if (idx < p1) {
+                ht[idx - p0] = (uint32_t)(oc[q] >> 32);
+                hp[idx - p0] = (lw[q] << 21) | (uint32_t)oc[q];
+              }
+            }
+          }
+#else
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
             uint32_t lo = 0, hi = 64;            // last j with seg[j] <= idx
             while (hi - lo > 1) {
@@ -701,6 +757,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             ht[idx - p0] = (uint32_t)(oc >> 32);
             hp[idx - p0] = (lo << 21) | (uint32_t)oc;
           }
+#endif
           for (uint32_t i = lane; i < 2 * OVL_MAXT; i += 64) cnt[i] = 0;
 #if OVL_CHAIN_RUNS
           if (lane < OVL_HCAP / 64) lst[lane] = 0;
@@ -790,35 +847,45 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           // reads its neighbours before any lane writes, and the block after it is done.
           {
             const uint32_t tn = p1 - p0;
-            auto start = [&](uint32_t i) -> bool { return (lst[i >> 6] >> (i & 63)) & 1ull; };
             uint32_t next_break = tn;                  // first break at or after the block
             for (int32_t b0 = (int32_t)((tn - 1) & ~63u); b0 >= 0; b0 -= 64) {
               const uint32_t i = (uint32_t)b0 + lane;
+              // the list starts around the block: bit 64 + l of (prev, cur) = entry b0 + l
+              const uint64_t lc = lst[b0 >> 6];
+              const uint64_t lp = b0 ? lst[(b0 >> 6) - 1] : 0ull;
+              const uint64_t ln = (uint32_t)b0 + 64 < OVL_HCAP ? lst[(b0 >> 6) + 1] : 0ull;
+              const bool st_i = (lc >> lane) & 1ull;
+              const bool st_m1 = lane ? (lc >> (lane - 1)) & 1ull : (lp >> 63) & 1ull;
+              const bool st_p1 = lane < 63 ? (lc >> (lane + 1)) & 1ull : ln & 1ull;
+              // neighbours through lane exchanges (the block's entries) and, at its edges,
+              // LDS reads of the entries around it (the block after it already holds its
+              // run bits, masked off)
+              uint32_t v = i < tn ? (sv[i] & 0x7FFFFFFu) : 0u;
+              const uint32_t vm1 = lane ? (uint32_t)__shfl_up((int)v, 1)
+                                        : (i > 0 ? (sv[i - 1] & 0x7FFFFFFu) : 0u);
+              uint32_t vm2 = (uint32_t)__shfl_up((int)v, 2);
+              if (lane < 2) vm2 = i >= 2 ? (sv[i - 2] & 0x7FFFFFFu) : 0u;
+              uint32_t vp1 = (uint32_t)__shfl_down((int)v, 1);
+              if (lane == 63) vp1 = i + 1 < tn ? (sv[i + 1] & 0x7FFFFFFu) : 0u;
               bool cont = false;
-              uint32_t v = 0;
-              if (i < tn) {
-                v = sv[i] & 0x7FFFFFFu;
-                if (i > 0 && !start(i)) {
-                  const uint32_t w = sv[i - 1] & 0x7FFFFFFu;
-                  const uint32_t o = v >> 21, ow = w >> 21;
-                  const int32_t dg = (int32_t)(v & 0x1FFFFFu) - (int32_t)o;
-                  const int32_t dw = (int32_t)(w & 0x1FFFFFu) - (int32_t)ow;
-                  cont = ow + 1 == o && dg == dw &&
-                         (i + 1 >= tn || start(i + 1) || ((sv[i + 1] & 0x7FFFFFFu) >> 21) != o) &&
-                         (i < 2 || start(i - 1) || ((sv[i - 2] & 0x7FFFFFFu) >> 21) != ow);
-                }
+              if (i < tn && i > 0 && !st_i) {
+                const uint32_t o = v >> 21, ow = vm1 >> 21;
+                const int32_t dg = (int32_t)(v & 0x1FFFFFu) - (int32_t)o;
+                const int32_t dw = (int32_t)(vm1 & 0x1FFFFFu) - (int32_t)ow;
+                cont = ow + 1 == o && dg == dw &&
+                       (i + 1 >= tn || st_p1 || (vp1 >> 21) != o) &&
+                       (i < 2 || st_m1 || (vm2 >> 21) != ow);
               }
               const uint64_t brk = __builtin_amdgcn_ballot_w64(!cont);   // lanes past tn break
               const uint64_t above = brk & ~((2ull << lane) - 1ull);
               const uint32_t nb = above ? (uint32_t)b0 + (uint32_t)__builtin_ctzll(above) : next_break;
-              WAVE_SYNC();
               if (i < tn) {
                 const uint32_t r = nb - i - 1;
                 sv[i] = v | ((r < 31 ? r : 31u) << 27);
               }
               if (brk) next_break = (uint32_t)b0 + (uint32_t)__builtin_ctzll(brk);
-              WAVE_SYNC();
             }
+            WAVE_SYNC();
           }
           WAVE_SYNC();
 #endif
