@@ -1379,7 +1379,7 @@ static bool use_bloom(const ovl_ctx *c, uint32_t bgn, uint32_t end) {
 // The sorted query windows of an OverlapDriver job (k_sq_keys / k_probe_sorted): the units
 // find_impl searches (ref reads bgn..end of libraries [lib_lo, lib_hi] at least --minlength
 // and k long, both orientations, read order), their windows keyed by mix64(k-mer) and
-// radix-sorted once, in runs of <= 2^30 windows.  A batch searches the units of the reads
+// radix-sorted once, in runs of <= 2^29 windows.  A batch searches the units of the reads
 // below its last hash read: a prefix of them, so per run a window-id bound.  Off (and the
 // random-lookup probe used) when the keys would take more than half the free HBM.
 static void sq_release(ovl_ctx *c) {
@@ -1410,8 +1410,11 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   }
   const uint32_t nu = (uint32_t)Q.units.size();
   if (nu == 0) return OVL_OK;
-  // runs of <= 2^30 windows (hipcub sorts index with int)
-  const uint64_t RUN = 1ull << 30;
+  // runs of <= RUN windows (hipcub sorts index with int)
+  // 2^29 windows per run: a run's sort needs ~24 B per window beside the 12 B it keeps (the
+  // configs[4] rank-0 job at 1/8 scale: 3.8 G windows, 58 GB with 2^29-window runs, 71 GB
+  // with 2^30 -- past half of the ~133 GB free when its second batch starts)
+  const uint64_t RUN = 1ull << 29;
   uint64_t total = 0, maxrun = 0;
   for (uint32_t u = 0; u < nu;) {
     ovl_ctx::SqRun R;
@@ -1430,7 +1433,7 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   }
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return OVL_OK;
-  const uint64_t need = 12ull * total + 20ull * maxrun + 8ull * (maxrun >> 9) + 64ull * nu;
+  const uint64_t need = 12ull * total + 24ull * maxrun + 8ull * (maxrun >> 9) + 64ull * nu;
   if (getenv("OVL_TIMING"))
     fprintf(stderr, "OVL_TIMING sorted query windows: %u units, %llu windows in %zu runs, "
             "%.1f GB needed, %.1f GB free\n", nu, (unsigned long long)total, Q.runs.size(),

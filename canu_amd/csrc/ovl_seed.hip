@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(256) k_probe(ProbeArgs A) {
 // miss the batch, so k_probe's one random table lookup per window per batch runs at the
 // memory system's random-access rate (~40 G lookups/s, whatever the table's size).  Here the
 // job's query windows are keyed by their k-mer's mix64 and radix-sorted ONCE (k_sq_keys, in
-// runs of <= 2^30 windows); each batch then streams a run in key order, which is table-slot
+// runs of <= 2^29 windows); each batch then streams a run in key order, which is table-slot
 // order (a slot is the top tab_bits of the same mix64): consecutive windows read consecutive
 // slots, the table and the windows are both read as streams, and only the windows whose
 // k-mer the batch holds write a Probe record back to window order (k_probe_sorted).  The
