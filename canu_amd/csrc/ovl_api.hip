@@ -2738,10 +2738,13 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   uint32_t bgn = g_bgn_hash;
   uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
   uint64_t batches = 0;
-  // the query windows sorted once for the job's batches (sq_prepare) from its second batch
-  // on -- a one-batch job probes at random as ovl_find_overlaps does; OVL_SQ=0: never,
-  // OVL_SQ=1: from the first batch.  They are the job's own work: released at its end.
-  int sq_mode = 2;
+  // the query windows sorted once for the job's batches (sq_prepare): OVL_SQ=2 from the
+  // second batch on, 1 from the first, 0 (the default) never.  Off by default: on the
+  // configs[4] rank-0 job the sorted probe takes 456 instead of 654 ms, but sorting the job's
+  // 3.8 G windows over all 64 key bits costs ~310 ms (seed 1,141 vs 1,030 ms,
+  // profiles/r04m_c4_sq*.json); a partial-range sort would pay, and this ROCm's returned
+  // wrong orders.  They are the job's own work: released at its end.
+  int sq_mode = 0;
   if (const char *e = getenv("OVL_SQ")) sq_mode = atoi(e);
   struct SqOff {
     ovl_ctx *c;

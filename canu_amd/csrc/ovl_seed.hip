@@ -375,6 +375,9 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 }
 
 #define OVL_HCAP   256           // staged occurrences per wave
+#ifndef OVL_SCATTER_BALLOT
+#define OVL_SCATTER_BALLOT 1     // a staged entry's rank in its target's list from ballots
+#endif
 #ifndef OVL_STAGE_BATCH
 #define OVL_STAGE_BATCH 0        // stage a chunk's 4 x 64 occurrences with their loads together
 #endif
@@ -817,6 +820,30 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           // stable scatter: within each 64-entry step a lane's rank among the lanes of its
           // slot is the popcount of the lower lanes in the slot's lane mask (one LDS OR per
           // lane), so every slot's list keeps the staged (window, chain) order
+#if OVL_SCATTER_BALLOT
+          // (here the lanes of a slot come from 7 ballots of the slot's bits -- no LDS masks
+          // and one barrier per step instead of three)
+          for (uint32_t b0 = p0; b0 < p1; b0 += 64) {
+            const uint32_t idx = b0 + lane;
+            const uint32_t slot = (idx < p1) ? hs[idx - p0] : 0xFFu;
+            const bool has = slot != 0xFFu;
+            uint64_t mk = __builtin_amdgcn_ballot_w64(has);
+#pragma unroll
+            for (int bit = 0; bit < 7; bit++) {
+              const bool on = (slot >> bit) & 1u;
+              const uint64_t m = __builtin_amdgcn_ballot_w64(has && on);
+              mk &= on ? m : ~m;
+            }
+            if (has) {
+              const uint32_t rank = __builtin_popcountll(mk & ((1ull << lane) - 1));
+              sv[cnt[slot] + cnt[OVL_MAXT + slot] + rank] = hp[idx - p0];
+            }
+            WAVE_SYNC();
+            if (has && lane == 63u - (uint32_t)__builtin_clzll(mk))   // the slot's last lane
+              cnt[OVL_MAXT + slot] += __builtin_popcountll(mk);
+            WAVE_SYNC();
+          }
+#else
           for (uint32_t b0 = p0; b0 < p1; b0 += 64) {
             uint32_t idx = b0 + lane;
             uint32_t slot = (idx < p1) ? hs[idx - p0] : 0xFFu;
@@ -836,6 +863,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             }
             WAVE_SYNC();
           }
+#endif
           WAVE_SYNC();
 #if OVL_CHAIN_RUNS
           // Runs (see replay below): entry i of a target's list only extends the head node

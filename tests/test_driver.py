@@ -126,6 +126,37 @@ def test_gpu_driver_vs_oracle_and_reference(built, case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["table_load", "datalen_threads"])
+def test_gpu_driver_sorted_windows_vs_oracle(built, monkeypatch, case):
+    """The driver cases with the job's sorted query windows from the second batch on
+    (OVL_SQ=2; off by default): the table-load case is the one whose 882,524-window run a
+    partial-range radix sort returned with duplicated window ids."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    monkeypatch.setenv("OVL_SQ", "2")
+    kw, batch, threads, rr = CASES[case]
+    rs = synth_reads(**kw)
+    P = _params()
+    want, wst, batches = oracle.run_oracle_driver(
+        rs, P, ref_range=rr or (1, oracle.UINT32_MAX), threads=threads, with_stats=True,
+        **_driver_kw(batch))
+    d = _driver_kw(batch)
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=d["hashstrings"], Max_Hash_Data_Len=d["hashdatalen"],
+                      Hash_Mask_Bits=d["hashbits"], Max_Hash_Load=d["hashload"],
+                      Num_PThreads=threads).finalize()
+    if rr:
+        O.bgnRefID, O.endRefID = rr
+    oic = OverlapInCore(O, device=0)
+    got = oic.run_driver(rs)
+    st = oic.stats()
+    oic.close()
+    assert st["hash_batches"] == len(batches) >= 3
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for _, ok in STAT_KEYS:
+        assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
+
+
+@pytest.mark.gpu
 def test_gpu_driver_10kb_production_batches(built):
     """Reads at the benchmark's 10 kb length under byte-limited batches (canu's
     partitionLength hands each job --hashdatalen; here ~1 Mbp per batch): 4 batches, the
