@@ -265,6 +265,7 @@ struct ovl_ctx {
     DBuf<Unit> dunits;
     DBuf<uint8_t> tmp;
     DBuf<uint32_t> uhits, uflags;
+    uint32_t resorted = 0;       // runs whose partial-range sort came back unordered
     int probed = -1;             // the run whose records fb.probe holds for this batch
     uint32_t probed_nu = 0;      // ... for this many of its units
     double ms_sort = 0;
@@ -1434,6 +1435,7 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return OVL_OK;
   const uint64_t need = 12ull * total + 24ull * maxrun + 8ull * (maxrun >> 9) + 64ull * nu;
+  Q.resorted = 0;
   if (getenv("OVL_TIMING"))
     fprintf(stderr, "OVL_TIMING sorted query windows: %u units, %llu windows in %zu runs, "
             "%.1f GB needed, %.1f GB free\n", nu, (unsigned long long)total, Q.runs.size(),
@@ -1443,14 +1445,23 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   hipStream_t s = c->stream;
   const auto t0 = std::chrono::steady_clock::now();
   size_t tmpb = 0;
-  // the whole 64-bit key orders the windows (a table slot is the key's top tab_bits).
-  // Sorting only the top 24 bits would do (3 radix passes instead of 8), but this ROCm's
-  // hipcub / rocPRIM radix sort over bits [40, 64) of 64-bit keys returned duplicated ids
-  // and an unsorted order on an 882,524-window run (the full range sorted it exactly; the
-  // OVL_SQ_CHECK compare in git history, profiles/r04i_sq_sort.txt)
-  const int SQ_BITS = 64;
-  HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, Q.key2.p, Q.key.p, Q.wid2.p, Q.wid.p,
-                                          (int)std::min<uint64_t>(maxrun, RUN), 64 - SQ_BITS, 64, s));
+  // Windows need only be ordered by the key's top 24 bits (a table slot is its top
+  // tab_bits): 3 radix passes instead of 8.  This ROCm's hipcub / rocPRIM radix sort over a
+  // partial bit range of 64-bit keys returned duplicated ids and an unsorted order below
+  // ~1.4 M items (tools/sortcheck.hip: 100 k and 882,524 items wrong for [32|40|48, 64),
+  // 1.44 M to 2^27 right; profiles/r04n_sortcheck.log), so runs under PART_MIN windows sort
+  // all 64 bits, and a partially sorted run is checked (k_sq_sorted_check) and sorted again
+  // over all bits if its order is broken.
+  const uint64_t PART_MIN = 1ull << 22;
+  const int PART_LO = 40;
+  {
+    size_t t64 = 0;
+    HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, Q.key2.p, Q.key.p, Q.wid2.p, Q.wid.p,
+                                            (int)std::min<uint64_t>(maxrun, RUN), PART_LO, 64, s));
+    HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t64, Q.key2.p, Q.key.p, Q.wid2.p, Q.wid.p,
+                                            (int)std::min<uint64_t>(maxrun, RUN), 0, 64, s));
+    tmpb = std::max(tmpb, t64);
+  }
   std::vector<uint32_t> ublk;
   for (auto &R : Q.runs) {
     R.ub0 = ublk.size();
@@ -1484,8 +1495,24 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
     hipLaunchKernelGGL(k_sq_keys, dim3((KA.nunits + 3) / 4), dim3(256), 0, s, KA);
     HIPC(hipGetLastError());
     size_t tb = tmpb;
+    const int lo = R.n >= PART_MIN ? PART_LO : 0;
     HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
-                                            Q.wid.p + R.e0, (int)R.n, 64 - SQ_BITS, 64, s));
+                                            Q.wid.p + R.e0, (int)R.n, lo, 64, s));
+    if (lo) {
+      HIPC(hipMemsetAsync(Q.uhits.p, 0, 4, s));      // a flag word (uhits is filled later)
+      hipLaunchKernelGGL(k_sq_sorted_check, dim3(4 * c->n_cu), dim3(256), 0, s,
+                         (const uint64_t *)(Q.key.p + R.e0), R.n, (uint32_t)lo, Q.uhits.p);
+      uint32_t broken = 0;
+      HIPC(hipMemcpyAsync(&broken, Q.uhits.p, 4, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+      if (broken) {                                  // the keys again, every bit sorted
+        hipLaunchKernelGGL(k_sq_keys, dim3((KA.nunits + 3) / 4), dim3(256), 0, s, KA);
+        tb = tmpb;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
+                                                Q.wid.p + R.e0, (int)R.n, 0, 64, s));
+        Q.resorted++;
+      }
+    }
   }
   HIPC(hipStreamSynchronize(s));
   // the sort buffers go: only the sorted runs stay for the job
@@ -1493,6 +1520,9 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   Q.wid2.release();
   Q.tmp.release();
   Q.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (getenv("OVL_TIMING"))
+    fprintf(stderr, "OVL_TIMING sorted query windows: sorted in %.1f ms (%u runs sorted again "
+            "over all bits)\n", Q.ms_sort, Q.resorted);
   c->stats.ms_seed += Q.ms_sort;
   Q.ref_bgn = bgn; Q.ref_end = end; Q.lib_lo = lib_lo; Q.lib_hi = lib_hi;
   Q.on = true;

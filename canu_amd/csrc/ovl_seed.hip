@@ -308,6 +308,14 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
   }
 }
 
+// a partially sorted run's order on the key bits from `shift` up (see sq_prepare)
+__global__ void __launch_bounds__(256) k_sq_sorted_check(const uint64_t *key, uint64_t n,
+                                                         uint32_t shift, uint32_t *bad) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    if ((key[i] >> shift) < (key[i - 1] >> shift)) { atomicOr(bad, 1u); return; }
+}
+
 // the units' hit counts (k_probe's unit_hits) from the records: one wave per unit, its
 // windows' records read once (a random atomic per hit would cost more)
 __global__ void __launch_bounds__(256) k_sq_unit_hits(const Probe *rec, const uint64_t *wbase,
@@ -376,7 +384,8 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 
 #define OVL_HCAP   256           // staged occurrences per wave
 #ifndef OVL_SCATTER_BALLOT
-#define OVL_SCATTER_BALLOT 1     // a staged entry's rank in its target's list from ballots
+#define OVL_SCATTER_BALLOT 0     // 1: a staged entry's rank in its target's list from ballots
+                                 // (measured +1.7 ms per step, not kept)
 #endif
 #ifndef OVL_STAGE_BATCH
 #define OVL_STAGE_BATCH 0        // stage a chunk's 4 x 64 occurrences with their loads together
