@@ -309,7 +309,7 @@ __global__ void __launch_bounds__(256) k_rand_lookup(const uint4 *t, uint64_t ma
       v[q] = t[(x >> 17) & mask];
     }
 #pragma unroll
-    for (int q = 0; q < Q; q++) acc ^= v[q].x ^ v[q].w;
+    for (int q = 0; q < Q; q++) acc ^= v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;   // whole 16-B loads
   }
   if (acc == 0x9E3779B9u) sink[0] = acc;       // keeps the loads live; (almost) never taken
 }
@@ -336,21 +336,30 @@ __global__ void __launch_bounds__(256) k_slot_list(ReadsDev R, const Unit *units
   }
 }
 
-// the same lookups as pure loads: 8 slots per lane in flight, nothing else in the loop
+// the same lookups as pure loads: 8 table entries per lane in flight, the next group's 8
+// slot indices loaded while they are (so no phase of the loop waits on the slot stream)
 __global__ void __launch_bounds__(256) k_slot_replay(const uint4 *t, const uint32_t *slot,
                                                      uint64_t n, uint32_t *sink) {
   uint32_t acc = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i0 < n; i0 += 8 * stride) {
+  uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  uint32_t sl[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint64_t i = i0 + q * stride;
+    sl[q] = i < n ? slot[i] : 0xFFFFFFFFu;
+  }
+  for (; i0 < n; i0 += 8 * stride) {
     uint4 v[8];
 #pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = sl[q] != 0xFFFFFFFFu ? t[sl[q]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
     for (int q = 0; q < 8; q++) {
-      const uint64_t i = i0 + q * stride;
-      const uint32_t sl = i < n ? slot[i] : 0xFFFFFFFFu;
-      v[q] = sl != 0xFFFFFFFFu ? t[sl] : make_uint4(0, 0, 0, 0);
+      const uint64_t i = i0 + 8 * stride + q * stride;
+      sl[q] = i < n ? slot[i] : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) acc ^= v[q].x ^ v[q].w;
+    for (int q = 0; q < 8; q++) acc ^= v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;   // whole 16-B loads
   }
   if (acc == 0x9E3779B9u) sink[0] = acc;
 }
