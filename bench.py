@@ -585,10 +585,11 @@ def rooflines(args, job, st, world):
                          "valu_frac": round(valu / valu_pk, 4), "hbm": hbm,
                          "limiter": "instruction issue of the greedy O(ND) rows: integer "
                                     "VALU and the per-row scalar control at about equal "
-                                    "shares of their peaks, 6 waves per SIMD (LDS-capped); "
-                                    "a 12.5 % SALU cut moved the time 1 % (DESIGN.md), so "
-                                    "no one unit binds alone.  HBM moves the row log and "
-                                    "spills (hbm.traffic_gbs), not the algorithmic bytes"})
+                                    "shares of their peaks; 6 waves per SIMD (LDS-capped), "
+                                    "and 8 measured no faster (DESIGN.md round 4), so the "
+                                    "waves' dependency chains are covered and the row's "
+                                    "instruction count is what binds.  HBM moves the row log "
+                                    "and spills (hbm.traffic_gbs), not the algorithmic bytes"})
         else:
             roof.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": hbm["frac"], "traffic": None,
