@@ -406,9 +406,26 @@ class Configs4Rank(Configs2):
         genome_len = int(n * a.read_len / a.coverage)
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world
-        part = synth_reads_parallel(n, a.read_len, genome_len, a.read_error, seed=a.seed,
-                                    len_jitter=0.2, read_range=(lo, hi),
-                                    workers=max(1, 16 // self.world))
+        # CANU_C4_READS_CACHE=<dir> (one rank): the read set saved there once and loaded by
+        # later runs -- the PMC passes run under rocprofv3, whose signal handling hangs the
+        # generator's worker pool (tools/c4_cache.py writes it)
+        cache = os.environ.get("CANU_C4_READS_CACHE") if self.world == 1 else None
+        key = f"c4_{n}_{a.read_len}_{a.coverage}_{a.read_error}_{a.seed}"
+        if cache and os.path.exists(os.path.join(cache, key + "_lengths.npy")):
+            from canu_amd.synth import ReadSet
+            lens = np.load(os.path.join(cache, key + "_lengths.npy"))
+            offs = np.zeros(lens.shape[0], dtype=np.uint64)
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            part = ReadSet(bases=np.load(os.path.join(cache, key + "_bases.npy")),
+                           offsets=offs, lengths=lens)
+        else:
+            part = synth_reads_parallel(n, a.read_len, genome_len, a.read_error, seed=a.seed,
+                                        len_jitter=0.2, read_range=(lo, hi),
+                                        workers=max(1, 16 // self.world))
+            if cache:
+                os.makedirs(cache, exist_ok=True)
+                np.save(os.path.join(cache, key + "_bases.npy"), part.bases)
+                np.save(os.path.join(cache, key + "_lengths.npy"), part.lengths)
         if self.world == 1:
             bases = torch.from_numpy(part.bases).to(self.dev)
             lengths = part.lengths
