@@ -396,7 +396,8 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 #define OVL_MAXT   128           // targets per pass (2 per lane)
 #define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
 #ifndef OVL_CHAIN_OCC
-#define OVL_CHAIN_OCC 6          // k_chain waves per SIMD (80 VGPRs)
+#define OVL_CHAIN_OCC 5          // k_chain waves per SIMD (96 VGPRs: 13 spilled instead of 47 at 6;
+                                 // chain 74 -> 62 ms per step at 50k x 10 kb, r04s A/B)
 #endif
 
 struct ChainArgs {
