@@ -1155,7 +1155,14 @@ static const uint64_t MAX_STRING_NUM = (1ull << 31) - 1; // overlapInCore.C:57-6
 // previous search hold (released when a build needs it), less 64 GB kept for the seed and
 // extension buffers (whose budgets shrink to fit).  OVL_TEST_INDEX_WINDOW_CAP lowers
 // it (tests of the capped path).
-static void sq_release(ovl_ctx *c);
+static void sq_release(ovl_ctx *c, bool free_mem = true);
+// the sorted-window probe checks the batch's Bloom filter before the table (OVL_SQ_BLOOM=0:
+// it reads the table for every window, and the batch is built without the filter)
+static bool sq_bloom() {
+  static const bool on = !getenv("OVL_SQ_BLOOM") || atoi(getenv("OVL_SQ_BLOOM")) != 0;
+  return on;
+}
+static size_t sq_held_bytes(const ovl_ctx *c);
 static void release_find_buffers(ovl_ctx *c) {
   auto &f = c->fb;
   for (int i = 0; i < 2; i++) {
@@ -1193,7 +1200,8 @@ static uint64_t index_window_cap(ovl_ctx *c) {
                           (f.pairs[0].n + f.pairs[1].n) * sizeof(PairRec) +
                           4ull * (f.rows.n + f.rowdir.n + f.deltas.n) +
                           c->acc.units.n * sizeof(Unit) + c->acc.pnodes.n * sizeof(Node) +
-                          c->acc.pairs.n * sizeof(PairRec);
+                          c->acc.pairs.n * sizeof(PairRec) +
+                          (c->sq.on ? 0 : sq_held_bytes(c));   // an earlier job's sorted windows
     // the search and extension buffers of the batch are sized by budget (up to ~64 GB on a
     // 288 GB part): keep that much aside, or a fifth of a smaller device
     const uint64_t avail = fr + held;
@@ -1300,10 +1308,11 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
         eb = id;
       }
     }
-    if ((rc = build_index(c, bgn, eb, !c->sq.on)) == OVL_ERR_OOM) {
+    const bool bloom = !c->sq.on || sq_bloom();
+    if ((rc = build_index(c, bgn, eb, bloom)) == OVL_ERR_OOM) {
       // the previous batch's search buffers make room (the next search grows them again)
       release_find_buffers(c);
-      rc = build_index(c, bgn, eb, !c->sq.on);
+      rc = build_index(c, bgn, eb, bloom);
     }
     if (rc) return rc;
     if (!load_may_cut) break;
@@ -1392,11 +1401,23 @@ static bool use_bloom(const ovl_ctx *c, uint32_t bgn, uint32_t end) {
 // radix-sorted once, in runs of <= 2^29 windows.  A batch searches the units of the reads
 // below its last hash read: a prefix of them, so per run a window-id bound.  Off (and the
 // random-lookup probe used) when the keys would take more than half the free HBM.
-static void sq_release(ovl_ctx *c) {
+//
+// The device arrays outlive the job (free_mem false at a job's end): they are grow-only like
+// the search buffers, since hipMalloc of the ~58 GB a configs[4] rank job sorts takes ~1.7 s
+// here (profiles/r04s_chain_occ_c4_sq.txt) -- the keys themselves are recomputed and sorted by
+// every job.
+static size_t sq_held_bytes(const ovl_ctx *c) {
+  const auto &Q = c->sq;
+  return 8 * (Q.key.n + Q.key2.n + Q.dwbase.n) + 4 * (Q.wid.n + Q.wid2.n + Q.ublk.n + Q.uhits.n +
+         Q.uflags.n) + Q.tmp.n + sizeof(Unit) * Q.dunits.n;
+}
+static void sq_release(ovl_ctx *c, bool free_mem) {
   auto &Q = c->sq;
   Q.on = false;
-  Q.key.release(); Q.key2.release(); Q.wid.release(); Q.wid2.release(); Q.ublk.release();
-  Q.dwbase.release(); Q.dunits.release(); Q.tmp.release(); Q.uhits.release(); Q.uflags.release();
+  if (free_mem) {
+    Q.key.release(); Q.key2.release(); Q.wid.release(); Q.wid2.release(); Q.ublk.release();
+    Q.dwbase.release(); Q.dunits.release(); Q.tmp.release(); Q.uhits.release(); Q.uflags.release();
+  }
   Q.units.clear(); Q.ureadiid.clear(); Q.uwin.clear(); Q.wb.clear(); Q.runs.clear();
   Q.probed = -1;
 }
@@ -1405,7 +1426,7 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   auto &Q = c->sq;
   if (Q.on && Q.ref_bgn == bgn && Q.ref_end == end && Q.lib_lo == lib_lo && Q.lib_hi == lib_hi)
     return OVL_OK;
-  sq_release(c);
+  sq_release(c, false);
   const uint32_t k = c->P.kmer_len;
   for (uint32_t a = bgn; a <= end && a >= bgn; a++) {         // find_impl's unit rule
     const uint32_t r = a - c->first_iid;
@@ -1449,8 +1470,9 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
     fprintf(stderr, "OVL_TIMING sorted query windows: %u units, %llu windows in %zu runs, "
             "%.1f GB needed, %.1f GB free\n", nu, (unsigned long long)total, Q.runs.size(),
             need / 1e9, fr / 1e9);
-  // up to half the free HBM (the configs[4] rank-0 job at 1/8 scale: 3.8 G windows, 67 GB)
-  if (need > fr / 2) { sq_release(c); return OVL_OK; }
+  // up to half the free HBM (the configs[4] rank-0 job at 1/8 scale: 3.8 G windows, 67 GB),
+  // counting what an earlier job's arrays hold as free
+  if (need > (fr + sq_held_bytes(c)) / 2) { sq_release(c); return OVL_OK; }
   hipStream_t s = c->stream;
   const auto t0 = std::chrono::steady_clock::now();
   size_t tmpb = 0;
@@ -1524,10 +1546,6 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
     }
   }
   HIPC(hipStreamSynchronize(s));
-  // the sort buffers go: only the sorted runs stay for the job
-  Q.key2.release();
-  Q.wid2.release();
-  Q.tmp.release();
   Q.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (getenv("OVL_TIMING"))
     fprintf(stderr, "OVL_TIMING sorted query windows: sorted in %.1f ms (%u runs sorted again "
@@ -2272,6 +2290,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         HIPC(hipMemsetAsync(Q.uflags.p + R.u0, 0, 4ull * (ue - R.u0), s));
         SqProbeArgs SA;
         SA.X = index_dev(c);
+        if (c->bloom_ok && sq_bloom()) {        // the filter in front of the table
+          SA.X.bloom = c->d_bloom.p;
+          SA.X.bloom_w = c->bloom_w;
+        }
         SA.R = c->reads();
         SA.key = Q.key.p + R.e0;
         SA.wid = Q.wid.p + R.e0;
@@ -2778,16 +2800,18 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
   uint64_t batches = 0;
   // the query windows sorted once for the job's batches (sq_prepare): OVL_SQ=2 from the
-  // second batch on, 1 from the first, 0 (the default) never.  Off by default: on the
-  // configs[4] rank-0 job the sorted probe takes 456 instead of 654 ms, but sorting the job's
-  // 3.8 G windows over all 64 key bits costs ~310 ms (seed 1,141 vs 1,030 ms,
-  // profiles/r04m_c4_sq*.json); a partial-range sort would pay, and this ROCm's returned
-  // wrong orders.  They are the job's own work: released at its end.
-  int sq_mode = 0;
+  // second batch on, 1 from the first, 0 never, 3 (the default) from the first when the first
+  // batch's size puts the job at SQ_AUTO_BATCHES batches or more.  The sort costs several
+  // random-lookup probes of the same windows (the configs[4] rank-0 job at 1/8 scale, 14
+  // batches: sort 134 ms, seed 847 against 892 ms; profiles/r04y_c4_*.log), so a job of a few
+  // batches keeps the random-lookup probe.
+  const uint64_t SQ_AUTO_BATCHES = 10;
+  int sq_mode = 3;
   if (const char *e = getenv("OVL_SQ")) sq_mode = atoi(e);
+  bool sq_auto = false;
   struct SqOff {
     ovl_ctx *c;
-    ~SqOff() { c->sq_request = false; sq_release(c); }
+    ~SqOff() { c->sq_request = false; sq_release(c, false); }
   } sq_off{c};
   while (bgn < g_end_hash) {                                             // :222
     if (end > g_end_hash) end = g_end_hash;
@@ -2802,7 +2826,11 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
       // the batches' pairs are extended together: the last batch flushes what is pending
       uint64_t n = 0;
       const bool last_batch = !(end + 1 < g_end_hash);
-      c->sq_request = sq_mode == 1 || (sq_mode == 2 && batches >= 2);
+      if (sq_mode == 3 && batches == 1) {        // the job's batches, from the first one's reads
+        const uint64_t per = std::max<uint64_t>((uint64_t)end + 1 - bgn, 1);
+        sq_auto = (uint64_t)g_end_hash + 1 - g_bgn_hash >= SQ_AUTO_BATCHES * per;
+      }
+      c->sq_request = sq_mode == 1 || (sq_mode == 2 && batches >= 2) || sq_auto;
       if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n,
                           last_batch)))
         return rc;

@@ -690,6 +690,15 @@ __device__ __forceinline__ double uni(double v) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// Extend_Alignment's kind is DOVETAIL only when both of its extensions match to an end
+// (prefixEditDistance-extend.C:207), and Process_Matches reads nothing of any other result
+// but its kind unless partial overlaps are on (Process_String_Overlaps.C:500, :520).  So an
+// extension that stops short of the end needs no traceback, and after a forward one that
+// did the reverse one is not run (extend_alignment).  1: skip both; 0: compute them.
+#ifndef OVL_SKIP_MOOT_REVERSE
+#define OVL_SKIP_MOOT_REVERSE 0
+#endif
+
 // The row loop stays a call: inlined into process_pair (always_inline) the kernel keeps 80
 // VGPRs but spills 576 B per lane inside the loop -- extension 218 -> 297 ms (+37 %) on the
 // 10k-read job (r02v A/B).
@@ -1153,6 +1162,12 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     out.mte = 0;
     tb_e = max_score_best_e; tb_d = max_score_best_d;
   }
+#if OVL_SKIP_MOOT_REVERSE
+  if (out.mte == 0 && !partial) {              // not a dovetail end: the deltas are unread
+    out.nd = -1;
+    return out;
+  }
+#endif
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
@@ -1279,6 +1294,18 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
   }
   S_Hi += S_Right_Begin - 1;
   T_Hi += T_Right_Begin - 1;
+
+  // a forward extension that stopped short of the end leaves the reverse one unread (see
+  // OVL_SKIP_MOOT_REVERSE)
+#if OVL_SKIP_MOOT_REVERSE
+  if (!rmte && !X.partial) {
+    r.kind = K_NONE;
+    r.Errors = 0;
+    r.S_Lo = r.S_Hi = r.T_Lo = r.T_Hi = 0;
+    r.ld_len = 0;
+    return r;
+  }
+#endif
 
   if (S_Left_Begin < 0 || T_Left_Begin < 0) {
     S_Lo = 0; T_Lo = 0; lmte = 1;

@@ -295,6 +295,21 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
       w[q] = i < A.n ? A.wid[i] : 0xFFFFFFFFu;
       M[q] = i < A.n ? A.key[i] : 0ull;
     }
+    // the batch's Bloom filter first (when it has one): most windows miss the batch, and a
+    // miss read from the table is a linear probe to the slice's next empty slot -- dependent
+    // loads -- where the filter rejects it with one load (sorted keys: few lines per wave)
+    if (A.X.bloom) {
+      uint64_t bw[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        bw[q] = w[q] < A.wlim ? A.X.bloom[bloom_word(M[q] >> shift, A.X.slice_bits, M[q],
+                                                     A.X.bloom_w)] : 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint64_t bm = bloom_mask(M[q]);
+        if ((bw[q] & bm) != bm) w[q] = 0xFFFFFFFFu;
+      }
+    }
     TabEntry t[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
