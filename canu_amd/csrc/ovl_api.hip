@@ -1340,7 +1340,24 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
       if (entries >= entry_limit) { el = bgn + i; reached = true; break; }
     }
     if (reached) {
-      if (el < eb && (rc = build_index(c, bgn, el, !c->sq.on))) return rc;
+      if (el < eb) {
+        // the prefix's index cut down to the batch (k_cut_index), or built again over it
+        static const bool cut = !getenv("OVL_CUT_FILTER") || atoi(getenv("OVL_CUT_FILTER")) != 0;
+        if (cut) {
+          HIPC(hipEventRecord(c->ev[0], s));
+          hipLaunchKernelGGL(k_cut_index, dim3(8 * c->n_cu), dim3(256), 0, s, c->d_tab.p,
+                             1ull << c->tab_bits, (const uint64_t *)c->d_occ.p, el);
+          HIPC(hipGetLastError());
+          HIPC(hipEventRecord(c->ev[1], s));
+          HIPC(hipStreamSynchronize(s));
+          float ms = 0;
+          (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+          c->stats.ms_index += ms;
+          c->hash_end_iid = el;
+        } else if ((rc = build_index(c, bgn, el, bloom))) {
+          return rc;
+        }
+      }
       e = el;
       uint64_t cw = 0;
       for (uint32_t id = bgn; id <= el; id++) {

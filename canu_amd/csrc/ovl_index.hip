@@ -726,6 +726,31 @@ __global__ void __launch_bounds__(1024) k_first_reads_lds(const uint64_t *__rest
   }
 }
 
+// A load-cut batch (Build_Hash_Index.C:495-541: the table load stops the batch at read
+// `last`) from the index of a longer prefix: every k-mer's occurrence run is position-
+// descending, so its occurrences in reads past `last` lead the run -- the entry skips them.
+// A k-mer left with none keeps its slot (probe sequences stay intact) with an empty run,
+// which every lookup reads as the miss it is in the cut batch's own index ({off 0, cnt 0},
+// the record a miss writes).  Skip k-mer entries are kept as they are.  The Bloom filter
+// keeps the prefix's k-mers: a superset, so still exact.
+__global__ void k_cut_index(TabEntry *tab, uint64_t nslots, const uint64_t *__restrict__ occ,
+                            uint32_t last) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = tab[i].cnt;
+    if (c == 0 || (c & OVL_FLAG_SKIP)) continue;
+    const uint32_t off = tab[i].off, n = c & OVL_CNT_MASK;
+    uint32_t lo = 0, hi = n;                     // first occurrence in a read <= last
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((uint32_t)(occ[off + mid] >> 32) > last) lo = mid + 1; else hi = mid;
+    }
+    if (lo == 0) continue;
+    tab[i].off = lo < n ? off + lo : 0u;
+    tab[i].cnt = (c & ~OVL_CNT_MASK) | (n - lo);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Small utilities
 
