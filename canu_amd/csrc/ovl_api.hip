@@ -1908,7 +1908,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0, nodes_tot = 0;
   uint64_t staged_pairs = 0, long_pairs = 0, generic_pairs = 0;
   uint32_t chain_retries = 0;
-  uint32_t n_probe_launch = 0, n_ext_launch = 0;
+  uint32_t n_probe_launch = 0, n_ext_launch = 0, n_probe_sorted = 0;
   uint32_t nu = (uint32_t)units.size();
   uint32_t u0 = 0;
   const uint32_t ctr_next[4] = {5, 11, 13, 15}, ctr_defer[4] = {8, 12, 14, 10};
@@ -2302,7 +2302,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       if (Q.probed != (int)sq_run) {
         const uint64_t wlim = Q.wb[R.wb0 + (ue - R.u0)];
         if (d_probe.grow(R.n)) return fail(OVL_ERR_OOM, "probe records (%llu)", (unsigned long long)R.n);
-        HIPC(hipEventRecord(c->ev[2], s));
         HIPC(hipMemsetAsync(d_probe.p, 0, 8ull * wlim, s));
         HIPC(hipMemsetAsync(Q.uflags.p + R.u0, 0, 4ull * (ue - R.u0), s));
         SqProbeArgs SA;
@@ -2322,12 +2321,16 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         SA.k = k;
         SA.out = d_probe.p;
         SA.unit_flags = Q.uflags.p + R.u0;
+        // the kernel alone is timed (the records' zeroing and the unit hit counts around it
+        // are not the probe's bytes)
+        HIPC(hipEventRecord(c->ev[2], s));
         hipLaunchKernelGGL(k_probe_sorted, dim3(8 * c->n_cu), dim3(256), 0, s, SA);
+        HIPC(hipEventRecord(c->ev[3], s));
         n_probe_launch++;
+        n_probe_sorted++;
         hipLaunchKernelGGL(k_sq_unit_hits, dim3((ue - R.u0 + 3) / 4), dim3(256), 0, s, d_probe.p,
                            Q.dwbase.p + R.wb0, ue - R.u0, Q.uhits.p + R.u0);
         HIPC(hipGetLastError());
-        HIPC(hipEventRecord(c->ev[3], s));
         sq_uh.resize(ue - R.u0);
         HIPC(hipMemcpyAsync(sq_uh.data(), Q.uhits.p + R.u0, 4ull * (ue - R.u0),
                             hipMemcpyDeviceToHost, s));
@@ -2335,9 +2338,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         float t = 0;
         (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
         ms_probe += t;
-        // algorithmic bytes: the sorted windows (8-B key + 4-B id), the table read once, a
-        // record written for every searched window (the zeroing and the hits)
-        probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) + 8ull * wlim;
+        // algorithmic bytes: the sorted windows (8-B key + 4-B id) and the table and its
+        // filter read once each (the hits' 8-B records on top are not counted)
+        probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) +
+                       (SA.X.bloom ? 8ull * ((1ull << (c->tab_bits - c->slice_bits)) << c->bloom_w) : 0ull);
         Q.probed = (int)sq_run;
       }
       nb = ue - u0;
@@ -2637,6 +2641,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   c->stats.ms_probe_kernel += ms_probe;
   c->stats.probe_bytes += probe_bytes;
   c->stats.probe_launches += n_probe_launch;
+  c->stats.probe_sorted_launches += n_probe_sorted;
   c->stats.extend_launches += n_ext_launch;
   *n_out = c->nout;
   return OVL_OK;

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 5
+#define OVL_ABI_VERSION 6
 
 typedef enum {
   OVL_OK               =  0,
@@ -234,6 +234,9 @@ typedef struct {
   uint32_t long_stage_len;         /* longest read of the long-read class (0: none)      */
   uint64_t seed_nodes;             /* match nodes (Add_Match lists) handed to the extension
                                       (ABI 3) */
+  uint32_t probe_sorted_launches;  /* of probe_launches: the sorted-window probe
+                                      (k_probe_sorted, ABI 6); its ms_probe_kernel and
+                                      probe_bytes are that kernel's alone */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

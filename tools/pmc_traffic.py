@@ -34,7 +34,8 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-SHORT = {"k_extend": "k_extend", "k_probe": "k_probe", "k_chain": "k_chain",
+SHORT = {"k_extend": "k_extend", "k_probe": "k_probe", "k_probe_sorted": "k_probe_sorted",
+         "k_chain": "k_chain",
          "k_fine": "k_fine", "k_table": "k_table", "k_coarse_scatter": "k_coarse_scatter",
          "k_coarse_hist": "k_coarse_hist", "k_pack": "k_pack"}
 
