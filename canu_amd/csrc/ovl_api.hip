@@ -1905,6 +1905,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     return rc;
 
   float ms_probe = 0, ms_chain = 0, ms_ext = 0;
+  float ms_probe_rest = 0;        // the sorted-window probe step's work beside its kernel
   uint64_t npairs_tot = 0, probe_bytes = 0, seed_hits_tot = 0, n_big_units = 0, nodes_tot = 0;
   uint64_t staged_pairs = 0, long_pairs = 0, generic_pairs = 0;
   uint32_t chain_retries = 0;
@@ -2302,6 +2303,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       if (Q.probed != (int)sq_run) {
         const uint64_t wlim = Q.wb[R.wb0 + (ue - R.u0)];
         if (d_probe.grow(R.n)) return fail(OVL_ERR_OOM, "probe records (%llu)", (unsigned long long)R.n);
+        HIPC(hipEventRecord(c->ev[4], s));           // the probe step: seed-phase time
         HIPC(hipMemsetAsync(d_probe.p, 0, 8ull * wlim, s));
         HIPC(hipMemsetAsync(Q.uflags.p + R.u0, 0, 4ull * (ue - R.u0), s));
         SqProbeArgs SA;
@@ -2331,13 +2333,16 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         hipLaunchKernelGGL(k_sq_unit_hits, dim3((ue - R.u0 + 3) / 4), dim3(256), 0, s, d_probe.p,
                            Q.dwbase.p + R.wb0, ue - R.u0, Q.uhits.p + R.u0);
         HIPC(hipGetLastError());
+        HIPC(hipEventRecord(c->ev[5], s));
         sq_uh.resize(ue - R.u0);
         HIPC(hipMemcpyAsync(sq_uh.data(), Q.uhits.p + R.u0, 4ull * (ue - R.u0),
                             hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
-        float t = 0;
+        float t = 0, tstep = 0;
         (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+        (void)hipEventElapsedTime(&tstep, c->ev[4], c->ev[5]);
         ms_probe += t;
+        ms_probe_rest += tstep > t ? tstep - t : 0.f;  // zeroing + unit hit counts
         // algorithmic bytes: the sorted windows (8-B key + 4-B id) and the table and its
         // filter read once each (the hits' 8-B records on top are not counted)
         probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) +
@@ -2636,7 +2641,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   c->stats.bad_long_window += hs[9];
   c->stats.pairs += npairs_tot;
   c->stats.seed_nodes += nodes_tot;
-  c->stats.ms_seed += ms_probe + ms_chain;
+  c->stats.ms_seed += ms_probe + ms_probe_rest + ms_chain;
   c->stats.ms_extend += ms_ext;
   c->stats.ms_probe_kernel += ms_probe;
   c->stats.probe_bytes += probe_bytes;
