@@ -101,6 +101,12 @@ def main() -> None:
     backend = os.environ.get("CANU_DIST_BACKEND", "nccl")
 
     import torch
+    dev = torch.device("cuda", local)
+    job = (Configs4Rank if args.workload == "configs4-rank" else Configs2)(args, rank, world, dev)
+    # the read set is generated on the host before anything touches the GPU: its generator
+    # may fork a worker pool, which must not happen after GPU initialisation
+    t_setup = time.time()
+    job.generate()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -110,7 +116,8 @@ def main() -> None:
         else:
             dist.init_process_group(backend)
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
-    dev = torch.device("cuda", local)
+    job.dist = dist
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
     red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     def reduce(v, op, dtype):
@@ -119,12 +126,6 @@ def main() -> None:
             dist.all_reduce(t, op=op)
         return t.item()
 
-    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
-    if args.workload == "configs4-rank":
-        job = Configs4Rank(args, rank, world, dist, dev)
-    else:
-        job = Configs2(args, rank, world, dist, dev)
-    t_setup = time.time()
     job.setup(OicParameters, OverlapInCore)
     setup_s = time.time() - t_setup
     oic = job.oic
@@ -217,8 +218,9 @@ def main() -> None:
 class Configs2:
     """BASELINE configs[2]: the all-vs-all job over one index, query shards per rank."""
 
-    def __init__(self, args, rank, world, dist, dev):
-        self.args, self.rank, self.world, self.dist, self.dev = args, rank, world, dist, dev
+    def __init__(self, args, rank, world, dev):
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        self.dist = None
 
     def release(self):
         """Drop the device copies of the read store (the context is closed by the caller)."""
@@ -230,18 +232,23 @@ class Configs2:
                 "coverage": a.coverage, "read_error": a.read_error, "seed": a.seed, "k": a.k,
                 "maxerate": float(np.float32(a.maxerate)), "minlength": a.minlength}
 
-    def setup(self, OicParameters, OverlapInCore):
-        import torch
+    def generate(self):
+        """This rank's slice of the read set, on the host (no GPU call)."""
         from canu_amd.synth import synth_reads, random_genome
-        from canu_amd.dist import gather_read_store, query_shards
         a, n = self.args, self.args.reads
         genome_len = int(n * a.read_len / a.coverage)
         genome = random_genome(np.random.default_rng(a.seed), genome_len)
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world
-        part = synth_reads(n_reads=n, read_len=a.read_len, genome_len=genome_len,
-                           error_rate=a.read_error, seed=a.seed, genome=genome,
-                           read_range=(lo, hi))
+        self._part = synth_reads(n_reads=n, read_len=a.read_len, genome_len=genome_len,
+                                 error_rate=a.read_error, seed=a.seed, genome=genome,
+                                 read_range=(lo, hi))
+
+    def setup(self, OicParameters, OverlapInCore):
+        import torch
+        from canu_amd.dist import gather_read_store, query_shards
+        a, n = self.args, self.args.reads
+        part, self._part = self._part, None
         if self.world == 1:
             bases = torch.from_numpy(part.bases).to(self.dev)
             lengths = part.lengths
@@ -398,17 +405,16 @@ class Configs4Rank(Configs2):
                 "maxerate": float(np.float32(a.maxerate)), "minlength": a.minlength,
                 "rank_job": a.rank_job}
 
-    def setup(self, OicParameters, OverlapInCore):
-        import torch
+    def generate(self):
+        """This rank's slice of the read set, on the host before any GPU call (the
+        generator's worker pool is forked here)."""
         from canu_amd.synth import synth_reads_parallel
-        from canu_amd.dist import gather_read_store, hash_block_jobs
         a, n = self.args, self.args.reads
         genome_len = int(n * a.read_len / a.coverage)
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world
         # CANU_C4_READS_CACHE=<dir> (one rank): the read set saved there once and loaded by
-        # later runs -- the PMC passes run under rocprofv3, whose signal handling hangs the
-        # generator's worker pool (tools/c4_cache.py writes it)
+        # later runs (saves the generation's ~10 s in repeated PMC passes)
         cache = os.environ.get("CANU_C4_READS_CACHE") if self.world == 1 else None
         key = f"c4_{n}_{a.read_len}_{a.coverage}_{a.read_error}_{a.seed}"
         if cache and os.path.exists(os.path.join(cache, key + "_lengths.npy")):
@@ -426,6 +432,13 @@ class Configs4Rank(Configs2):
                 os.makedirs(cache, exist_ok=True)
                 np.save(os.path.join(cache, key + "_bases.npy"), part.bases)
                 np.save(os.path.join(cache, key + "_lengths.npy"), part.lengths)
+        self._part = part
+
+    def setup(self, OicParameters, OverlapInCore):
+        import torch
+        from canu_amd.dist import gather_read_store, hash_block_jobs
+        a, n = self.args, self.args.reads
+        part, self._part = self._part, None
         if self.world == 1:
             bases = torch.from_numpy(part.bases).to(self.dev)
             lengths = part.lengths

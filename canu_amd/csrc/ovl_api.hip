@@ -216,9 +216,6 @@ struct ovl_ctx {
     DBuf<uint64_t> hcnt, hbase;              // ovl_seed_hits: per-unit hit counts / bases
     DBuf<uint4> hbuf;                        // ovl_seed_hits: one piece of the hit list
     DBuf<uint32_t> oa, ob, ucnt, useg;
-    DBuf<uint64_t> shk[2];                   // shared-strand order: keys, sorted keys
-    DBuf<uint32_t> shi[2], shw, seg, nseg;   // pair indices (sorted), unit work, groups
-    DBuf<uint8_t> shf, shtmp;                // group-start flags, hipcub scratch
     DBuf<Node> pool, pnodes[2];
     DBuf<PairRec> pairs[2];
     DBuf<unsigned long long> stats;
@@ -265,7 +262,8 @@ struct ovl_ctx {
     DBuf<Unit> dunits;
     DBuf<uint8_t> tmp;
     DBuf<uint32_t> uhits, uflags;
-    uint32_t resorted = 0;       // runs whose partial-range sort came back unordered
+    DBuf<unsigned long long> sig;   // a run's (key, wid) signatures before / after its sort + flag
+    uint32_t resorted = 0;       // runs whose partial-range sort failed its check
     int probed = -1;             // the run whose records fb.probe holds for this batch
     uint32_t probed_nu = 0;      // ... for this many of its units
     double ms_sort = 0;
@@ -602,36 +600,6 @@ static int load_common(ovl_ctx *c, uint32_t first_iid, uint32_t nreads, const ui
 
 // Work-order keys for the extension queue: a pair's match-node count (its extension work
 // grows with it), so the longest pairs start first and the kernel's tail is short.
-// The shared-strand kernel's work order (k_extend<.., SH>): pairs grouped by unit, units by
-// descending work (their pairs' node counts summed), a unit's pairs by descending node count
-// -- one 64-bit key: [~work 20 | unit 28 | ~nodes 16] sorted ascending (work clamped: ties
-// only reorder units).
-__global__ void k_sh_unit_work(const PairRec *pairs, uint32_t n, uint32_t *uwork) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicAdd(&uwork[pairs[i].unit], pairs[i].node_cnt);
-}
-
-__global__ void k_sh_keys(const PairRec *pairs, uint32_t n, const uint32_t *uwork,
-                          uint64_t *keys, uint32_t *idx) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const PairRec P = pairs[i];
-    const uint64_t w = std::min<uint32_t>(uwork[P.unit], 0xFFFFFu);
-    const uint64_t nc = std::min<uint32_t>(P.node_cnt, 0xFFFFu);
-    keys[i] = ((0xFFFFFull - w) << 44) | ((uint64_t)P.unit << 16) | (0xFFFFull - nc);
-    idx[i] = i;
-  }
-}
-
-// first position of every unit group in the sorted keys (bits 16.. differ from the previous)
-__global__ void k_sh_flags(const uint64_t *keys, uint32_t n, uint8_t *flags) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    flags[i] = (i == 0 || (keys[i] >> 16) != (keys[i - 1] >> 16)) ? 1 : 0;
-}
-
-__global__ void k_sh_seg_end(uint32_t *seg, const uint32_t *nseg, uint32_t n) {
-  seg[*nseg] = n;
-}
-
 __global__ void k_pair_order_keys(const PairRec *pairs, uint32_t n, uint32_t *keys,
                                   uint32_t *idx) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -986,11 +954,8 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = fals
   }
   {
     // the sort phase: runs grouped in an LDS hash table, records in registers (cap / 64 per
-    // lane); bitonic sorts when the grouped layout would not fit a CU's LDS (cap 1024) or
-    // when OVL_FINE_BITONIC=1 (A/B)
-    const char *fb_env = getenv("OVL_FINE_BITONIC");
-    const bool group = !(fb_env && atoi(fb_env)) &&
-                       fine_lds_bytes(true, nfb, F.cap) + 256 <= 160 * 1024;
+    // lane); bitonic sorts when the grouped layout would not fit a CU's LDS (cap 1024)
+    const bool group = fine_lds_bytes(true, nfb, F.cap) + 256 <= 160 * 1024;
     const size_t fine_lds = fine_lds_bytes(group, nfb, F.cap);
     const void *kf =
         !group           ? reinterpret_cast<const void *>(k_fine<1, false>)
@@ -1175,9 +1140,7 @@ static void release_find_buffers(ovl_ctx *c) {
   f.ok64a.release(); f.ok64b.release(); f.dkey.release(); f.oa.release(); f.ob.release();
   f.ucnt.release(); f.useg.release(); f.hcnt.release(); f.hbase.release(); f.hbuf.release();
   f.rows.release(); f.rowdir.release(); f.deltas.release();
-  for (int i = 0; i < 2; i++) { f.shk[i].release(); f.shi[i].release(); }
   sq_release(c);
-  f.shw.release(); f.seg.release(); f.nseg.release(); f.shf.release(); f.shtmp.release();
   // the extension accumulator's buffers, once nothing waits in them
   if (c->acc.np == 0) {
     c->acc.units.release(); c->acc.pnodes.release(); c->acc.pairs.release();
@@ -1434,6 +1397,7 @@ static void sq_release(ovl_ctx *c, bool free_mem) {
   if (free_mem) {
     Q.key.release(); Q.key2.release(); Q.wid.release(); Q.wid2.release(); Q.ublk.release();
     Q.dwbase.release(); Q.dunits.release(); Q.tmp.release(); Q.uhits.release(); Q.uflags.release();
+    Q.sig.release();
   }
   Q.units.clear(); Q.ureadiid.clear(); Q.uwin.clear(); Q.wb.clear(); Q.runs.clear();
   Q.probed = -1;
@@ -1498,8 +1462,11 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   // partial bit range of 64-bit keys returned duplicated ids and an unsorted order below
   // ~1.4 M items (tools/sortcheck.hip: 100 k and 882,524 items wrong for [32|40|48, 64),
   // 1.44 M to 2^27 right; profiles/r04n_sortcheck.log), so runs under PART_MIN windows sort
-  // all 64 bits, and a partially sorted run is checked (k_sq_sorted_check) and sorted again
-  // over all bits if its order is broken.
+  // all 64 bits, and a partially sorted run is checked on both properties that broke
+  // (k_sq_sorted_check: key order, and the (key, wid) multiset against k_sq_keys' signature)
+  // and sorted again over all bits if either fails.  OVL_TEST_SQ_CORRUPT=1 (tests) checks
+  // every run and duplicates a window id in the first run's sorted output, so the fallback
+  // path runs.
   const uint64_t PART_MIN = 1ull << 22;
   const int PART_LO = 40;
   {
@@ -1522,10 +1489,11 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   if (Q.key.alloc(total) || Q.wid.alloc(total) || Q.key2.alloc(maxrun) || Q.wid2.alloc(maxrun) ||
       Q.tmp.alloc(std::max<size_t>(tmpb, 1)) || Q.dwbase.alloc(Q.wb.size()) ||
       Q.dunits.alloc(nu) || Q.ublk.alloc(std::max<size_t>(ublk.size(), 1)) ||
-      Q.uhits.alloc(nu) || Q.uflags.alloc(nu)) {
+      Q.uhits.alloc(nu) || Q.uflags.alloc(nu) || Q.sig.alloc(5)) {
     sq_release(c);
     return OVL_OK;                                 // no room: the random-lookup probe
   }
+  const bool test_corrupt = getenv("OVL_TEST_SQ_CORRUPT") && atoi(getenv("OVL_TEST_SQ_CORRUPT"));
   HIPC(hipMemcpyAsync(Q.dwbase.p, Q.wb.data(), 8ull * Q.wb.size(), hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(Q.dunits.p, Q.units.data(), sizeof(Unit) * nu, hipMemcpyHostToDevice, s));
   if (!ublk.empty())
@@ -1540,28 +1508,47 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
     KA.kmask = (1ull << (2 * k)) - 1;
     KA.key = Q.key2.p;
     KA.wid = Q.wid2.p;
-    hipLaunchKernelGGL(k_sq_keys, dim3((KA.nunits + 3) / 4), dim3(256), 0, s, KA);
-    HIPC(hipGetLastError());
-    size_t tb = tmpb;
-    const int lo = R.n >= PART_MIN ? PART_LO : 0;
-    HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
-                                            Q.wid.p + R.e0, (int)R.n, lo, 64, s));
-    if (lo) {
-      HIPC(hipMemsetAsync(Q.uhits.p, 0, 4, s));      // a flag word (uhits is filled later)
+    KA.sig = Q.sig.p;
+    // keys, sort, and (partial-range runs) the check; with `bits_lo` 0 the sort is over all bits
+    auto sort_run = [&](int bits_lo, bool corrupt) -> int {
+      HIPC(hipMemsetAsync(Q.sig.p, 0, 5 * sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_sq_keys, dim3((KA.nunits + 3) / 4), dim3(256), 0, s, KA);
+      HIPC(hipGetLastError());
+      size_t tb = tmpb;
+      HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
+                                              Q.wid.p + R.e0, (int)R.n, bits_lo, 64, s));
+      if (corrupt && R.n >= 2)
+        HIPC(hipMemcpyAsync(Q.wid.p + R.e0 + 1, Q.wid.p + R.e0, 4, hipMemcpyDeviceToDevice, s));
+      return OVL_OK;
+    };
+    auto check_run = [&](int bits_lo, bool *broken) -> int {
       hipLaunchKernelGGL(k_sq_sorted_check, dim3(4 * c->n_cu), dim3(256), 0, s,
-                         (const uint64_t *)(Q.key.p + R.e0), R.n, (uint32_t)lo, Q.uhits.p);
-      uint32_t broken = 0;
-      HIPC(hipMemcpyAsync(&broken, Q.uhits.p, 4, hipMemcpyDeviceToHost, s));
+                         (const uint64_t *)(Q.key.p + R.e0), (const uint32_t *)(Q.wid.p + R.e0),
+                         R.n, (uint32_t)bits_lo, Q.sig.p, (uint32_t *)(Q.sig.p + 4));
+      HIPC(hipGetLastError());
+      unsigned long long h[5] = {0, 0, 0, 0, 0};
+      HIPC(hipMemcpyAsync(h, Q.sig.p, sizeof(h), hipMemcpyDeviceToHost, s));
       HIPC(hipStreamSynchronize(s));
+      *broken = (uint32_t)h[4] != 0 || h[0] != h[2] || h[1] != h[3];
+      return OVL_OK;
+    };
+    const int lo = R.n >= PART_MIN ? PART_LO : 0;
+    const bool corrupt = test_corrupt && &R == &Q.runs[0];
+    if (int rc = sort_run(lo, corrupt)) return rc;
+    if (lo || test_corrupt) {
+      bool broken = false;
+      if (int rc = check_run(lo, &broken)) return rc;
       if (broken) {                                  // the keys again, every bit sorted
-        hipLaunchKernelGGL(k_sq_keys, dim3((KA.nunits + 3) / 4), dim3(256), 0, s, KA);
-        tb = tmpb;
-        HIPC(hipcub::DeviceRadixSort::SortPairs(Q.tmp.p, tb, Q.key2.p, Q.key.p + R.e0, Q.wid2.p,
-                                                Q.wid.p + R.e0, (int)R.n, 0, 64, s));
+        if (int rc = sort_run(0, false)) return rc;
+        if (int rc = check_run(0, &broken)) return rc;
+        if (broken)
+          return fail(OVL_ERR_HIP, "sorted query windows: run of %llu windows failed its check "
+                      "after a full-range sort", (unsigned long long)R.n);
         Q.resorted++;
       }
     }
   }
+  c->stats.sq_resorted += Q.resorted;
   HIPC(hipStreamSynchronize(s));
   Q.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (getenv("OVL_TIMING"))
@@ -1691,16 +1678,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   auto sw_of = [](uint64_t L) { return (int32_t)(((L + 31) / 32 + 2) & ~1ull); };
   auto stg_lds_of = [&](uint64_t L) { return 4ull * (4ull * (uint64_t)sw_of(L) + OVL_SCR_STAGE); };
   auto ml_of = [](int32_t ec) { return 4ull * (((uint64_t)(ec + 2) + 3) & ~3ull); };
-  // the staged kernel's block-shared Edit_Match_Limit table (none with OVL_GML)
-  auto sml_of = [&](int32_t ec) { return OVL_GML ? 0ull : ml_of(ec); };
+  // the staged kernel's block-shared Edit_Match_Limit table
+  auto sml_of = [&](int32_t ec) { return ml_of(ec); };
   auto fits = [&](uint64_t L, uint32_t wpb, size_t cap) {
     return stg_lds_of(L) * wpb + sml_of(ecap_of(L)) <= cap;
-  };
-  // the shared-strand block: Edit_Match_Limit table, slot control, OVL_SH_SLOTS query
-  // strands, then per wave its target strand and scratch (k_extend<.., SH>)
-  auto sh_lds_of = [&](uint64_t L, uint32_t wpb) -> size_t {
-    return ml_of(ecap_of(L)) + OVL_SH_SLOTS * sizeof(ShSlot) + 16 +
-           8ull * OVL_SH_SLOTS * (uint64_t)sw_of(L) + wpb * (8ull * (uint64_t)sw_of(L) + 4ull * OVL_SCR);
   };
   auto longest_fitting = [&](uint32_t wpb, size_t cap) -> uint32_t {
     uint64_t lo = 0, hi = c->max_len;
@@ -1718,16 +1699,9 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     bool l16 = false;
     uint64_t stride = 0;
     bool wide = false;             // the 2 x OVL_RJ-chunk register window (wide bands)
-    bool sh = false;               // the block-shared query strand (first class only)
   };
   // the staged kernel instance of a class
-  auto stage_kernel = [](bool l16, bool wide, bool sh = false) -> const void * {
-#if OVL_SH_BUILD
-    if (sh) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, OVL_RJ, true>)
-                       : reinterpret_cast<const void *>(k_extend<true, false, false, OVL_RJ, true>);
-#else
-    (void)sh;
-#endif
+  auto stage_kernel = [](bool l16, bool wide) -> const void * {
     if (wide) return l16 ? reinterpret_cast<const void *>(k_extend<true, true, false, 2 * OVL_RJ>)
                          : reinterpret_cast<const void *>(k_extend<true, false, false, 2 * OVL_RJ>);
     return l16 ? reinterpret_cast<const void *>(k_extend<true, true>)
@@ -1738,24 +1712,16 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   auto per_wave_bytes = [](const ExtClass &g) {
     return g.stride * 4 + 16ull * (g.ecap + 2) + 28ull * (g.ecap + 8);
   };
-  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob, bool wide = false,
-                        bool sh = false) -> int {
+  auto make_stage = [&](uint32_t L, size_t cap, bool allow_knob, bool wide = false) -> int {
     ExtClass g;
     g.len = L;
     g.wide = wide;
-    g.sh = sh;
     g.ecap = ecap_of(L);
     g.sw = sw_of(L);
     g.l16 = L < 16384;
-    if (sh) {
-      g.wpb = 8;
-      g.lds = sh_lds_of(L, g.wpb);
-      if (g.lds > cap) return -1;
-    } else {
-      g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, sml_of(g.ecap))) / stg_lds_of(L));
-      if (g.wpb < 1) return -1;
-      g.lds = stg_lds_of(L) * g.wpb + sml_of(g.ecap);
-    }
+    g.wpb = (uint32_t)std::min<uint64_t>(8, (cap - std::min<uint64_t>(cap, sml_of(g.ecap))) / stg_lds_of(L));
+    if (g.wpb < 1) return -1;
+    g.lds = stg_lds_of(L) * g.wpb + sml_of(g.ecap);
     // experiment knob: OVL_EXT_BLOCKS_PER_CU pads the LDS so that at most that many blocks
     // fit on a CU (occupancy studies); unset = natural occupancy
     if (allow_knob)
@@ -1767,13 +1733,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     uint64_t st = (uint64_t)(g.ecap + 2) * lw / (g.l16 ? 2 : 1);   // the row log
     if (window) st = std::max<uint64_t>(st, 3ull * (g.ecap + 9) + 2ull * L + 64);
     g.stride = (st + 63) & ~63ull;
-    const void *kfn = stage_kernel(g.l16, wide, sh);
+    const void *kfn = stage_kernel(g.l16, wide);
     if (g.lds > 64 * 1024)
       if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess)
         return -1;
     // persistent grid: as many blocks as are resident at once (registers and LDS), so no
     // block starts only after the work queue has drained; within the scratch budget
-    uint32_t waves = 4u * (sh ? OVL_SH_OCC : OVL_EXT_OCC) * c->n_cu;
+    uint32_t waves = 4u * OVL_EXT_OCC * c->n_cu;
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kfn, 64 * g.wpb, g.lds) == hipSuccess &&
         bpc > 0)
@@ -1791,29 +1757,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   // exactly what a job without the longer reads would get.
   {
     uint32_t prev = 0;
-    // the shared-strand class (OVL_SHARED=1 turns it on): 4 blocks of 8 waves per CU within
-    // 40 KB each (32 waves: the reads <= ~11 kb), or 3 within 52 KB (24 waves, <= ~15 kb)
-    // when every read fits that and not the first; the -l kernel has its own order
-    const char *she = OVL_SH_BUILD ? getenv("OVL_SHARED") : nullptr;
-    if (!ordered && she && atoi(she) != 0) {
-      auto longest_sh = [&](size_t cap) -> uint32_t {
-        uint32_t L = 0;
-        for (uint32_t x : c->h_len)
-          if (x > L && sh_lds_of(x, 8) <= cap) L = x;
-        return L;
-      };
-      uint32_t L = longest_sh(40 * 1024);
-      size_t cap = 40 * 1024;
-      if (L < c->max_len && longest_sh(52 * 1024) == c->max_len) {
-        L = c->max_len;
-        cap = 52 * 1024;
-      }
-      if (L >= 64) {
-        if (make_stage(L, cap, true, false, true)) return fail(OVL_ERR_HIP, "shared staged kernel setup");
-        prev = L;
-      }
-    }
-    const size_t tier_cap[3] = {OVL_EXT_OCC == 8 ? 40 * 1024 : 52 * 1024, 52 * 1024, 160 * 1024};
+    const size_t tier_cap[3] = {52 * 1024, 52 * 1024, 160 * 1024};
     const uint32_t tier_wpb[3] = {8, 6, 1};
     for (int t = 0; t < 3; t++) {
       const uint32_t T = longest_fitting(tier_wpb[t], tier_cap[t]);
@@ -2000,9 +1944,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       EA.ord_slot = nullptr;
       EA.ord_diag = nullptr;
       EA.dkey = nullptr;
-      EA.seg = nullptr;
-      EA.nseg_dev = nullptr;
-      EA.seg_next = x_ctr.p + 6;
       slot_pairs[slot] = npairs;
       HIPC(hipMemsetAsync(x_ctr.p, 0, 64, xs));
       if (npairs && ordered) {
@@ -2076,47 +2017,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
               fb.otmp.grow(std::max<size_t>(tmp, 1)))
             return fail(OVL_ERR_OOM, "work order");
         }
-        const bool sh = !ext_stage.empty() && ext_stage[0].sh;
-        if (sh) {
-          // the shared-strand class's order: pairs grouped by unit (k_sh_keys), the groups'
-          // first positions selected (hipcub), the end appended
-          const int n = (int)npairs;
-          size_t t1 = 0, t2 = 0;
-          if (nc >= (1u << 28))
-            return fail(OVL_ERR_UNSUPPORTED, "%u units in one extension launch: past the shared-"
-                        "strand order's 28-bit unit field (OVL_SHARED=0 runs without it)", nc);
-          HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, fb.shk[0].p, fb.shk[1].p,
-                                                  fb.shi[0].p, fb.shi[1].p, n, 0, 64, xs));
-          hipcub::CountingInputIterator<uint32_t> it(0);
-          HIPC(hipcub::DeviceSelect::Flagged(nullptr, t2, it, fb.shf.p, fb.seg.p, fb.nseg.p, n, xs));
-          const size_t t = std::max(t1, t2);
-          if (fb.shk[0].n < npairs || fb.shk[1].n < npairs || fb.shi[0].n < npairs ||
-              fb.shi[1].n < npairs || fb.shw.n < nc || fb.seg.n < (size_t)npairs + 1 ||
-              fb.shf.n < npairs || fb.shtmp.n < t || !fb.nseg.p) {
-            HIPC(hipStreamSynchronize(xs));
-            if (fb.shk[0].grow(npairs) || fb.shk[1].grow(npairs) || fb.shi[0].grow(npairs) ||
-                fb.shi[1].grow(npairs) || fb.shw.grow(std::max<uint32_t>(nc, 1)) ||
-                fb.seg.grow((size_t)npairs + 1) || fb.shf.grow(npairs) ||
-                fb.shtmp.grow(std::max<size_t>(t, 1)) || fb.nseg.grow(1))
-              return fail(OVL_ERR_OOM, "shared-strand work order");
-          }
-          const dim3 grid(std::min<uint32_t>((npairs + 255) / 256, 4096)), blk(256);
-          HIPC(hipMemsetAsync(fb.shw.p, 0, 4ull * std::max<uint32_t>(nc, 1), xs));
-          hipLaunchKernelGGL(k_sh_unit_work, grid, blk, 0, xs, ext_pairs, npairs, fb.shw.p);
-          hipLaunchKernelGGL(k_sh_keys, grid, blk, 0, xs, ext_pairs, npairs, fb.shw.p, fb.shk[0].p,
-                             fb.shi[0].p);
-          size_t tt = t1;
-          HIPC(hipcub::DeviceRadixSort::SortPairs(fb.shtmp.p, tt, fb.shk[0].p, fb.shk[1].p,
-                                                  fb.shi[0].p, fb.shi[1].p, n, 0, 64, xs));
-          hipLaunchKernelGGL(k_sh_flags, grid, blk, 0, xs, fb.shk[1].p, npairs, fb.shf.p);
-          tt = t2;
-          HIPC(hipcub::DeviceSelect::Flagged(fb.shtmp.p, tt, it, fb.shf.p, fb.seg.p, fb.nseg.p, n, xs));
-          hipLaunchKernelGGL(k_sh_seg_end, dim3(1), dim3(1), 0, xs, fb.seg.p, fb.nseg.p, npairs);
-          HIPC(hipGetLastError());
-          EA.list = fb.shi[1].p;
-          EA.seg = fb.seg.p;
-          EA.nseg_dev = fb.nseg.p;
-        } else if (npairs > 1) {
+        if (npairs > 1) {
           // longest-first work order (node count descending; ties keep pair order)
           hipLaunchKernelGGL(k_pair_order_keys, dim3(std::min<uint32_t>((npairs + 255) / 256, 4096)),
                              dim3(256), 0, xs, ext_pairs, npairs, fb.okey.p, fb.oidx.p);
@@ -2170,16 +2071,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
             // an empty class defers nothing: its counter stays 0 for the next one
           } else {
           n_ext_launch++;
-          if (false) {
-#if OVL_SH_BUILD
-          } else if (g.sh && g.l16) {
-            hipLaunchKernelGGL((k_extend<true, true, false, OVL_RJ, true>), dim3(g.waves / g.wpb),
-                               dim3(64 * g.wpb), g.lds, xs, EA);
-          } else if (g.sh) {
-            hipLaunchKernelGGL((k_extend<true, false, false, OVL_RJ, true>), dim3(g.waves / g.wpb),
-                               dim3(64 * g.wpb), g.lds, xs, EA);
-#endif
-          } else if (g.wide && g.l16)
+          if (g.wide && g.l16)
             hipLaunchKernelGGL((k_extend<true, true, false, 2 * OVL_RJ>), dim3(g.waves / g.wpb),
                                dim3(64 * g.wpb), g.lds, xs, EA);
           else if (g.wide)

@@ -66,12 +66,6 @@ struct ExtendArgs {
   const uint32_t *ord_slot;     // String_Olap_Space order (Add_Ref's hash slots)
   const uint32_t *ord_diag;     // By_Diag_Sum order, ties in String_Olap_Space order (stable)
   const uint64_t *dkey;         // per pair: its average diagonal as an order-preserving key
-  // SH (the staged kernel with a block-shared query strand): list[] holds the pairs grouped
-  // by unit (units by descending work, a unit's pairs by descending node count); unit group
-  // g is list[seg[g] .. seg[g+1]); a block's waves share the query strand of each group
-  const uint32_t *seg;
-  const uint32_t *nseg_dev;
-  uint32_t *seg_next;           // global cursor over the groups
 };
 
 // debug counters (dbg != null): 0 ped calls 1 rows 2 chunks 3 slide words 4 tb steps
@@ -103,22 +97,10 @@ __device__ __forceinline__ void wave_argmax(int32_t &v, int32_t &d) {
   }
 }
 
-// OVL_GML: the staged kernel reads Edit_Match_Limit from global memory through the constant
-// address space (one scalar load per row, scalar-cache resident) instead of a block-shared LDS
-// copy; with OVL_SCR_STAGE = 0 its waves hold no LDS scratch either (the removal pass keeps
-// its thresholds in the wave's global scratch), so a 10 kb pair's wave needs only its two
-// strands in LDS -- 32 waves per CU at 8 waves per SIMD (OVL_EXT_OCC = 8)
-#ifndef OVL_GML
-#define OVL_GML 0
-#endif
-#ifndef OVL_SCR_STAGE
-#define OVL_SCR_STAGE 256
-#endif
-#if OVL_GML
-typedef const __attribute__((address_space(4))) int32_t ml_t;
-#else
+// the register kernel's Edit_Match_Limit: a block-shared LDS copy (r4 measured a global
+// table read through the constant address space, which frees the LDS for 32 waves per CU:
+// no faster)
 typedef const __attribute__((address_space(3))) int32_t ml_t;
-#endif
 
 struct WaveMem {
   int32_t *rows;      // global: band-compact log of every row (read by the traceback)
@@ -129,7 +111,7 @@ struct WaveMem {
   lds_i32 *ldc;       // LDS: Left_Delta cache for Lies_On_Alignment
   int32_t  ldcap;
   const lds_i32 *mlim;  // LDS: Edit_Match_Limit[0 .. e_cap+1], shared by the block
-  ml_t    *rmlim;       // the register kernel's Edit_Match_Limit (LDS copy, or global: OVL_GML)
+  ml_t    *rmlim;       // the register kernel's Edit_Match_Limit (the LDS copy)
 };
 
 __device__ __forceinline__ void lds_sync() {
@@ -469,9 +451,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #define OVL_RJ 8
 #endif
 #define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
-#ifndef OVL_INPLACE
-#define OVL_INPLACE 0            // 1: the row loop updates its row registers in place (A/B)
-#endif
 static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 
 #ifdef OVL_PROFILE
@@ -690,15 +669,6 @@ __device__ __forceinline__ double uni(double v) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-// Extend_Alignment's kind is DOVETAIL only when both of its extensions match to an end
-// (prefixEditDistance-extend.C:207), and Process_Matches reads nothing of any other result
-// but its kind unless partial overlaps are on (Process_String_Overlaps.C:500, :520).  So an
-// extension that stops short of the end needs no traceback, and after a forward one that
-// did the reverse one is not run (extend_alignment).  1: skip both; 0: compute them.
-#ifndef OVL_SKIP_MOOT_REVERSE
-#define OVL_SKIP_MOOT_REVERSE 0
-#endif
-
 // The row loop stays a call: inlined into process_pair (always_inline) the kernel keeps 80
 // VGPRs but spills 576 B per lane inside the loop -- extension 218 -> 297 ms (+37 %) on the
 // 10k-read job (r02v A/B).
@@ -811,16 +781,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     // ---- A+B per chunk: neighbours from row e-1 (DPP, no LDS), then the first 32-base
     // slide step of every lane, branch-free (one pass: each unrolled chunk costs a scalar
     // compare-and-branch on jr) --------------------------------------------------------
-#if OVL_INPLACE
-    // Row e is computed in place of row e-1 (R[j]); chunk j's lower neighbour is chunk j-1's
-    // OLD value, kept in prev_old.  The bases left before the end are recomputed where they
-    // are needed (the rare continued slides, the end row), and the end test is one mask of
-    // lanes whose slide reached its limit: 16 VGPRs fewer than keeping NR[] / RM[] arrays.
-    int32_t prev_old = -2;
-    uint64_t endm = 0;
-#else
     int32_t NR[J], RM[J];   // row value; lanes: bases left before the end (0 = end)
-#endif
     uint64_t need[J];
     uint64_t any = 0;
 #pragma unroll
@@ -829,11 +790,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       const int32_t d = B + 64 * j + (int32_t)lane;
       const int32_t p0 = R[j];
       // row e-1 at d-1 and d+1 (diagonal B-1 and B+64J are outside the band: -2)
-#if OVL_INPLACE
-      const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, prev_old);
-#else
       const int32_t pm = (j == 0) ? dpp_from_lower(p0, -2) : dpp_lower_across(p0, R[j > 0 ? j - 1 : 0]);
-#endif
       const int32_t pp = (j + 1 < J) ? dpp_upper_across(p0, R[j + 1 < J ? j + 1 : j])
                                      : dpp_from_upper(p0, -2);
       // q = Row - 1 = max(pm - 1, p0, pp): the +1 of the max3 folds into the constants
@@ -864,15 +821,8 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
                                     : (int32_t)__builtin_clz(mm | 1u);
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
-#if OVL_INPLACE
-      prev_old = p0;
-      R[j] = q + 1 + k;                        // lim >= 0 inside the band
-      // the slide reached its limit (no bases left): outside the band k = lim < lmin
-      endm |= __builtin_amdgcn_ballot_w64(k >= lmin);
-#else
       NR[j] = q + 1 + k;                       // lim >= 0 inside the band
       RM[j] = lmin - k;                        // inside: lim - k >= 0; outside: > 0
-#endif
       // run == 31 && lim > 31  <=>  min(run, lim - 1) == 31 (run <= 31): one ballot, no
       // scalar AND of two
       need[j] = __builtin_amdgcn_ballot_w64((run < lim - 1 ? run : lim - 1) == 31);
@@ -890,28 +840,12 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
         if (need[j]) {
-#if OVL_INPLACE
-          // the lane's end flag is set inside the divergent branch and balloted after it: a
-          // ballot merged out of a divergent region makes the mask (and every branch on it)
-          // divergent
-          bool fend = false;
-#endif
           if (need[j] & (1ull << lane)) {
             const int32_t d = B + 64 * j + (int32_t)lane;
-#if OVL_INPLACE
-            const int32_t rm = (m - R[j]) < (n - d - R[j]) ? (m - R[j]) : (n - d - R[j]);
-            const int32_t sl = slide_any<DIR>(A, a0, T, t0, R[j], d, rm);
-            R[j] += sl;
-            fend = sl >= rm;
-#else
             const int32_t sl = slide_any<DIR>(A, a0, T, t0, NR[j], d, RM[j]);
             NR[j] += sl;
             RM[j] -= sl;
-#endif
           }
-#if OVL_INPLACE
-          endm |= __builtin_amdgcn_ballot_w64(fend);
-#endif
 #ifdef OVL_PROFILE
           pc_slide++;
 #endif
@@ -929,19 +863,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     // first or last chunk, or the whole band) every chunk is rescanned below.  The end test
     // is a per-lane min of the bases left, one ballot per row.  (The per-chunk s_ff1 /
     // s_flbit / min reduction was 6 scalar instructions per chunk.)
-#if OVL_INPLACE
-#define NRJ(j) R[j]
-    uint64_t km0 = 0, kml = 0;
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      if (j >= JU && j > jr) break;
-      const int32_t d = B + 64 * j + (int32_t)lane;
-      kml = __builtin_amdgcn_ballot_w64(R[j] + (d > 0 ? d : 0) >= ML);
-      if (j == 0) km0 = kml;
-    }
-    const uint64_t endany = endm;
-#else
-#define NRJ(j) NR[j]
     int32_t rmin = RM[0];
     uint64_t km0 = 0, kml = 0;
 #pragma unroll
@@ -953,7 +874,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       if (j == 0) km0 = kml;
     }
     const uint64_t endany = __builtin_amdgcn_ballot_w64(rmin == 0);
-#endif
     uint32_t nlo, nhi;                         // min window offset of a kept lane; min
                                                // reversed offset (64J-1 - o) of one
     // s_ff1 / s_flbit give ~0u on an empty mask: one signed test of their OR sends the row
@@ -970,7 +890,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jr) break;
         const int32_t d = B + 64 * j + (int32_t)lane;
-        const uint64_t km = __builtin_amdgcn_ballot_w64(NRJ(j) + (d > 0 ? d : 0) >= ML);
+        const uint64_t km = __builtin_amdgcn_ballot_w64(NR[j] + (d > 0 ? d : 0) >= ML);
         uint32_t f1, fb;
         asm("s_ff1_i32_b64 %0, %1" : "=s"(f1) : "s"(km));
         asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(km));
@@ -999,16 +919,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
 #pragma unroll
       for (int j = J - 1; j >= 0; j--) {
         if (j >= JU && j > jr) continue;
-#if OVL_INPLACE
-        const int32_t d = B + 64 * j + (int32_t)lane;
-        const int32_t rm = (m - R[j]) < (n - d - R[j]) ? (m - R[j]) : (n - d - R[j]);
-        const uint64_t em = __builtin_amdgcn_ballot_w64(rm == 0);
-        if (em) {
-          const int32_t l = (int32_t)__builtin_ctzll(em);
-          end_d = B + 64 * j + l;
-          end_row = __builtin_amdgcn_readlane(R[j], l);
-        }
-#else
         const uint64_t em = __builtin_amdgcn_ballot_w64(RM[j] == 0);
         if (em) {
           const int32_t l = (int32_t)__builtin_ctzll(em);
@@ -1018,17 +928,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
           end_pp = (l < 63) ? __builtin_amdgcn_readlane(R[j], l + 1)
                  : (j + 1 < J) ? __builtin_amdgcn_readlane(R[j + 1 < J ? j + 1 : j], 0) : -2;
         }
-#endif
       }
-#if OVL_INPLACE
-      // row e-1 at end_d+1, from the row log (R holds row e now); the forward rule below
-      // needs it only when the end is A's end: one load, once per extension
-      if (DIR > 0) {
-        vm_sync();
-        const int32_t c = (end_d + 1) & (LW - 1);
-        end_pp = (int32_t)clog[(size_t)(e - 1) * LW + c];
-      }
-#endif
       ended = true;
       end_e = e;
       e = limit + 1;
@@ -1052,7 +952,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jrs) break;
         const int32_t d = B + 64 * j + (int32_t)lane;
-        const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NRJ(j) : -2;
+        const int32_t v = ((uint32_t)(d - nl) <= kspan) ? NR[j] : -2;
         R[j] = v;
         const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
         kmx = key > kmx ? key : kmx;
@@ -1125,7 +1025,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   }
   // stopped with rows left to compute: the window overflowed (every other stop sets e
   // past the limit)
-#undef NRJ
   if (e <= limit) out.ovf = 1;
   if (out.ovf) return out;
   const int32_t max_score_best_d = ms_B + ((1 << WB) - 1) - (ms_key & ((1 << WB) - 1));
@@ -1162,12 +1061,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     out.mte = 0;
     tb_e = max_score_best_e; tb_d = max_score_best_d;
   }
-#if OVL_SKIP_MOOT_REVERSE
-  if (out.mte == 0 && !partial) {              // not a dovetail end: the deltas are unread
-    out.nd = -1;
-    return out;
-  }
-#endif
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
@@ -1211,15 +1104,7 @@ struct ExtOut {
 };
 
 // Extend_Alignment (prefixEditDistance-extend.C:86).  Leaves the merged Left_Delta in LD.
-#ifndef OVL_UNI_STATE
-#define OVL_UNI_STATE 1
-#endif
-
-#if OVL_UNI_STATE
 #define UNI(v) uni(v)
-#else
-#define UNI(v) (v)
-#endif
 template <bool FAST, bool L16, int RJ, typename SS>
 __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS &S,
                                    int32_t S_Len, const SS &T, int32_t T_Len,
@@ -1294,18 +1179,6 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
   }
   S_Hi += S_Right_Begin - 1;
   T_Hi += T_Right_Begin - 1;
-
-  // a forward extension that stopped short of the end leaves the reverse one unread (see
-  // OVL_SKIP_MOOT_REVERSE)
-#if OVL_SKIP_MOOT_REVERSE
-  if (!rmte && !X.partial) {
-    r.kind = K_NONE;
-    r.Errors = 0;
-    r.S_Lo = r.S_Hi = r.T_Lo = r.T_Hi = 0;
-    r.ld_len = 0;
-    return r;
-  }
-#endif
 
   if (S_Left_Begin < 0 || T_Left_Begin < 0) {
     S_Lo = 0; T_Lo = 0; lmte = 1;
@@ -1748,8 +1621,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     // Lies_On_Alignment (:307) by binary search: walking the deltas, delta i is reached
     // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
     // and compares with diag_i (or with the final diag).  thr is non-decreasing.  The
-    // thresholds live in the wave's LDS scratch, or (OVL_SCR_STAGE = 0) in the spare slot of
-    // its global delta scratch.
+    // thresholds live in the wave's LDS scratch.
     auto by_search = [&](auto *thr, auto *dgl, auto sync) {
       int32_t cs = S_Lo, cd = T_Lo - S_Lo;
       for (int32_t i0 = 0; i0 < ld_len; i0 += 64) {
@@ -1788,14 +1660,9 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
       }
       sync();
     };
-    typedef typename std::conditional<T16, __attribute__((address_space(1))) int16_t,
-                                      __attribute__((address_space(1))) int32_t>::type g_t;
     if (on_aln && per * (ld_len + 1) <= WM.ldcap) {
       lds_t *thr = (lds_t *)WM.ldc;
       by_search(thr, thr + ld_len + 1, [] { lds_sync(); });
-    } else if (FAST && OVL_SCR_STAGE == 0 && on_aln && per * (ld_len + 1) <= X.e_cap + 8) {
-      g_t *thr = (g_t *)(LD + (X.e_cap + 8));
-      by_search(thr, thr + ld_len + 1, [] { vm_sync(); });
     } else {
       const int32_t *ldp = LD;
       if (ld_len <= WM.ldcap) {
@@ -1914,9 +1781,8 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
   return L;
 }
 
-#define OVL_SCR 256              // shared-strand kernel: per-wave LDS scratch ints
+#define OVL_SCR_STAGE 256        // the staged kernel's per-wave LDS scratch ints
                                  // (Lies_On_Alignment thresholds, Left_Delta cache)
-// OVL_SCR_STAGE: the staged kernel's per-wave LDS scratch ints (defined with OVL_GML above)
 
 // STAGE = true: exception-free pairs, strands staged in LDS, rows in registers; pairs with
 // 'n' bases or a band wider than the register window are deferred to the generic kernel.
@@ -1930,43 +1796,18 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
 #endif
 // RJ: register chunks of the staged kernel's row window (OVL_RJ; the wide class that takes
 // the pairs whose band outgrows it runs 2 x OVL_RJ at lower occupancy)
-#define OVL_SH_SLOTS 3           // SH: query strands a block holds at once (LDS slots)
-
-// SH: block-shared query strands.  At 10 kb each wave's two staged strands (2 x 2.5 KB) plus
-// its scratch cap a CU at 24 waves by LDS alone; the pairs of one (query, orientation) unit
-// share the query strand (12.6 pairs per unit in the 50k x 10 kb job), so a block keeps
-// OVL_SH_SLOTS query strands and each wave stages only its target.  Slot protocol (LDS
-// atomics, no block barrier after the start): ctl = (end << 32) | next over the sorted pair
-// list; a wave takes pair `next` of a slot after incrementing the slot's users; a slot whose
-// pairs are all taken and that no wave is using is reloaded with the next unit group by the
-// wave that claims it (loading flag) -- no wave can be reading its old strand then, since a
-// reader holds a valid pair and so a user count.
-struct ShSlot {
-  unsigned long long ctl;       // (end << 32) | next
-  int32_t users;                // waves holding a pair of this slot
-  int32_t loading;              // a wave is reloading the slot
-  int32_t bad;                  // the unit's query strand cannot be staged: defer its pairs
-  int32_t pad[3];
-};
-
-// The shared-strand kernel is built only with OVL_SH_BUILD=1 (measured slower, DESIGN.md
-// round 4): its 8-wave instance shares the row-loop functions with the 6-wave kernel, and a
-// callee takes the tightest register budget of its callers (64 VGPRs), which made the
-// previous row loop spill 96 B per lane in every kernel
-#ifndef OVL_SH_BUILD
-#define OVL_SH_BUILD 0
-#endif
-#ifndef OVL_SH_OCC
-#define OVL_SH_OCC 8             // waves per SIMD the shared-strand kernel is compiled for
-#endif
-template <bool STAGE, bool L16, bool ORD = false, int RJ = OVL_RJ, bool SH = false>
-__global__ void __launch_bounds__(512, SH ? OVL_SH_OCC : RJ > OVL_RJ ? 3 : OVL_EXT_OCC)
+// Block-shared query strands (the pairs of one unit share the query strand, so a block can
+// hold a few query strands and each wave stage only its target: 32 waves per CU at 10 kb)
+// were built and measured in round 4, and ran slower (waves idle at a slot's end of pairs;
+// DESIGN.md round 4): not kept.
+template <bool STAGE, bool L16, bool ORD = false, int RJ = OVL_RJ>
+__global__ void __launch_bounds__(512, RJ > OVL_RJ ? 3 : OVL_EXT_OCC)
 k_extend(ExtendArgs X) {
   extern __shared__ __attribute__((aligned(16))) int32_t s_ext0[];
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
   constexpr bool GR = !STAGE && L16;
-  constexpr bool NOML = GR || (STAGE && OVL_GML);   // no LDS Edit_Match_Limit table
+  constexpr bool NOML = GR;                         // no LDS Edit_Match_Limit table
   int32_t mlsz = NOML ? 0 : ((X.e_cap + 2) + 3) & ~3;
   if constexpr (!NOML) {
     for (int32_t i = threadIdx.x; i < X.e_cap + 2; i += blockDim.x)
@@ -1979,36 +1820,9 @@ k_extend(ExtendArgs X) {
   WM.rows = X.rows + (size_t)gw * X.rows_cap;
   WM.rowdir = X.rowdir + (size_t)gw * 4 * (X.e_cap + 2);
   WM.mlim = l_ext0;
-#if OVL_GML
-  WM.rmlim = (ml_t *)X.match_limit;           // padded past max_errors on the host
-#else
   WM.rmlim = l_ext0;
-#endif
   lds_u64 *sw = nullptr, *tw = nullptr;
-  ShSlot *slots = nullptr;
-  lds_u64 *sstr = nullptr;
-  if constexpr (SH) {
-    // block: [slot control][query strand slots] then per wave [T words | scratch]
-    slots = (ShSlot *)s_ext;
-    sstr = (lds_u64 *)(s_ext + (OVL_SH_SLOTS * sizeof(ShSlot) + 16) / 4);
-    lds_i32 *wbase = (lds_i32 *)(sstr + OVL_SH_SLOTS * X.sw_words);
-    uint32_t wave_ints = 2 * (uint32_t)X.sw_words + OVL_SCR;
-    lds_i32 *wlds = wbase + wave * wave_ints;
-    tw = (lds_u64 *)wlds;
-    WM.lrow = nullptr;
-    WM.wcap = 0;
-    WM.tbw = wlds + 2 * X.sw_words;
-    WM.ldc = WM.tbw;
-    WM.ldcap = OVL_SCR;
-    if (threadIdx.x < OVL_SH_SLOTS) {
-      slots[threadIdx.x].ctl = 0;                     // next = end = 0: exhausted, unused
-      slots[threadIdx.x].users = 0;
-      slots[threadIdx.x].loading = 0;
-      slots[threadIdx.x].bad = 0;
-    }
-    if (threadIdx.x == 0) *(int32_t *)(slots + OVL_SH_SLOTS) = 0;   // no more groups
-    __syncthreads();
-  } else if constexpr (STAGE) {
+  if constexpr (STAGE) {
     // per wave: [S words | T words] (u64) then the scratch
     uint32_t wave_ints = 4 * (uint32_t)X.sw_words + OVL_SCR_STAGE;
     lds_i32 *wlds = s_ext + wave * wave_ints;
@@ -2037,105 +1851,7 @@ k_extend(ExtendArgs X) {
   unsigned long long st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t npairs = X.npairs_dev ? __builtin_amdgcn_readfirstlane(*X.npairs_dev) : X.npairs;
 
-  if constexpr (SH) {
-    static_assert(STAGE, "SH is a staged kernel");
-    volatile int32_t *done = (volatile int32_t *)(slots + OVL_SH_SLOTS);
-    const uint32_t nseg = __builtin_amdgcn_readfirstlane(*X.nseg_dev);
-    int32_t last = (int32_t)(wave % OVL_SH_SLOTS);
-    for (;;) {
-      // a pair from a loaded slot (the wave's last slot first)
-      int32_t slot = -1;
-      uint32_t li = 0;
-      for (int32_t kk = 0; kk < OVL_SH_SLOTS; kk++) {
-        const int32_t sl = (last + kk) % OVL_SH_SLOTS;
-        unsigned long long c = 0;
-        if (lane == 0) {
-          // counted before the pair is taken (seq_cst: the two are not reordered)
-          __hip_atomic_fetch_add(&slots[sl].users, 1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
-          c = __hip_atomic_fetch_add(&slots[sl].ctl, 1ull, __ATOMIC_SEQ_CST,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        const uint32_t idx = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)c);
-        const uint32_t end = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(c >> 32));
-        if (idx < end) { slot = sl; li = idx; break; }
-        if (lane == 0)
-          __hip_atomic_fetch_add(&slots[sl].users, -1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (slot < 0) {
-        // none: reload a slot whose pairs are all taken and that no wave uses
-        bool loaded = false, finished = false;
-        for (int32_t sl = 0; sl < OVL_SH_SLOTS && !loaded && !finished; sl++) {
-          // claim the slot first, then check it: only the claimant may publish a new group,
-          // so once claimed an exhausted ctl stays exhausted, and a zero user count then
-          // means no wave holds one of its pairs (a holder counts itself before it takes
-          // a pair).  Checking before claiming raced with another loader's publish.
-          int32_t claim = 0;
-          if (lane == 0) {
-            if (atomicCAS(&slots[sl].loading, 0, 1) == 0) {
-              const unsigned long long c = __hip_atomic_load(&slots[sl].ctl, __ATOMIC_SEQ_CST,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-              const int32_t us = __hip_atomic_load(&slots[sl].users, __ATOMIC_SEQ_CST,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-              if ((uint32_t)c >= (uint32_t)(c >> 32) && us == 0) claim = 1;
-              else atomicExch(&slots[sl].loading, 0);
-            }
-          }
-          claim = __builtin_amdgcn_readfirstlane(claim);
-          if (!claim) continue;
-          uint32_t g = 0;
-          if (lane == 0) g = atomicAdd(X.seg_next, 1u);
-          g = __builtin_amdgcn_readfirstlane(g);
-          if (g >= nseg) {
-            if (lane == 0) { *done = 1; atomicExch(&slots[sl].loading, 0); }
-            finished = true;
-            break;
-          }
-          const uint32_t b = X.seg[g], e = X.seg[g + 1];
-          const PairRec P0 = X.pairs[X.list[b]];
-          const Unit un0 = X.units[P0.unit];
-          const Strand S0 = un0.dir ? strand_rc(X.R, un0.r) : strand_fwd(X.R, un0.r);
-          const bool ok = !(S0.ex_wild || S0.ex_nul) && S0.len <= X.stage_len;
-          if (ok) (void)stage_strand(S0, sstr + sl * X.sw_words, lane);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          lds_sync();
-          if (lane == 0) {
-            slots[sl].bad = ok ? 0 : 1;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            atomicExch(&slots[sl].ctl, ((unsigned long long)e << 32) | b);
-            atomicExch(&slots[sl].loading, 0);
-          }
-          loaded = true;
-          last = sl;
-        }
-        if (loaded) continue;
-        if (finished || *done) break;        // no unit group left: the slots hold the rest
-        __builtin_amdgcn_s_sleep(2);         // a slot is still in use: wait for it
-        continue;
-      }
-      last = slot;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      const uint32_t pi = X.list[li];
-      PairRec P = X.pairs[pi];
-      Unit un = X.units[P.unit];
-      Strand S = un.dir ? strand_rc(X.R, un.r) : strand_fwd(X.R, un.r);
-      Strand T = strand_fwd(X.R, P.tgt);
-      bool ok = false;
-      const int32_t bad = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(&slots[slot].bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      if (!bad && !T.ex_wild && T.len <= X.stage_len) {
-        StrandLP SL;
-        SL.w = sstr + slot * X.sw_words;
-        SL.len = S.len;
-        StrandLP TL = stage_strand(T, tw, lane);
-        lds_sync();
-        ok = process_pair<true, L16, false, RJ>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
-      }
-      if (!ok && lane == 0) X.defer[atomicAdd(X.ndefer, 1u)] = pi;
-      lds_sync();
-      if (lane == 0)      // release: every read of the slot's strand is done
-        __hip_atomic_fetch_add(&slots[slot].users, -1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  } else if constexpr (ORD) {
+  if constexpr (ORD) {
     static_assert(!STAGE, "the -l kernel is the generic one");
     for (;;) {
       uint32_t ui = 0;

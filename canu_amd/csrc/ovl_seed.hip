@@ -45,24 +45,8 @@ __device__ __forceinline__ uint32_t unit_windows(const ReadsDev &R, const Unit &
 }
 
 // Number of leading entries of a descending occurrence list whose read iid > a.
-#ifndef OVL_QUAL_UNROLL
-#define OVL_QUAL_UNROLL 0
-#endif
 __device__ __forceinline__ uint32_t qualifying(const uint64_t *occ, uint32_t off, uint32_t cnt,
                                                uint32_t a_iid) {
-#if OVL_QUAL_UNROLL
-  if (cnt <= 8) {
-    // the (at most two) lines of a short list read by independent loads issued together,
-    // instead of a scan whose every load waits for the previous compare
-    uint32_t iid[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) iid[q] = (uint32_t)q < cnt ? (uint32_t)(occ[off + q] >> 32) : 0u;
-    uint32_t n = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) n += (iid[q] > a_iid) ? 1u : 0u;   // a descending prefix
-    return n;
-  }
-#endif
   if (cnt <= 8) {
     uint32_t q = 0;
     while (q < cnt && (uint32_t)(occ[off + q] >> 32) > a_iid) q++;
@@ -211,9 +195,36 @@ struct SqKeyArgs {
   uint64_t kmask;
   uint64_t *key;                // run-local window id -> mix64(k-mer)
   uint32_t *wid;                // -> the window id; 0xFFFFFFFF: no k-mer there (an N, a NUL)
+  unsigned long long *sig;      // [0..1]: the run's (key, wid) multiset signature
 };
 
-// one wave per unit: its windows' keys, k_probe's window rule (unit_windows, the N / NUL masks)
+// Multiset signature of a run's (key, wid) pairs: two independent 64-bit sums of a mix of
+// each pair, computed before the sort (k_sq_keys) and after it (k_sq_sorted_check).  A sort
+// that returns its keys in order but with a window id duplicated or lost (what this ROCm's
+// partial-range radix sort did) changes both sums.
+__device__ __forceinline__ void sq_sig_add(uint64_t key, uint32_t wid, uint64_t &s1,
+                                           uint64_t &s2) {
+  const uint64_t h = mix64(key ^ ((uint64_t)wid * 0x9E3779B97F4A7C15ull));
+  s1 += h;
+  s2 += mix64(h ^ 0xD6E8FEB86659FD93ull);
+}
+__device__ __forceinline__ void sq_sig_flush(uint64_t s1, uint64_t s2, uint32_t lane,
+                                             unsigned long long *sig) {
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (lane == 0) {
+    atomicAdd(&sig[0], (unsigned long long)s1);
+    atomicAdd(&sig[1], (unsigned long long)s2);
+  }
+}
+
+// one wave per unit: its windows' keys, k_probe's window rule (unit_windows, the N / NUL
+// masks).  The unit owns wbase[u+1] - wbase[u] slots (L - k + 1, sq_prepare); a reverse unit
+// whose strand holds a NUL has fewer windows (unit_windows), and its tail slots are written
+// as "no k-mer" too -- left unwritten they would keep an earlier run's (key, wid) pairs,
+// which the sort and the probe would then read as windows.
 __global__ void __launch_bounds__(256) k_sq_keys(SqKeyArgs A) {
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t u = blockIdx.x * 4 + wave;
@@ -225,12 +236,18 @@ __global__ void __launch_bounds__(256) k_sq_keys(SqKeyArgs A) {
   const int32_t L = S.len;
   const uint32_t kbits = (1u << A.k) - 1u;
   const uint64_t b = A.wbase[u];
-  for (uint32_t o = lane; o < nw; o += 64) {
-    bool ok = (int32_t)(o + A.k) <= L;
+  const uint32_t ns = (uint32_t)(A.wbase[u + 1] - b);
+  uint64_t s1 = 0, s2 = 0;
+  for (uint32_t o = lane; o < ns; o += 64) {
+    bool ok = o < nw && (int32_t)(o + A.k) <= L;
     if (ok && bad) ok = (mask_at(bad, (int32_t)o) & kbits) == 0;
-    A.key[b + o] = ok ? mix64(bases_at(S.w, (int32_t)o) & A.kmask) : ~0ull;
-    A.wid[b + o] = ok ? (uint32_t)(b + o) : 0xFFFFFFFFu;
+    const uint64_t key = ok ? mix64(bases_at(S.w, (int32_t)o) & A.kmask) : ~0ull;
+    const uint32_t wid = ok ? (uint32_t)(b + o) : 0xFFFFFFFFu;
+    A.key[b + o] = key;
+    A.wid[b + o] = wid;
+    sq_sig_add(key, wid, s1, s2);
   }
+  sq_sig_flush(s1, s2, lane, A.sig);
 }
 
 struct SqProbeArgs {
@@ -323,12 +340,22 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
   }
 }
 
-// a partially sorted run's order on the key bits from `shift` up (see sq_prepare)
-__global__ void __launch_bounds__(256) k_sq_sorted_check(const uint64_t *key, uint64_t n,
-                                                         uint32_t shift, uint32_t *bad) {
+// A partially sorted run, checked on both properties a sort must keep (see sq_prepare): the
+// order of the key bits from `shift` up, and the (key, wid) multiset -- its signature into
+// sig[2..3], compared on the host with k_sq_keys' sig[0..1].  bad: any order violation.
+__global__ void __launch_bounds__(256) k_sq_sorted_check(const uint64_t *key, const uint32_t *wid,
+                                                         uint64_t n, uint32_t shift,
+                                                         unsigned long long *sig, uint32_t *bad) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = 1 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride)
-    if ((key[i] >> shift) < (key[i - 1] >> shift)) { atomicOr(bad, 1u); return; }
+  uint64_t s1 = 0, s2 = 0;
+  bool ordered = true;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = key[i];
+    if (i > 0 && (k >> shift) < (key[i - 1] >> shift)) ordered = false;
+    sq_sig_add(k, wid[i], s1, s2);
+  }
+  sq_sig_flush(s1, s2, threadIdx.x & 63, sig + 2);
+  if (!ordered) atomicOr(bad, 1u);
 }
 
 // the units' hit counts (k_probe's unit_hits) from the records: one wave per unit, its
@@ -398,16 +425,6 @@ __global__ void __launch_bounds__(256) k_hitlist(HitArgs A) {
 }
 
 #define OVL_HCAP   256           // staged occurrences per wave
-#ifndef OVL_SCATTER_BALLOT
-#define OVL_SCATTER_BALLOT 0     // 1: a staged entry's rank in its target's list from ballots
-                                 // (measured +1.7 ms per step, not kept)
-#endif
-#ifndef OVL_STAGE_BATCH
-#define OVL_STAGE_BATCH 0        // stage a chunk's 4 x 64 occurrences with their loads together
-#endif
-#ifndef OVL_CHAIN_RUNS
-#define OVL_CHAIN_RUNS 1         // replay runs of head extensions at once (A/B: 0)
-#endif
 #define OVL_MAXT   128           // targets per pass (2 per lane)
 #define OVL_NODE_BLOCK 4096      // nodes a wave claims at a time
 #ifndef OVL_CHAIN_OCC
@@ -651,9 +668,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   __shared__ uint32_t s_hp[4][OVL_HCAP];
   __shared__ uint8_t  s_hs[4][OVL_HCAP];      // its target slot (0..127), 0xFF: none
   __shared__ uint32_t s_sv[4][OVL_HCAP];      // payloads sorted by (slot, staged order)
-#if OVL_CHAIN_RUNS
   __shared__ uint64_t s_lst[4][OVL_HCAP / 64]; // bit i: sorted entry i starts a target's list
-#endif
   __shared__ uint32_t s_cnt[4][2 * OVL_MAXT]; // per slot: base, running count
   __shared__ uint32_t s_seg[4][65];
   __shared__ uint32_t s_off[4][64];
@@ -666,9 +681,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
   uint32_t *hp = s_hp[wave];
   uint8_t *hs = s_hs[wave];
   uint32_t *sv = s_sv[wave];
-#if OVL_CHAIN_RUNS
   uint64_t *lst = s_lst[wave];
-#endif
   uint32_t *cnt = s_cnt[wave];
   uint32_t *seg = s_seg[wave];
   uint32_t *soff = s_off[wave];
@@ -745,36 +758,6 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           CPROF_T(t_c);
           uint32_t p1 = p0 + OVL_HCAP < total ? p0 + OVL_HCAP : total;
           // stage occurrences p0..p1 of this chunk, in order (ordered compaction)
-#if OVL_STAGE_BATCH
-          {
-            // the 4 x 64 entries' windows first (independent LDS searches), then their
-            // occurrence loads issued together: one memory round trip instead of four
-            constexpr int NB = OVL_HCAP / 64;
-            uint32_t lw[NB], src[NB];
-#pragma unroll
-            for (int q = 0; q < NB; q++) {
-              const uint32_t idx = p0 + 64 * q + lane;
-              uint32_t lo = 0, hi = 64;          // last j with seg[j] <= idx
-              while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (seg[mid] <= idx) lo = mid; else hi = mid;
-              }
-              lw[q] = lo;
-              src[q] = idx < p1 ? soff[lo] + (idx - seg[lo]) : 0xFFFFFFFFu;
-            }
-            uint64_t oc[NB];
-#pragma unroll
-            for (int q = 0; q < NB; q++) oc[q] = src[q] != 0xFFFFFFFFu ? A.occ[src[q]] : 0ull;
-#pragma unroll
-            for (int q = 0; q < NB; q++) {
-              const uint32_t idx = p0 + 64 * q + lane;
-              if (idx < p1) {
-                ht[idx - p0] = (uint32_t)(oc[q] >> 32);
-                hp[idx - p0] = (lw[q] << 21) | (uint32_t)oc[q];
-              }
-            }
-          }
-#else
           for (uint32_t idx = p0 + lane; idx < p1; idx += 64) {
             uint32_t lo = 0, hi = 64;            // last j with seg[j] <= idx
             while (hi - lo > 1) {
@@ -785,11 +768,8 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             ht[idx - p0] = (uint32_t)(oc >> 32);
             hp[idx - p0] = (lo << 21) | (uint32_t)oc;
           }
-#endif
           for (uint32_t i = lane; i < 2 * OVL_MAXT; i += 64) cnt[i] = 0;
-#if OVL_CHAIN_RUNS
           if (lane < OVL_HCAP / 64) lst[lane] = 0;
-#endif
           WAVE_SYNC();
           CPROF_T(t_d);
           CPROF_ADD(1, t_c, t_d);
@@ -834,10 +814,8 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             WAVE_SYNC();
             cnt[2 * lane] = ex;                    // base of slot 2*lane
             cnt[2 * lane + 1] = ex + c0;           // base of slot 2*lane+1
-#if OVL_CHAIN_RUNS
             if (c0) atomicOr((unsigned long long *)&lst[ex >> 6], 1ull << (ex & 63));
             if (c1) atomicOr((unsigned long long *)&lst[(ex + c0) >> 6], 1ull << ((ex + c0) & 63));
-#endif
             cnt[OVL_MAXT + 2 * lane] = 0;          // running counts
             cnt[OVL_MAXT + 2 * lane + 1] = 0;
           }
@@ -845,30 +823,6 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           // stable scatter: within each 64-entry step a lane's rank among the lanes of its
           // slot is the popcount of the lower lanes in the slot's lane mask (one LDS OR per
           // lane), so every slot's list keeps the staged (window, chain) order
-#if OVL_SCATTER_BALLOT
-          // (here the lanes of a slot come from 7 ballots of the slot's bits -- no LDS masks
-          // and one barrier per step instead of three)
-          for (uint32_t b0 = p0; b0 < p1; b0 += 64) {
-            const uint32_t idx = b0 + lane;
-            const uint32_t slot = (idx < p1) ? hs[idx - p0] : 0xFFu;
-            const bool has = slot != 0xFFu;
-            uint64_t mk = __builtin_amdgcn_ballot_w64(has);
-#pragma unroll
-            for (int bit = 0; bit < 7; bit++) {
-              const bool on = (slot >> bit) & 1u;
-              const uint64_t m = __builtin_amdgcn_ballot_w64(has && on);
-              mk &= on ? m : ~m;
-            }
-            if (has) {
-              const uint32_t rank = __builtin_popcountll(mk & ((1ull << lane) - 1));
-              sv[cnt[slot] + cnt[OVL_MAXT + slot] + rank] = hp[idx - p0];
-            }
-            WAVE_SYNC();
-            if (has && lane == 63u - (uint32_t)__builtin_clzll(mk))   // the slot's last lane
-              cnt[OVL_MAXT + slot] += __builtin_popcountll(mk);
-            WAVE_SYNC();
-          }
-#else
           for (uint32_t b0 = p0; b0 < p1; b0 += 64) {
             uint32_t idx = b0 + lane;
             uint32_t slot = (idx < p1) ? hs[idx - p0] : 0xFFu;
@@ -888,9 +842,7 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             }
             WAVE_SYNC();
           }
-#endif
           WAVE_SYNC();
-#if OVL_CHAIN_RUNS
           // Runs (see replay below): entry i of a target's list only extends the head node
           // when the list's previous entry is the window before on the same diagonal and
           // both are their windows' only occurrence of the target.  The number of such
@@ -941,7 +893,6 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
             WAVE_SYNC();
           }
           WAVE_SYNC();
-#endif
           CPROF_T(t_f);
           CPROF_ADD(3, t_e, t_f);
           uint32_t t0 = tgt[lane], t1 = tgt[lane + 64];
@@ -951,7 +902,6 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
           // next payload is loaded before the current one is applied (no LDS round trip on
           // the loop's dependency chain)
           {
-#if OVL_CHAIN_RUNS
             // An entry followed by rl run entries: once it is applied, if the head node is
             // the one holding it (expected next window o + 1 on its diagonal), each run entry
             // would take Add_Match's first branch -- Len++ -- so the run is applied at once:
@@ -978,21 +928,6 @@ __global__ void __launch_bounds__(256, OVL_CHAIN_OCC) k_chain(ChainArgs A) {
                 }
               }
             };
-#else
-            auto replay = [&](SlotState &ss, uint32_t b, uint32_t n) {
-              uint32_t v = n ? sv[b] : 0u;
-              for (uint32_t i = 0; i < n; i++) {
-                const uint32_t cur = v;
-                if (i + 1 < n) v = sv[b + i + 1];
-                const int32_t pp = (int32_t)(cur & 0x1FFFFFu);
-                const int32_t o_j = (int32_t)(base + (cur >> 21));
-                ss.diag_ct++;                                 // Add_Ref (:203-206)
-                if (ss.diag_bgn > o_j) ss.diag_bgn = o_j;
-                if (ss.diag_end < o_j) ss.diag_end = o_j;
-                add_match(ss, pp, o_j, k, A.pool, W, A, lane);
-              }
-            };
-#endif
             replay(s0, cnt[lane], cnt[OVL_MAXT + lane]);
             replay(s1, cnt[lane + 64], cnt[OVL_MAXT + lane + 64]);
           }

@@ -63,7 +63,7 @@ class _Stats(ctypes.Structure):
          ("generic_pairs", ctypes.c_uint64), ("ext_waves", ctypes.c_uint32),
          ("generic_waves", ctypes.c_uint32), ("stage_len", ctypes.c_uint32),
          ("long_stage_len", ctypes.c_uint32), ("seed_nodes", ctypes.c_uint64),
-         ("probe_sorted_launches", ctypes.c_uint32)]
+         ("probe_sorted_launches", ctypes.c_uint32), ("sq_resorted", ctypes.c_uint32)]
 
 
 class _HashLimits(ctypes.Structure):
@@ -92,7 +92,7 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
 _lib = None
 
 
-ABI_VERSION = 6          # OVL_ABI_VERSION of include/canu_ovl.h
+ABI_VERSION = 7          # OVL_ABI_VERSION of include/canu_ovl.h
 
 
 def load_library(path: str | None = None):

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 6
+#define OVL_ABI_VERSION 7
 
 typedef enum {
   OVL_OK               =  0,
@@ -237,6 +237,9 @@ typedef struct {
   uint32_t probe_sorted_launches;  /* of probe_launches: the sorted-window probe
                                       (k_probe_sorted, ABI 6); its ms_probe_kernel and
                                       probe_bytes are that kernel's alone */
+  uint32_t sq_resorted;            /* sorted-window runs whose partial-range radix sort failed
+                                      its order / permutation check and were sorted again
+                                      over all key bits (ABI 7) */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(built):
 
 
 def test_abi_version(built):
-    assert oic.load_library().ovl_abi_version() == 6
+    assert oic.load_library().ovl_abi_version() == 7
 
 
 def test_driver_defaults_match_reference(built):
