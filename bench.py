@@ -259,6 +259,7 @@ class Configs2:
         offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
         self._keep = (bases, torch.from_numpy(offsets.view(np.int64)).to(self.dev))
         self.total_bases = int(lengths.sum(dtype=np.uint64))
+        self.nloaded = int(lengths.shape[0])
         self.n = n
         self.P = OicParameters(Kmer_Len=a.k, maxErate=float(np.float32(a.maxerate)),
                                Min_Olap_Len=a.minlength).finalize()
@@ -409,14 +410,24 @@ class Configs4Rank(Configs2):
         """This rank's slice of the read set, on the host before any GPU call (the
         generator's worker pool is forked here)."""
         from canu_amd.synth import synth_reads_parallel
+        from canu_amd.dist import hash_block_jobs
         a, n = self.args, self.args.reads
         genome_len = int(n * a.read_len / a.coverage)
+        plan_ranks = 8 if self.world == 1 else self.world
+        load = self.HASHLOAD * (1 << self.HASHBITS) * 21
+        self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load)
+        self.job = self.jobs[a.rank_job if self.world == 1 else self.rank]
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world
+        if self.world == 1:
+            # one GPU runs one job of the plan: only the reads it touches (1..max(h, r)) are
+            # generated and loaded; the genome is the whole read set's, so they are the same
+            # reads as in the full set (read i depends on (seed, i) and the genome alone)
+            hi = max(self.job["h"][1], self.job["r"][1])
         # CANU_C4_READS_CACHE=<dir> (one rank): the read set saved there once and loaded by
         # later runs (saves the generation's ~10 s in repeated PMC passes)
         cache = os.environ.get("CANU_C4_READS_CACHE") if self.world == 1 else None
-        key = f"c4_{n}_{a.read_len}_{a.coverage}_{a.read_error}_{a.seed}"
+        key = f"c4_{n}_{hi}_{a.read_len}_{a.coverage}_{a.read_error}_{a.seed}"
         if cache and os.path.exists(os.path.join(cache, key + "_lengths.npy")):
             from canu_amd.synth import ReadSet
             lens = np.load(os.path.join(cache, key + "_lengths.npy"))
@@ -436,7 +447,7 @@ class Configs4Rank(Configs2):
 
     def setup(self, OicParameters, OverlapInCore):
         import torch
-        from canu_amd.dist import gather_read_store, hash_block_jobs
+        from canu_amd.dist import gather_read_store
         a, n = self.args, self.args.reads
         part, self._part = self._part, None
         if self.world == 1:
@@ -446,16 +457,12 @@ class Configs4Rank(Configs2):
             bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(self.dev),
                                                part.lengths, self.dist, self.dev)
         del part
-        offsets = np.zeros(n, dtype=np.uint64)
+        offsets = np.zeros(lengths.shape[0], dtype=np.uint64)
         offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
         self._keep = (bases, torch.from_numpy(offsets.view(np.int64)).to(self.dev))
         self.total_bases = int(lengths.sum(dtype=np.uint64))
+        self.nloaded = int(lengths.shape[0])
         self.n = n
-        plan_ranks = 8 if self.world == 1 else self.world
-        load = self.HASHLOAD * (1 << self.HASHBITS) * 21
-        self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load)
-        ji = a.rank_job if self.world == 1 else self.rank
-        self.job = self.jobs[ji]
         (h_lo, h_hi), (r_lo, r_hi) = self.job["h"], self.job["r"]
         hashed = int(lengths[h_lo - 1:h_hi].sum(dtype=np.uint64)) + (h_hi - h_lo + 1)
         self.P = OicParameters(Kmer_Len=a.k, maxErate=float(np.float32(a.maxerate)),
@@ -575,7 +582,7 @@ def rooflines(args, job, st, world):
     issue -- with its HBM figures beside; and the hash-probe kernel against HBM."""
     traffic, note = load_traffic(job, world)
     n = job.n
-    avg_len = job.total_bases / max(n, 1)
+    avg_len = job.total_bases / max(job.nloaded, 1)
     strand = 8.0 * (np.ceil(avg_len / 32.0) + 1.0)
     # algorithmic HBM bytes of k_extend per pair: both packed strands, 16 B per seed-match
     # node (the Add_Match lists), 24 B per record written

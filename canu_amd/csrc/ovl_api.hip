@@ -471,6 +471,88 @@ int ovl_probe_replay(ovl_ctx *c, uint32_t bgn, uint32_t end, double *gloads_per_
   return OVL_OK;
 }
 
+// ---- index export / import (ABI 7) ----------------------------------------------------
+int ovl_export_index(ovl_ctx *c, ovl_index_desc *o) {
+  if (!c || !o) return fail(OVL_ERR_STATE, "null argument");
+  if (!c->have_index) return fail(OVL_ERR_STATE, "no index built");
+  memset(o, 0, sizeof(*o));
+  o->bgn_iid = c->hash_bgn_iid;
+  o->end_iid = c->hash_end_iid;
+  o->first_iid = c->first_iid;
+  o->nreads = c->nreads;
+  o->kmer_len = c->P.kmer_len;
+  o->tab_bits = c->tab_bits;
+  o->slice_bits = c->slice_bits;
+  o->hash_lib_lo = c->stats_hash_lib_lo;
+  o->hash_lib_hi = c->stats_hash_lib_hi;
+  o->records = c->index_records;
+  o->table = c->d_tab.p;
+  o->table_bytes = sizeof(TabEntry) << c->tab_bits;
+  o->occ = c->d_occ.p;
+  o->occ_bytes = 8ull * c->index_records;
+  if (c->bloom_ok) {
+    o->bloom_w = c->bloom_w;
+    o->bloom = c->d_bloom.p;
+    o->bloom_bytes = 8ull * ((1ull << (c->tab_bits - c->slice_bits)) << c->bloom_w);
+  }
+  o->read_flags = c->d_flags.p;
+  o->read_flags_bytes = 4ull * c->nreads;
+  return OVL_OK;
+}
+
+int ovl_import_index(ovl_ctx *c, const ovl_index_desc *in) {
+  if (!c || !in) return fail(OVL_ERR_STATE, "null argument");
+  if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
+  if (in->first_iid != c->first_iid || in->nreads != c->nreads)
+    return fail(OVL_ERR_BAD_PARAM, "index of reads %u+%u, this context holds %u+%u",
+                in->first_iid, in->nreads, c->first_iid, c->nreads);
+  if (in->kmer_len != c->P.kmer_len)
+    return fail(OVL_ERR_BAD_PARAM, "index of %u-mers, this context uses -k %u", in->kmer_len,
+                c->P.kmer_len);
+  if (in->tab_bits > 40 || in->slice_bits > in->tab_bits ||
+      in->table_bytes != (sizeof(TabEntry) << in->tab_bits) || in->occ_bytes != 8ull * in->records ||
+      in->read_flags_bytes != 4ull * in->nreads || !in->table || (in->records && !in->occ) ||
+      !in->read_flags || (in->bloom_bytes && (!in->bloom ||
+      in->bloom_bytes != 8ull * ((1ull << (in->tab_bits - in->slice_bits)) << in->bloom_w))))
+    return fail(OVL_ERR_BAD_PARAM, "inconsistent index descriptor");
+  if (in->end_iid < in->bgn_iid || in->bgn_iid < c->first_iid ||
+      in->end_iid > c->first_iid + c->nreads - 1)
+    return fail(OVL_ERR_BAD_PARAM, "index of hash reads %u-%u outside the loaded reads",
+                in->bgn_iid, in->end_iid);
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  c->have_index = false;
+  if (c->d_tab.alloc(1ull << in->tab_bits) || c->d_occ.alloc(std::max<uint64_t>(in->records, 1)) ||
+      (in->bloom_bytes && c->d_bloom.alloc(in->bloom_bytes / 8)))
+    return fail(OVL_ERR_OOM, "imported index (%.1f GB)",
+                (in->table_bytes + in->occ_bytes + in->bloom_bytes) / 1e9);
+  HIPC(hipEventRecord(c->ev[0], s));
+  HIPC(hipMemcpyAsync(c->d_tab.p, in->table, in->table_bytes, hipMemcpyDefault, s));
+  if (in->records)
+    HIPC(hipMemcpyAsync(c->d_occ.p, in->occ, in->occ_bytes, hipMemcpyDefault, s));
+  if (in->bloom_bytes)
+    HIPC(hipMemcpyAsync(c->d_bloom.p, in->bloom, in->bloom_bytes, hipMemcpyDefault, s));
+  HIPC(hipMemcpyAsync(c->d_flags.p, in->read_flags, in->read_flags_bytes, hipMemcpyDefault, s));
+  HIPC(hipEventRecord(c->ev[1], s));
+  HIPC(hipStreamSynchronize(s));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+  c->stats.ms_index = ms;                      // the copy stands in for the build
+  c->hash_bgn_iid = in->bgn_iid;
+  c->hash_end_iid = in->end_iid;
+  c->tab_bits = in->tab_bits;
+  c->slice_bits = in->slice_bits;
+  c->bloom_w = in->bloom_bytes ? in->bloom_w : 0;
+  c->bloom_ok = in->bloom_bytes != 0;
+  c->index_records = in->records;
+  c->stats_hash_lib_lo = in->hash_lib_lo;
+  c->stats_hash_lib_hi = in->hash_lib_hi;
+  // the copied flags carry the exporter's NOHASH bits (-H): a later build re-derives them
+  if (in->hash_lib_lo != 0 || in->hash_lib_hi != UINT32_MAX) c->nohash_set = true;
+  c->have_index = true;
+  return OVL_OK;
+}
+
 int ovl_ctx_create(const ovl_params *p, int device, ovl_ctx **out) {
   *out = nullptr;
   if (p->kmer_len == 0) return fail(OVL_ERR_BAD_PARAM, "kmer length (-k) needed");
@@ -2679,6 +2761,60 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
 }
 
 // OverlapDriver (overlapInCore.C:190-300).
+// Query chunks of an OverlapDriver job whose sorted query windows (sq_prepare) would not fit
+// the HBM all at once (configs[4]'s full-size rank jobs: ~28 G windows, 330 GB of keys and
+// ids).  The ref range bgn..end is cut into consecutive chunks whose windows fit the budget
+// sq_prepare checks against (half the HBM free now and held by sorted windows, less a margin
+// for the next builds), counted with sq_prepare's unit rule.  One chunk: the whole range.
+// OVL_SQ_CHUNK_WINDOWS (tests) caps a chunk's windows.
+static std::vector<std::pair<uint32_t, uint32_t>> plan_query_chunks(ovl_ctx *c, uint32_t bgn,
+                                                                    uint32_t end, uint32_t lib_lo,
+                                                                    uint32_t lib_hi) {
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  const uint32_t k = c->P.kmer_len;
+  size_t fr = 0, tot = 0;
+  uint64_t budget = UINT64_MAX;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+    const uint64_t half = (fr + sq_held_bytes(c)) / 2;
+    const uint64_t fixed = 24ull * (1ull << 29) + 8ull * (1ull << 20);   // one run's sort scratch
+    budget = half > fixed ? (half - fixed) * 9 / 10 : 0;
+  }
+  uint64_t wcap = budget / 13;                       // 12 B per window + the unit arrays
+  if (const char *e = getenv("OVL_SQ_CHUNK_WINDOWS")) wcap = std::min<uint64_t>(wcap, strtoull(e, nullptr, 10));
+  wcap = std::max<uint64_t>(wcap, 1);
+  uint32_t lo = bgn;
+  uint64_t w = 0;
+  for (uint32_t a = bgn; a <= end && a >= bgn; a++) {
+    const uint32_t r = a - c->first_iid;
+    const int32_t L = (int32_t)c->h_len[r];
+    const uint32_t lib = read_lib(c, r);
+    uint64_t add = 0;
+    if (!(lib < lib_lo || lib > lib_hi || L < c->P.min_olap_len || L < (int32_t)k))
+      add = 2ull * (uint64_t)(L - (int32_t)k + 1);
+    if (w + add > wcap && a > lo) {
+      out.push_back({lo, a - 1});
+      lo = a;
+      w = 0;
+    }
+    w += add;
+  }
+  if (end >= bgn) out.push_back({lo, end});
+  return out;
+}
+
+// ref reads of bgn..end that find_impl counts in ref_reads (Process_Overlaps.C:108-114)
+static uint64_t count_ref_reads(const ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo,
+                                uint32_t lib_hi) {
+  uint64_t n = 0;
+  for (uint32_t a = bgn; a <= end && a >= bgn; a++) {
+    const uint32_t r = a - c->first_iid;
+    const uint32_t lib = read_lib(c, r);
+    if (lib < lib_lo || lib > lib_hi || (int32_t)c->h_len[r] < c->P.min_olap_len) continue;
+    n++;
+  }
+  return n;
+}
+
 int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) {
   if (!c || !d || !n_out) return fail(OVL_ERR_STATE, "null argument");
   if (c->nreads == 0) return fail(OVL_ERR_STATE, "no reads loaded");
@@ -2732,6 +2868,22 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     ovl_ctx *c;
     ~SqOff() { c->sq_request = false; sq_release(c, false); }
   } sq_off{c};
+  // When the job's sorted query windows do not fit the HBM at once (configs[4]'s full-size
+  // rank jobs), the ref range is cut into query chunks (plan_query_chunks): the batches are
+  // built and searched by the first chunk as below, then every later chunk is sorted once and
+  // searched by each batch whose reads reach past the chunk's first read (a query meets only
+  // hash reads with larger IDs: find_impl's a < hash_end_iid), the batch rebuilt over its
+  // recorded range.  Records and counters are sums over (batch, query) searches, so the
+  // order does not change them.
+  std::vector<std::pair<uint32_t, uint32_t>> qchunks;       // decided at the first batch
+  std::vector<std::pair<uint32_t, uint32_t>> bat;           // every batch's [bgn, end]
+  std::vector<std::pair<size_t, size_t>> later;            // (chunk, batch) searches after
+  auto plan_later = [&]() {
+    later.clear();
+    for (size_t qi = 1; qi < qchunks.size(); qi++)
+      for (size_t bi = 0; bi < bat.size(); bi++)
+        if (qchunks[qi].first < bat[bi].second) later.push_back({qi, bi});
+  };
   while (bgn < g_end_hash) {                                             // :222
     if (end > g_end_hash) end = g_end_hash;
     uint32_t loaded = 0;
@@ -2741,8 +2893,9 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     const auto t1 = std::chrono::steady_clock::now();
     end = loaded;
     batches++;
+    bat.push_back({bgn, end});
     if (any_ref) {
-      // the batches' pairs are extended together: the last batch flushes what is pending
+      // the batches' pairs are extended together: the last search flushes what is pending
       uint64_t n = 0;
       const bool last_batch = !(end + 1 < g_end_hash);
       if (sq_mode == 3 && batches == 1) {        // the job's batches, from the first one's reads
@@ -2750,9 +2903,21 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
         sq_auto = (uint64_t)g_end_hash + 1 - g_bgn_hash >= SQ_AUTO_BATCHES * per;
       }
       c->sq_request = sq_mode == 1 || (sq_mode == 2 && batches >= 2) || sq_auto;
-      if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n,
-                          last_batch)))
+      if (batches == 1) {
+        if (sq_mode == 1 || sq_auto)
+          qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref);
+        if (qchunks.empty()) qchunks.push_back({g_bgn_ref, ref_last});
+        if (getenv("OVL_TIMING") && qchunks.size() > 1)
+          fprintf(stderr, "OVL_TIMING query chunks: %zu over refs %u-%u\n", qchunks.size(),
+                  g_bgn_ref, ref_last);
+      }
+      if (last_batch) plan_later();
+      const uint32_t q_hi = qchunks[0].second;
+      if ((rc = find_impl(c, g_bgn_ref, q_hi, d->min_lib_ref, d->max_lib_ref, true, &n,
+                          last_batch && later.empty())))
         return rc;
+      if (qchunks.size() > 1)                    // the later chunks' ref reads, as one search counts them
+        c->stats.ref_reads += count_ref_reads(c, q_hi + 1, ref_last, d->min_lib_ref, d->max_lib_ref);
     }
     if (getenv("OVL_TIMING")) {
       const auto t2 = std::chrono::steady_clock::now();
@@ -2767,7 +2932,39 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     bgn = end + 1;
     end = bgn + L.max_hash_strings - 1;
   }
+  // the later query chunks, each searched by the batches that reach past it (their ref reads
+  // were counted with the first chunk's searches)
+  const uint64_t ref_reads = c->stats.ref_reads;
+  for (size_t li = 0; li < later.size(); li++) {
+    const auto [qi, bi] = later[li];
+    uint32_t hb = bat[bi].first, he = bat[bi].second;
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = clip_hash_range(c, hb, he);
+    if (rc) return rc;
+    const bool bloom = !c->sq.on || sq_bloom();
+    if ((rc = build_index(c, hb, he, bloom)) == OVL_ERR_OOM) {
+      release_find_buffers(c);
+      rc = build_index(c, hb, he, bloom);
+    }
+    if (rc) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
+    uint64_t n = 0;
+    if ((rc = find_impl(c, qchunks[qi].first, qchunks[qi].second, d->min_lib_ref, d->max_lib_ref,
+                        true, &n, li + 1 == later.size())))
+      return rc;
+    if (getenv("OVL_TIMING")) {
+      const auto t2 = std::chrono::steady_clock::now();
+      fprintf(stderr, "OVL_TIMING query chunk %zu (refs %u-%u) x batch %zu (hash %u-%u): wall "
+              "build %.1f ms, find %.1f ms; device index %.1f seed %.1f extend %.1f ms so far\n",
+              qi, qchunks[qi].first, qchunks[qi].second, bi + 1, hb, he,
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(), c->stats.ms_index,
+              c->stats.ms_seed, c->stats.ms_extend);
+    }
+  }
+  if (!later.empty()) c->stats.ref_reads = ref_reads;
   c->stats.hash_batches = batches;
+  c->stats.query_chunks = (uint32_t)qchunks.size();
   *n_out = c->nout;
   return OVL_OK;
 }

@@ -63,7 +63,20 @@ class _Stats(ctypes.Structure):
          ("generic_pairs", ctypes.c_uint64), ("ext_waves", ctypes.c_uint32),
          ("generic_waves", ctypes.c_uint32), ("stage_len", ctypes.c_uint32),
          ("long_stage_len", ctypes.c_uint32), ("seed_nodes", ctypes.c_uint64),
-         ("probe_sorted_launches", ctypes.c_uint32), ("sq_resorted", ctypes.c_uint32)]
+         ("probe_sorted_launches", ctypes.c_uint32), ("sq_resorted", ctypes.c_uint32),
+         ("query_chunks", ctypes.c_uint32)]
+
+
+class _IndexDesc(ctypes.Structure):
+    """ovl_index_desc (include/canu_ovl.h, ABI 7): a built index as device buffers."""
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "bgn_iid", "end_iid", "first_iid", "nreads", "kmer_len", "tab_bits", "slice_bits",
+        "bloom_w", "hash_lib_lo", "hash_lib_hi")] + \
+        [("records", ctypes.c_uint64),
+         ("table", ctypes.c_void_p), ("table_bytes", ctypes.c_uint64),
+         ("occ", ctypes.c_void_p), ("occ_bytes", ctypes.c_uint64),
+         ("bloom", ctypes.c_void_p), ("bloom_bytes", ctypes.c_uint64),
+         ("read_flags", ctypes.c_void_p), ("read_flags_bytes", ctypes.c_uint64)]
 
 
 class _HashLimits(ctypes.Structure):
@@ -87,7 +100,8 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
            "ovl_fetch_overlaps", "ovl_get_stats", "ovl_ctx_stream", "ovl_write_ovb",
            "ovl_ctx_write_ovb", "ovl_ctx_write_stats", "ovl_set_read_libraries",
            "ovl_hash_limits_init", "ovl_build_hash_batch", "ovl_driver_params_init",
-           "ovl_overlap_driver", "ovl_seed_hits", "ovl_probe_ceiling", "ovl_probe_replay"]
+           "ovl_overlap_driver", "ovl_seed_hits", "ovl_probe_ceiling", "ovl_probe_replay",
+           "ovl_export_index", "ovl_import_index"]
 
 _lib = None
 
@@ -143,6 +157,8 @@ def load_library(path: str | None = None):
     lib.ovl_overlap_driver.argtypes = [ctypes.c_void_p, P(_DriverParams), P(ctypes.c_uint64)]
     lib.ovl_seed_hits.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_void_p, ctypes.c_uint64, P(ctypes.c_uint64)]
+    lib.ovl_export_index.argtypes = [ctypes.c_void_p, P(_IndexDesc)]
+    lib.ovl_import_index.argtypes = [ctypes.c_void_p, P(_IndexDesc)]
     _lib = lib
     return lib
 
@@ -450,6 +466,17 @@ class OverlapInCore:
         self._check(self.lib.ovl_seed_hits(self.ctx, bgn, end, h.ctypes.data, n.value,
                                            ctypes.byref(n)))
         return h[:n.value]
+
+    def export_index(self) -> "_IndexDesc":
+        """The context's built index as device buffers (valid until its next build)."""
+        d = _IndexDesc()
+        self._check(self.lib.ovl_export_index(self.ctx, ctypes.byref(d)))
+        return d
+
+    def import_index(self, desc: "_IndexDesc") -> None:
+        """Copy an exported index (this GPU, a peer, or buffers a collective filled) into
+        this context, which then searches it as if it had built it."""
+        self._check(self.lib.ovl_import_index(self.ctx, ctypes.byref(desc)))
 
     def run(self, rs, skip_kmers=None) -> np.ndarray:
         """OverlapDriver() for one hash batch: load, index, search, fetch (sorted)."""

@@ -240,6 +240,9 @@ typedef struct {
   uint32_t sq_resorted;            /* sorted-window runs whose partial-range radix sort failed
                                       its order / permutation check and were sorted again
                                       over all key bits (ABI 7) */
+  uint32_t query_chunks;           /* query chunks of the last driver run whose sorted
+                                      windows were searched one after another (1: the
+                                      whole -r range at once; ABI 7) */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);
@@ -278,6 +281,34 @@ int         ovl_probe_ceiling(ovl_ctx *ctx, double *gloads_per_s, uint64_t *tabl
  * share k-mers, so the probe can beat it).  Reads the table only; needs an index. */
 int         ovl_probe_replay(ovl_ctx *ctx, uint32_t bgn, uint32_t end, double *gloads_per_s,
                              uint64_t *n_windows);
+
+/* A built k-mer index as device buffers (ABI 7): what Build_Hash_Index leaves for
+ * Find_Overlaps (overlapInCore-Build_Hash_Index.C:443 -- the hash table, the occurrence
+ * lists, and the reads' screened-end flags Mark_Skip_Kmers sets), so that one process can
+ * build it and others search it: the north star's "all-gather / share the k-mer index over
+ * xGMI" (INTEGRATION.md).
+ *   ovl_export_index  fills `out` with this context's device pointers and byte counts; they
+ *                     stay valid until its next index build or ovl_ctx_destroy.
+ *   ovl_import_index  copies an exported index -- device memory of this GPU, a peer's, or
+ *                     buffers a collective filled -- into this context (hipMemcpy), which then
+ *                     searches it as if it had built it.  The context must hold the same reads
+ *                     (first_iid, read count) and k-mer length as the exporter. */
+typedef struct {
+  uint32_t bgn_iid, end_iid;       /* hashed reads (-h)                                    */
+  uint32_t first_iid, nreads;      /* the read store the index was built over              */
+  uint32_t kmer_len;
+  uint32_t tab_bits, slice_bits;   /* table: 2^tab_bits 16-B slots in 2^slice_bits slices  */
+  uint32_t bloom_w;                /* Bloom filter: 2^bloom_w 8-B words per slice          */
+  uint32_t hash_lib_lo, hash_lib_hi;   /* -H libraries the index was built from            */
+  uint64_t records;                /* occurrence records                                   */
+  const void *table;      uint64_t table_bytes;
+  const void *occ;        uint64_t occ_bytes;
+  const void *bloom;      uint64_t bloom_bytes;    /* 0 bytes: no filter                   */
+  const void *read_flags; uint64_t read_flags_bytes;   /* 4 B per loaded read              */
+} ovl_index_desc;
+
+int         ovl_export_index(ovl_ctx *ctx, ovl_index_desc *out);
+int         ovl_import_index(ovl_ctx *ctx, const ovl_index_desc *in);
 
 #ifdef __cplusplus
 }

@@ -127,3 +127,23 @@ def test_record_layout():
     assert oic.RECORD_DTYPE.itemsize == 24
     r = np.zeros(1, dtype=oic.RECORD_DTYPE)
     assert r.dtype.names == ("a", "b", "w0", "w1")
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of ovl_stats and ovl_index_desc have the header's sizes and field
+    offsets (compiled against include/canu_ovl.h with the host C compiler)."""
+    import subprocess
+    inc = os.path.join(ROOT, "include")
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include <stddef.h>\n#include <stdio.h>\n#include "canu_ovl.h"\n'
+        'int main(void) { printf("%zu %zu %zu %zu %zu\\n", sizeof(ovl_stats), '
+        'offsetof(ovl_stats, sq_resorted), offsetof(ovl_stats, query_chunks), '
+        'sizeof(ovl_index_desc), offsetof(ovl_index_desc, read_flags_bytes)); return 0; }\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got == [ctypes.sizeof(oic._Stats), oic._Stats.sq_resorted.offset,
+                   oic._Stats.query_chunks.offset, ctypes.sizeof(oic._IndexDesc),
+                   oic._IndexDesc.read_flags_bytes.offset]

@@ -1,0 +1,94 @@
+"""Sharing a built k-mer index between contexts (ovl_export_index / ovl_import_index, ABI 7):
+the north star's "one index, shared over xGMI" path.  One context builds the index
+(Build_Hash_Index, overlapInCore-Build_Hash_Index.C:443 -- table, occurrence lists, and the
+screened-end flags Mark_Skip_Kmers sets on hashed reads); a second context holding the same
+reads imports it by device copy and searches it (Find_Overlaps.C:284): its records and -s
+counters must equal the builder's own search, and the oracle's.
+"""
+import numpy as np
+import pytest
+
+from canu_amd.synth import synth_reads
+
+import oracle
+
+STAT_KEYS = ["total_overlaps", "kmer_hits_with_olap", "kmer_hits_without_olap",
+             "multi_overlaps", "contained_overlaps", "dovetail_overlaps", "kmer_hits_skipped",
+             "seed_hits", "pairs"]
+
+
+def _end_skip_kmers(rs, k=22, step=23, span=110):
+    out = set()
+    for r in range(0, rs.nreads, 3):
+        seq = rs.read(r).decode().upper()
+        for i in list(range(0, span, step)) + list(range(len(seq) - span, len(seq) - k, step)):
+            s = seq[i:i + k]
+            if len(s) == k and set(s) <= set("ACGT"):
+                out.add(s)
+    return sorted(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [False, True])
+def test_gpu_imported_index_searches_like_the_built_one(built, batch):
+    """batch=False: ovl_build_hash_index over every read (one table, no filter);
+    batch=True: an OverlapDriver batch (ovl_build_hash_batch, reads 1-90, with its Bloom
+    filter) searched by every read, most of which lie outside it.  Skip k-mers near read ends
+    make the imported screened-end flags matter (the hopeless check reads them)."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    rs = synth_reads(n_reads=240, read_len=3000, genome_len=60_000, error_rate=0.035, seed=41,
+                     len_jitter=0.3, n_rate=0.001)
+    skip = _end_skip_kmers(rs)
+    P = oracle.default_params(kmer_len=22, max_erate=0.06, min_olap_len=500)
+    O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                      Max_Hash_Strings=90).finalize()
+    a = OverlapInCore(O, device=0)
+    b = OverlapInCore(O, device=0)
+    try:
+        a.load_reads(rs)
+        a.set_skip_kmers(skip)
+        if batch:
+            last = a.build_hash_batch(1, rs.nreads)
+            assert last == 90
+        else:
+            a.build_hash_index(1, rs.nreads)
+        desc = a.export_index()
+        assert desc.records > 0 and desc.table_bytes == 16 << desc.tab_bits
+        assert (desc.bloom_bytes > 0) == batch
+        b.load_reads(rs)
+        b.import_index(desc)
+        got_b = b.fetch(b.find_overlaps(1, rs.nreads))
+        st_b = b.stats()
+        got_a = a.fetch(a.find_overlaps(1, rs.nreads))
+        st_a = a.stats()
+    finally:
+        a.close()
+        b.close()
+    assert got_a.shape[0] > 100
+    assert got_b.shape == got_a.shape and np.array_equal(got_b, got_a)
+    for key in STAT_KEYS:
+        assert st_b[key] == st_a[key], (key, st_b[key], st_a[key])
+    if not batch:
+        want = oracle.run_oracle(rs, P, skip_kmers=skip)
+        assert np.array_equal(got_b, want)
+
+
+@pytest.mark.gpu
+def test_gpu_import_rejects_another_read_store(built):
+    """An index built over other reads (or another k) is refused, not searched."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore, OvlError
+    rs = synth_reads(n_reads=60, read_len=2000, genome_len=20_000, error_rate=0.02, seed=42)
+    O = OicParameters(Kmer_Len=22, maxErate=0.06, Min_Olap_Len=500).finalize()
+    a = OverlapInCore(O, device=0)
+    b = OverlapInCore(O, device=0)
+    try:
+        a.load_reads(rs)
+        a.build_hash_index(1, rs.nreads)
+        desc = a.export_index()
+        rs2 = synth_reads(n_reads=59, read_len=2000, genome_len=20_000, error_rate=0.02, seed=42)
+        b.load_reads(rs2)
+        with pytest.raises(OvlError, match="index of reads"):
+            b.import_index(desc)
+    finally:
+        a.close()
+        b.close()

@@ -114,3 +114,29 @@ def test_gpu_sorted_windows_corrupt_sort_falls_back(built, monkeypatch):
     assert got.shape == want.shape and np.array_equal(got, want)
     for _, ok in STAT_KEYS:
         assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
+
+
+@pytest.mark.gpu
+def test_gpu_query_chunks_are_exact(built, monkeypatch):
+    """Query chunks (plan_query_chunks in ovl_api.hip): when the job's sorted windows do not
+    fit at once, the -r range is searched chunk after chunk, every batch rebuilt for each
+    later chunk it reaches past.  OVL_SQ_CHUNK_WINDOWS forces ~7 chunks on the small job: the
+    same records and -s counters as the oracle's OverlapDriver, with N bases and poly-A."""
+    from canu_amd.overlap_in_core import OverlapInCore
+    monkeypatch.setenv("OVL_SQ", "1")
+    monkeypatch.setenv("OVL_SQ_CHUNK_WINDOWS", "200000")
+    rs = _reads()
+    P = _params()
+    rr = (1, 240)
+    oic = OverlapInCore(_opts(P, rr), device=0)
+    try:
+        got = oic.run_driver(rs)
+        st = oic.stats()
+    finally:
+        oic.close()
+    want, wst, batches = _oracle(rs, P, rr)
+    assert st["query_chunks"] >= 5
+    assert st["hash_batches"] == len(batches)
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for _, ok in STAT_KEYS:
+        assert st[ok] == wst[ok], (ok, st[ok], wst[ok])

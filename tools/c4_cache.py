@@ -1,34 +1,23 @@
 #!/usr/bin/env python3
-"""Write bench.py's configs4-rank read set (one rank, default sizes or --reads N) to the cache
-directory CANU_C4_READS_CACHE names, so that runs under rocprofv3 (tools/prof_traffic.sh)
-load it instead of generating it with a worker pool.  usage: CANU_C4_READS_CACHE=dir
-python tools/c4_cache.py [bench.py configs4-rank options]"""
+"""Write bench.py's configs4-rank read set (one GPU: the reads of the --rank-job's job) to the
+cache directory CANU_C4_READS_CACHE names, so that runs under rocprofv3 load it instead of
+generating it with a worker pool (a pool forked by a process the profiler has attached to the
+GPU).  usage: CANU_C4_READS_CACHE=dir python tools/c4_cache.py [bench.py configs4-rank options]"""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-
 import bench  # noqa: E402
-from canu_amd.synth import synth_reads_parallel  # noqa: E402
 
 
 def main():
+    assert os.environ.get("CANU_C4_READS_CACHE"), "set CANU_C4_READS_CACHE"
     a = bench.parse_args(["--workload", "configs4-rank"] + sys.argv[1:])
-    cache = os.environ["CANU_C4_READS_CACHE"]
-    n = a.reads
-    key = f"c4_{n}_{a.read_len}_{a.coverage}_{a.read_error}_{a.seed}"
-    if os.path.exists(os.path.join(cache, key + "_lengths.npy")):
-        print("cached", key)
-        return
-    part = synth_reads_parallel(n, a.read_len, int(n * a.read_len / a.coverage), a.read_error,
-                                seed=a.seed, len_jitter=0.2, read_range=(0, n), workers=16)
-    os.makedirs(cache, exist_ok=True)
-    np.save(os.path.join(cache, key + "_bases.npy"), part.bases)
-    np.save(os.path.join(cache, key + "_lengths.npy"), part.lengths)
-    print("wrote", key, part.total_bases(), "bases")
+    job = bench.Configs4Rank(a, 0, 1, None)
+    job.generate()                       # writes the cache (or finds it there)
+    print("cached", job._part.lengths.shape[0], "reads,", int(job._part.lengths.sum()), "bases")
 
 
 if __name__ == "__main__":
