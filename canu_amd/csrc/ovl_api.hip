@@ -2854,91 +2854,139 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   uint32_t bgn = g_bgn_hash;
   uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
   uint64_t batches = 0;
-  // the query windows sorted once for the job's batches (sq_prepare): OVL_SQ=2 from the
-  // second batch on, 1 from the first, 0 never, 3 (the default) from the first when the first
-  // batch's size puts the job at SQ_AUTO_BATCHES batches or more.  The sort costs several
-  // random-lookup probes of the same windows (the configs[4] rank-0 job at 1/8 scale, 14
-  // batches: sort 134 ms, seed 847 against 892 ms; profiles/r04y_c4_*.log), so a job of a few
-  // batches keeps the random-lookup probe.
-  const uint64_t SQ_AUTO_BATCHES = 10;
+  // the query windows sorted once per query chunk (sq_prepare): OVL_SQ=1 always, 0 never,
+  // 2 from a job's second search on, 3 (the default) when a query chunk is searched by
+  // SQ_AUTO_SEARCHES indexes or more.  The sort costs about one random-lookup probe of the
+  // same windows (the configs[4] rank-0 job at 1/8 scale, 14 batches: sort 134 ms, seed 847
+  // against 892 ms; profiles/r04y_c4_*.log).
+  const uint64_t SQ_AUTO_SEARCHES = 3;
   int sq_mode = 3;
   if (const char *e = getenv("OVL_SQ")) sq_mode = atoi(e);
-  bool sq_auto = false;
   struct SqOff {
     ovl_ctx *c;
     ~SqOff() { c->sq_request = false; sq_release(c, false); }
   } sq_off{c};
-  // When the job's sorted query windows do not fit the HBM at once (configs[4]'s full-size
-  // rank jobs), the ref range is cut into query chunks (plan_query_chunks): the batches are
-  // built and searched by the first chunk as below, then every later chunk is sorted once and
-  // searched by each batch whose reads reach past the chunk's first read (a query meets only
-  // hash reads with larger IDs: find_impl's a < hash_end_iid), the batch rebuilt over its
-  // recorded range.  Records and counters are sums over (batch, query) searches, so the
-  // order does not change them.
-  std::vector<std::pair<uint32_t, uint32_t>> qchunks;       // decided at the first batch
-  std::vector<std::pair<uint32_t, uint32_t>> bat;           // every batch's [bgn, end]
-  std::vector<std::pair<size_t, size_t>> later;            // (chunk, batch) searches after
-  auto plan_later = [&]() {
-    later.clear();
-    for (size_t qi = 1; qi < qchunks.size(); qi++)
-      for (size_t bi = 0; bi < bat.size(); bi++)
-        if (qchunks[qi].first < bat[bi].second) later.push_back({qi, bi});
+  auto timing_line = [&](const char *what, double build_ms, double find_ms) {
+    if (!getenv("OVL_TIMING")) return;
+    fprintf(stderr, "OVL_TIMING %s: wall build %.1f ms, find %.1f ms; device index %.1f seed %.1f "
+            "extend %.1f ms, alloc/free %.1f ms (%llu allocs, %.1f GB) so far\n", what, build_ms,
+            find_ms, c->stats.ms_index, c->stats.ms_seed, c->stats.ms_extend, g_alloc_ms,
+            (unsigned long long)g_alloc_n, g_alloc_bytes / 1e9);
   };
-  while (bgn < g_end_hash) {                                             // :222
-    if (end > g_end_hash) end = g_end_hash;
-    uint32_t loaded = 0;
-    const auto t0 = std::chrono::steady_clock::now();
-    int rc = build_batch_impl(c, bgn, end, &L, &loaded);
-    if (rc) return rc;
-    const auto t1 = std::chrono::steady_clock::now();
-    end = loaded;
-    batches++;
-    bat.push_back({bgn, end});
-    if (any_ref) {
-      // the batches' pairs are extended together: the last search flushes what is pending
-      uint64_t n = 0;
-      const bool last_batch = !(end + 1 < g_end_hash);
-      if (sq_mode == 3 && batches == 1) {        // the job's batches, from the first one's reads
-        const uint64_t per = std::max<uint64_t>((uint64_t)end + 1 - bgn, 1);
-        sq_auto = (uint64_t)g_end_hash + 1 - g_bgn_hash >= SQ_AUTO_BATCHES * per;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  // -l (Frag_Olap_Limit) counts a query's overlaps per Find_Overlaps call, i.e. per hash
+  // batch (A_/B_Olaps_For_Frag, Find_Overlaps.C:306), and orders its targets by their first
+  // hit in the batch: those jobs search batch by batch, as the reference does.
+  const bool ordered = c->P.frag_olap_limit != UINT64_MAX;
+  int sb_mode = 1;
+  if (const char *e = getenv("OVL_SUPERBATCH")) sb_mode = atoi(e);
+  if (!any_ref || ordered || sb_mode == 0) {
+    while (bgn < g_end_hash) {                                           // :222
+      if (end > g_end_hash) end = g_end_hash;
+      uint32_t loaded = 0;
+      const auto t0 = clk::now();
+      int rc = build_batch_impl(c, bgn, end, &L, &loaded);
+      if (rc) return rc;
+      const auto t1 = clk::now();
+      end = loaded;
+      batches++;
+      if (any_ref) {
+        // the batches' pairs are extended together: the last batch flushes what is pending
+        uint64_t n = 0;
+        const bool last_batch = !(end + 1 < g_end_hash);
+        c->sq_request = sq_mode == 1 || (sq_mode == 2 && batches >= 2);
+        if ((rc = find_impl(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref, true, &n,
+                            last_batch)))
+          return rc;
       }
-      c->sq_request = sq_mode == 1 || (sq_mode == 2 && batches >= 2) || sq_auto;
-      if (batches == 1) {
-        if (sq_mode == 1 || sq_auto)
-          qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref);
-        if (qchunks.empty()) qchunks.push_back({g_bgn_ref, ref_last});
-        if (getenv("OVL_TIMING") && qchunks.size() > 1)
-          fprintf(stderr, "OVL_TIMING query chunks: %zu over refs %u-%u\n", qchunks.size(),
-                  g_bgn_ref, ref_last);
-      }
-      if (last_batch) plan_later();
-      const uint32_t q_hi = qchunks[0].second;
-      if ((rc = find_impl(c, g_bgn_ref, q_hi, d->min_lib_ref, d->max_lib_ref, true, &n,
-                          last_batch && later.empty())))
-        return rc;
-      if (qchunks.size() > 1)                    // the later chunks' ref reads, as one search counts them
-        c->stats.ref_reads += count_ref_reads(c, q_hi + 1, ref_last, d->min_lib_ref, d->max_lib_ref);
+      char what[96];
+      snprintf(what, sizeof(what), "batch %llu: hash %u-%u", (unsigned long long)batches, bgn, end);
+      timing_line(what, ms_since(t0, t1), ms_since(t1, clk::now()));
+      bgn = end + 1;
+      end = bgn + L.max_hash_strings - 1;
     }
-    if (getenv("OVL_TIMING")) {
-      const auto t2 = std::chrono::steady_clock::now();
-      fprintf(stderr, "OVL_TIMING batch %llu: hash %u-%u, wall build %.1f ms, find %.1f ms; "
-              "device index %.1f seed %.1f extend %.1f ms, alloc/free %.1f ms (%llu allocs, %.1f GB) so far\n",
-              (unsigned long long)batches, bgn, end,
-              std::chrono::duration<double, std::milli>(t1 - t0).count(),
-              std::chrono::duration<double, std::milli>(t2 - t1).count(), c->stats.ms_index,
-              c->stats.ms_seed, c->stats.ms_extend, g_alloc_ms,
-              (unsigned long long)g_alloc_n, g_alloc_bytes / 1e9);
-    }
-    bgn = end + 1;
-    end = bgn + L.max_hash_strings - 1;
+    c->stats.hash_batches = batches;
+    c->stats.query_chunks = any_ref ? 1 : 0;
+    *n_out = c->nout;
+    return OVL_OK;
   }
-  // the later query chunks, each searched by the batches that reach past it (their ref reads
-  // were counted with the first chunk's searches)
-  const uint64_t ref_reads = c->stats.ref_reads;
-  for (size_t li = 0; li < later.size(); li++) {
-    const auto [qi, bi] = later[li];
-    uint32_t hb = bat[bi].first, he = bat[bi].second;
-    const auto t0 = std::chrono::steady_clock::now();
+
+  // ---- super-batches (the default without -l) -----------------------------------------
+  // A query read meets, in every batch it searches, exactly the hashed reads with larger IDs
+  // (Find_Overlaps.C:328), and everything Process_String_Olaps reads of a (query, target)
+  // pair -- its seed hits in window and chain order, its Add_Match list, the target's
+  // screened ends (Mark_Screened_Ends_Chain, Build_Hash_Index.C:147-170: per read), the
+  // query's hi_hits flags (skip k-mers are in every batch's table) -- depends on the pair
+  // alone.  So searching the UNION of consecutive batches' hashed reads gives every pair,
+  // record and -s counter the batches give one by one; only the batches' ends (the table-load
+  // cuts, the one-read tail that is never hashed, :222) need the reference's loading loop.
+  // Phase 1 runs that loop (Build_Hash_Index's stop rules, build_batch_impl) and records the
+  // batches; phase 2 groups consecutive batches into super-batches of up to sb_cap windows;
+  // phase 3 searches every (query chunk, super-batch) pair whose reads can meet: a canu job
+  // of ~100 batches is then ~10 searches of each query instead of ~100.
+  std::vector<std::pair<uint32_t, uint32_t>> bat;            // the reference's batches
+  double phase1_ms = 0;
+  {
+    const auto t0 = clk::now();
+    while (bgn < g_end_hash) {                                           // :222
+      if (end > g_end_hash) end = g_end_hash;
+      uint32_t loaded = 0;
+      int rc = build_batch_impl(c, bgn, end, &L, &loaded);
+      if (rc) return rc;
+      end = loaded;
+      batches++;
+      bat.push_back({bgn, end});
+      bgn = end + 1;
+      end = bgn + L.max_hash_strings - 1;
+    }
+    phase1_ms = ms_since(t0, clk::now());
+  }
+  c->stats.hash_batches = batches;
+  if (bat.empty()) {
+    c->stats.query_chunks = 0;
+    *n_out = c->nout;
+    return OVL_OK;
+  }
+  // phase 2: super-batches of up to sb_cap windows -- a share of what one index may take
+  // (index_window_cap, with this context's current index counted as free), leaving the rest
+  // of the HBM to the sorted query windows and the search buffers.  OVL_SB_WINDOWS caps it.
+  const uint32_t k = c->P.kmer_len;
+  auto batch_windows = [&](uint32_t b, uint32_t e) {
+    uint64_t w = 0;
+    for (uint32_t id = b; id <= e; id++) {
+      const uint32_t r = id - c->first_iid;
+      const uint32_t lib = read_lib(c, r);
+      if (lib >= L.min_lib_hash && lib <= L.max_lib_hash &&
+          (int64_t)c->h_len[r] >= (int64_t)c->P.min_olap_len && c->h_len[r] >= k)
+        w += c->h_len[r] - k + 1;
+    }
+    return w;
+  };
+  uint64_t sb_cap = index_window_cap(c) * 11 / 20;
+  if (const char *e = getenv("OVL_SB_WINDOWS")) sb_cap = std::min<uint64_t>(sb_cap, strtoull(e, nullptr, 10));
+  sb_cap = std::max<uint64_t>(sb_cap, 1);
+  std::vector<std::pair<uint32_t, uint32_t>> sbs;
+  {
+    uint64_t w = 0;
+    for (const auto &b : bat) {
+      const uint64_t bw = batch_windows(b.first, b.second);
+      if (!sbs.empty() && w + bw <= sb_cap) {
+        sbs.back().second = b.second;
+        w += bw;
+      } else {
+        sbs.push_back(b);
+        w = bw;
+      }
+    }
+  }
+  // phase 3: the searches.  The first super-batch is built, then the query chunks are planned
+  // with its index resident (plan_query_chunks: what the sorted windows may take).
+  auto build_sb = [&](size_t si) -> int {
+    uint32_t hb = sbs[si].first, he = sbs[si].second;
+    if (c->have_index && c->hash_bgn_iid == hb && c->hash_end_iid == he) return OVL_OK;
     int rc = clip_hash_range(c, hb, he);
     if (rc) return rc;
     const bool bloom = !c->sq.on || sq_bloom();
@@ -2946,25 +2994,51 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
       release_find_buffers(c);
       rc = build_index(c, hb, he, bloom);
     }
-    if (rc) return rc;
-    const auto t1 = std::chrono::steady_clock::now();
+    return rc;
+  };
+  const auto t_sb0 = clk::now();
+  if (int rc = build_sb(0)) return rc;
+  const double sb0_ms = ms_since(t_sb0, clk::now());
+  std::vector<std::pair<uint32_t, uint32_t>> qchunks;
+  // searches of one query chunk: the super-batches whose reads reach past its first read
+  auto searches_of = [&](uint32_t qlo) {
     uint64_t n = 0;
-    if ((rc = find_impl(c, qchunks[qi].first, qchunks[qi].second, d->min_lib_ref, d->max_lib_ref,
-                        true, &n, li + 1 == later.size())))
+    for (const auto &sb : sbs) n += qlo < sb.second ? 1 : 0;
+    return n;
+  };
+  const bool sq_on = sq_mode == 1 || (sq_mode == 2 && sbs.size() >= 2) ||
+                     (sq_mode == 3 && searches_of(g_bgn_ref) >= SQ_AUTO_SEARCHES);
+  if (sq_on) qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref);
+  if (qchunks.empty()) qchunks.push_back({g_bgn_ref, ref_last});
+  std::vector<std::pair<size_t, size_t>> plan;               // (chunk, super-batch)
+  for (size_t qi = 0; qi < qchunks.size(); qi++)
+    for (size_t si = 0; si < sbs.size(); si++)
+      if (qchunks[qi].first < sbs[si].second) plan.push_back({qi, si});
+  if (getenv("OVL_TIMING"))
+    fprintf(stderr, "OVL_TIMING super-batches: %llu batches (phase 1 %.1f ms) -> %zu super-batches "
+            "of <= %llu windows, %zu query chunks over refs %u-%u, %zu searches, sorted windows %s\n",
+            (unsigned long long)batches, phase1_ms, sbs.size(), (unsigned long long)sb_cap,
+            qchunks.size(), g_bgn_ref, ref_last, plan.size(), sq_on ? "on" : "off");
+  c->sq_request = sq_on;
+  for (size_t pi = 0; pi < plan.size(); pi++) {
+    const auto [qi, si] = plan[pi];
+    const auto t0 = clk::now();
+    if (int rc = build_sb(si)) return rc;
+    const auto t1 = clk::now();
+    uint64_t n = 0;
+    if (int rc = find_impl(c, qchunks[qi].first, qchunks[qi].second, d->min_lib_ref,
+                           d->max_lib_ref, true, &n, pi + 1 == plan.size()))
       return rc;
-    if (getenv("OVL_TIMING")) {
-      const auto t2 = std::chrono::steady_clock::now();
-      fprintf(stderr, "OVL_TIMING query chunk %zu (refs %u-%u) x batch %zu (hash %u-%u): wall "
-              "build %.1f ms, find %.1f ms; device index %.1f seed %.1f extend %.1f ms so far\n",
-              qi, qchunks[qi].first, qchunks[qi].second, bi + 1, hb, he,
-              std::chrono::duration<double, std::milli>(t1 - t0).count(),
-              std::chrono::duration<double, std::milli>(t2 - t1).count(), c->stats.ms_index,
-              c->stats.ms_seed, c->stats.ms_extend);
-    }
+    char what[128];
+    snprintf(what, sizeof(what), "query chunk %zu (refs %u-%u) x super-batch %zu (hash %u-%u)", qi,
+             qchunks[qi].first, qchunks[qi].second, si, sbs[si].first, sbs[si].second);
+    timing_line(what, pi == 0 ? sb0_ms : ms_since(t0, t1), ms_since(t1, clk::now()));
   }
-  if (!later.empty()) c->stats.ref_reads = ref_reads;
-  c->stats.hash_batches = batches;
+  // ref_reads as the reference counts them: every batch's search over the whole -r range
+  c->stats.ref_reads = batches * count_ref_reads(c, g_bgn_ref, ref_last, d->min_lib_ref,
+                                                 d->max_lib_ref);
   c->stats.query_chunks = (uint32_t)qchunks.size();
+  c->stats.super_batches = (uint32_t)sbs.size();
   *n_out = c->nout;
   return OVL_OK;
 }

@@ -64,7 +64,7 @@ class _Stats(ctypes.Structure):
          ("generic_waves", ctypes.c_uint32), ("stage_len", ctypes.c_uint32),
          ("long_stage_len", ctypes.c_uint32), ("seed_nodes", ctypes.c_uint64),
          ("probe_sorted_launches", ctypes.c_uint32), ("sq_resorted", ctypes.c_uint32),
-         ("query_chunks", ctypes.c_uint32)]
+         ("query_chunks", ctypes.c_uint32), ("super_batches", ctypes.c_uint32)]
 
 
 class _IndexDesc(ctypes.Structure):

@@ -243,6 +243,8 @@ typedef struct {
   uint32_t query_chunks;           /* query chunks of the last driver run whose sorted
                                       windows were searched one after another (1: the
                                       whole -r range at once; ABI 7) */
+  uint32_t super_batches;          /* indexes the last driver run searched: consecutive hash
+                                      batches joined (0: batch by batch, as with -l; ABI 7) */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

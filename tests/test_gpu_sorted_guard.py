@@ -117,14 +117,21 @@ def test_gpu_sorted_windows_corrupt_sort_falls_back(built, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_query_chunks_are_exact(built, monkeypatch):
-    """Query chunks (plan_query_chunks in ovl_api.hip): when the job's sorted windows do not
-    fit at once, the -r range is searched chunk after chunk, every batch rebuilt for each
-    later chunk it reaches past.  OVL_SQ_CHUNK_WINDOWS forces ~7 chunks on the small job: the
-    same records and -s counters as the oracle's OverlapDriver, with N bases and poly-A."""
+@pytest.mark.parametrize("chunk_w,sb_w", [("200000", None), ("200000", "300000"), (None, "250000")])
+def test_gpu_query_chunks_and_super_batches_are_exact(built, monkeypatch, chunk_w, sb_w):
+    """The driver's search plan (ovl_overlap_driver): the reference's hash batches found by
+    its loading loop, consecutive batches joined into super-batches (OVL_SB_WINDOWS caps
+    their k-mers), and the -r range searched in query chunks whose sorted windows fit
+    (OVL_SQ_CHUNK_WINDOWS caps them), every (chunk, super-batch) pair whose reads can meet
+    searched once.  On the small job the caps force ~7 chunks and / or ~5 super-batches: the
+    same records and -s counters as the oracle's batch-by-batch OverlapDriver, with N bases
+    and poly-A stretches."""
     from canu_amd.overlap_in_core import OverlapInCore
-    monkeypatch.setenv("OVL_SQ", "1")
-    monkeypatch.setenv("OVL_SQ_CHUNK_WINDOWS", "200000")
+    monkeypatch.setenv("OVL_SQ", "1" if chunk_w else "0")
+    if chunk_w:
+        monkeypatch.setenv("OVL_SQ_CHUNK_WINDOWS", chunk_w)
+    if sb_w:
+        monkeypatch.setenv("OVL_SB_WINDOWS", sb_w)
     rs = _reads()
     P = _params()
     rr = (1, 240)
@@ -135,8 +142,33 @@ def test_gpu_query_chunks_are_exact(built, monkeypatch):
     finally:
         oic.close()
     want, wst, batches = _oracle(rs, P, rr)
-    assert st["query_chunks"] >= 5
+    if chunk_w:
+        assert st["query_chunks"] >= 5
+    if sb_w:
+        assert 3 <= st["super_batches"] < len(batches)
     assert st["hash_batches"] == len(batches)
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for _, ok in STAT_KEYS:
+        assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
+
+
+@pytest.mark.gpu
+def test_gpu_batch_by_batch_driver_is_exact(built, monkeypatch):
+    """OVL_SUPERBATCH=0: the reference's loop order (build a batch, search it), which -l jobs
+    always take -- the same records and counters."""
+    from canu_amd.overlap_in_core import OverlapInCore
+    monkeypatch.setenv("OVL_SUPERBATCH", "0")
+    rs = _reads()
+    P = _params()
+    rr = (1, 240)
+    oic = OverlapInCore(_opts(P, rr), device=0)
+    try:
+        got = oic.run_driver(rs)
+        st = oic.stats()
+    finally:
+        oic.close()
+    want, wst, batches = _oracle(rs, P, rr)
+    assert st["super_batches"] == 0 and st["hash_batches"] == len(batches)
     assert got.shape == want.shape and np.array_equal(got, want)
     for _, ok in STAT_KEYS:
         assert st[ok] == wst[ok], (ok, st[ok], wst[ok])
