@@ -451,6 +451,12 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #define OVL_RJ 8
 #endif
 #define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
+// OVL_LOG_REL: row e's cells are logged relative to its window base B_e (cell 64j + lane
+// for chunk j, so every chunk store is one aligned 128-B line) and B_e goes to a per-row
+// array the traceback reads; 0: cell = d mod LW (chunk stores straddle lines)
+#ifndef OVL_LOG_REL
+#define OVL_LOG_REL 0
+#endif
 static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 
 #ifdef OVL_PROFILE
@@ -571,10 +577,10 @@ typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 #define OVL_TB_G 1
 #endif
 template <bool L16, int LW = OVL_LOGW>
-__device__ __forceinline__ void ped_traceback_codes(int32_t *log, int32_t tb_e,
-                                                    int32_t tb_d, int32_t last, int32_t *dst,
-                                                    uint32_t lane, int32_t &last_out,
-                                                    int32_t &nd_out) {
+__device__ __forceinline__ void ped_traceback_codes(int32_t *log, const int32_t *rowb,
+                                                    int32_t tb_e, int32_t tb_d, int32_t last,
+                                                    int32_t *dst, uint32_t lane,
+                                                    int32_t &last_out, int32_t &nd_out) {
   constexpr int W = LW;                        // cells per logged row, cell = d mod W
   // rows per window (lanes cover dc-31..dc+31): 16 keeps the unrolled walk and its code
   // registers within wave_ped_reg's 80 VGPRs (24 spills; 16 vs 24: -1 % extension time)
@@ -594,11 +600,21 @@ __device__ __forceinline__ void ped_traceback_codes(int32_t *log, int32_t tb_e,
     const int32_t dc = d;
     const int32_t cell = (dc - 31 + (int32_t)(lane < 63 ? lane : 62)) & (W - 1);
     int32_t V[G * TBR];
+#if OVL_LOG_REL
+    // the rows' window bases: lane i holds B of row kh-1-i
+    typedef __attribute__((address_space(1))) const int32_t g_cb;
+    const int32_t bl = (lane < G * TBR && (int32_t)lane < kh) ? ((g_cb *)rowb)[kh - 1 - (int32_t)lane] : 0;
+#endif
 #pragma unroll
     for (int i = 0; i < G * TBR; i++) {
       const int32_t kk = kh - 1 - i < 0 ? 0 : kh - 1 - i;   // row k-1 for k = kh - i
-      if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
-      else               V[i] = rows[(size_t)kk * W + cell];
+#if OVL_LOG_REL
+      const int32_t ci = (cell - __builtin_amdgcn_readlane(bl, i)) & (W - 1);
+#else
+      const int32_t ci = cell;
+#endif
+      if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + ci];
+      else               V[i] = rows[(size_t)kk * W + ci];
     }
 #pragma unroll 1
     for (int g = 0; g < G; g++) {
@@ -681,11 +697,17 @@ __device__ __forceinline__ double uni(double v) {
 // kernel's scratch made every call start with flat loads from scratch and a full vmcnt(0)
 // wait (which also waited for the caller's spill stores and the row-0 log store).  X is
 // only read by the OVL_PROFILE build.
+// DIR = 0: one function for both directions, the direction a runtime argument (rdir = +1 or
+// -1): half the row-loop code in the instruction cache, for a few more VALU per chunk
+// (OVL_ONE_DIR A/B)
+#ifndef OVL_ONE_DIR
+#define OVL_ONE_DIR 0
+#endif
 template <int DIR, typename SS, bool L16, int RJ = OVL_RJ>
 __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
-    const ExtendArgs &X, int32_t e_cap, int32_t partial_i, int32_t mbed, double bmv_in,
+    const ExtendArgs &X, int32_t rdir, int32_t e_cap, int32_t partial_i, int32_t mbed, double bmv_in,
     double mbts, const lds_u64 *aw, int32_t a0, int32_t m, const lds_u64 *tw, int32_t t0,
-    int32_t n, int32_t limit, int32_t *rows, ml_t *mlim, int32_t *dst,
+    int32_t n, int32_t limit, int32_t *rows, int32_t *rowb, ml_t *mlim, int32_t *dst,
     uint32_t lane) {
   SS A, T;
   A.w = aw; A.len = 0;
@@ -698,6 +720,15 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   static_assert(64 * J <= (1 << WB) && 64 * J <= LW, "key and log layout hold the window");
   static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
   limit = uni(limit);
+  // the direction: compile-time (DIR = +-1) or a wave-uniform runtime value (DIR = 0)
+  const bool fwd = DIR != 0 ? DIR > 0 : uni(rdir) > 0;
+  auto slide_d = [&](int32_t r, int32_t d, int32_t lim) -> int32_t {
+    if constexpr (DIR != 0) return slide_any<DIR>(A, a0, T, t0, r, d, lim);
+    else return fwd ? slide_any<1>(A, a0, T, t0, r, d, lim) : slide_any<-1>(A, a0, T, t0, r, d, lim);
+  };
+  // pa = sa + (+-q), pt = st + (+-(q + d)): (x ^ ms) - ms negates when ms = -1
+  const int32_t ms = fwd ? 0 : -1;
+  const int32_t sa = fwd ? a0 + 1 : a0 - 32, st = fwd ? t0 + 1 : t0 - 32;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;
@@ -710,7 +741,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   int32_t row0 = 0;
   {
     int32_t lim0 = m < n ? m : n;
-    if (lim0 > 0) row0 = slide_any<DIR>(A, a0, T, t0, 0, 0, lim0);
+    if (lim0 > 0) row0 = slide_d(0, 0, lim0);
     row0 = __builtin_amdgcn_readfirstlane(row0);
   }
   if (row0 == m) {
@@ -754,7 +785,15 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   // of the next row would wait for the log stores too
   typedef __attribute__((address_space(1))) cell_t g_cell_t;
   g_cell_t *clog = uni_ptr((g_cell_t *)rows);     // scalar base: stores use saddr + offset
+#if OVL_LOG_REL
+  clog[lane] = (cell_t)R[0];                   // row 0: window base B = -3
+  typedef __attribute__((address_space(1))) int32_t g_rb_t;
+  g_rb_t *grb = uni_ptr((g_rb_t *)rowb);
+  if (lane == 0) grb[0] = B;
+#else
+  (void)rowb;
   clog[(B + (int32_t)lane) & (LW - 1)] = (cell_t)R[0];
+#endif
   typedef __attribute__((address_space(1))) uint8_t g_u8;
   g_u8 *clogb = (g_u8 *)clog;
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
@@ -802,8 +841,14 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       const int32_t lmin = l1 < l2 ? l1 : l2;
       const int32_t lim = q >= -1 ? lmin : -(1 << 30);
 
-      const int32_t pa = (DIR > 0) ? (a0 + 1) + q : (a0 - 32) - q;
-      const int32_t pt = (DIR > 0) ? (t0 + 1) + q + d : (t0 - 32) - q - d;
+      int32_t pa, pt;
+      if constexpr (DIR != 0) {
+        pa = (DIR > 0) ? (a0 + 1) + q : (a0 - 32) - q;
+        pt = (DIR > 0) ? (t0 + 1) + q + d : (t0 - 32) - q - d;
+      } else {
+        pa = ((q ^ ms) - ms) + sa;
+        pt = (((q + d) ^ ms) - ms) + st;
+      }
       const int32_t ia = pa >> 5, it = pt >> 5;
       const uint64_t wa0 = A.w[ia], wa1 = A.w[ia + 1];
       const uint64_t wt0 = T.w[it], wt1 = T.w[it + 1];
@@ -817,8 +862,11 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
       // the first step examines 31 bases (a sentinel mismatch in the 32nd: no clamp of
       // the bit scan), lanes that matched all 31 with more left continue below
-      const int32_t run = (DIR > 0) ? (int32_t)__builtin_ctz(mm | 0x80000000u)
-                                    : (int32_t)__builtin_clz(mm | 1u);
+      int32_t run;
+      if constexpr (DIR != 0)
+        run = (DIR > 0) ? (int32_t)__builtin_ctz(mm | 0x80000000u) : (int32_t)__builtin_clz(mm | 1u);
+      else   // reverse: the 32 bases run downwards, bit 31 first
+        run = (int32_t)__builtin_ctz((fwd ? mm : __builtin_bitreverse32(mm)) | 0x80000000u);
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
       NR[j] = q + 1 + k;                       // lim >= 0 inside the band
@@ -842,7 +890,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
         if (need[j]) {
           if (need[j] & (1ull << lane)) {
             const int32_t d = B + 64 * j + (int32_t)lane;
-            const int32_t sl = slide_any<DIR>(A, a0, T, t0, NR[j], d, RM[j]);
+            const int32_t sl = slide_d(NR[j], d, RM[j]);
             NR[j] += sl;
             RM[j] -= sl;
           }
@@ -956,9 +1004,17 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
         R[j] = v;
         const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
         kmx = key > kmx ? key : kmx;
+#if OVL_LOG_REL
+        *(g_cell_t *)(clogb + (erow | ((uint32_t)(64 * j) + lane) * (uint32_t)sizeof(cell_t))) =
+            (cell_t)v;
+#else
         *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
             (cell_t)v;
+#endif
       }
+#if OVL_LOG_REL
+      if (lane == 0) grb[e] = B;                 // the row's window base, for the traceback
+#endif
       const int32_t K = wave_max(kmx);
       const int32_t M = K >> WB;
       if (M > longest) {                         // Longest, Best_d, Best_e of this row
@@ -1045,7 +1101,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     } else {
       int32_t d = end_d;
       // forward.C:212 -- force the last error to be a mismatch rather than an insertion
-      if (DIR > 0 && end_row == m && 1 + end_pp == end_row && d < pr + 1) d++;
+      if (fwd && end_row == m && 1 + end_pp == end_row && d < pr + 1) d++;
       out.err = e;
       out.a_len = end_row;
       out.t_len = end_row + d;
@@ -1064,7 +1120,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
-  ped_traceback_codes<L16, LW>(rows, tb_e, tb_d, tb_last, dst, lane, last, nd);
+  ped_traceback_codes<L16, LW>(rows, rowb, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
 #ifdef OVL_PROFILE
@@ -1144,9 +1200,9 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     PedOut po;
     PROF_T(pc0);
     if constexpr (FAST)
-      po = wave_ped_reg<1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
+      po = wave_ped_reg<OVL_ONE_DIR ? 0 : 1, SS, L16, RJ>(X, 1, X.e_cap, X.partial, X.min_branch_end_dist,
                                         X.branch_match_value, X.min_branch_tail_slope, A.w, a0,
-                                        am, B.w, b0, bn, error_limit, WM.rows, WM.rmlim, stk,
+                                        am, B.w, b0, bn, error_limit, WM.rows, WM.rowdir, WM.rmlim, stk,
                                         lane);
     else
       po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
@@ -1191,9 +1247,9 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     PedOut po;
     PROF_T(pc2);
     if constexpr (FAST)
-      po = wave_ped_reg<-1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
+      po = wave_ped_reg<OVL_ONE_DIR ? 0 : -1, SS, L16, RJ>(X, -1, X.e_cap, X.partial, X.min_branch_end_dist,
                                          X.branch_match_value, X.min_branch_tail_slope, A.w,
-                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.rmlim, LD,
+                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.rowdir, WM.rmlim, LD,
                                          lane);
     else
       po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);
