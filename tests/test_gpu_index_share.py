@@ -64,7 +64,7 @@ def test_gpu_imported_index_searches_like_the_built_one(built, batch):
     finally:
         a.close()
         b.close()
-    assert got_a.shape[0] > 100
+    assert got_a.shape[0] > (10 if batch else 100)
     assert got_b.shape == got_a.shape and np.array_equal(got_b, got_a)
     for key in STAT_KEYS:
         assert st_b[key] == st_a[key], (key, st_b[key], st_a[key])

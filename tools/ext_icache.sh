@@ -3,6 +3,8 @@
 # summed over k_extend dispatches by tools/pmc_sum.py.
 #   pass 1 (fetch):  instruction fetches and the SQC instruction cache
 #   pass 2 (stall):  wait / active cycles beside the instruction mix
+#   pass 3 (vmem):   vector-memory write issue and its FIFO stalls, LDS / VALU / SALU busy
+#   pass 4 (tc):     texture-address busy and stalls, L2 -> fabric write requests
 # usage: bash tools/ext_icache.sh TAG [reads]   (CANU_OVL_LIB may name a variant library)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -21,4 +23,8 @@ pass() {   # name counters...
 pass fetch SQ_IFETCH SQ_IFETCH_LEVEL SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES \
   SQC_ICACHE_MISSES_DUPLICATE SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
 pass stall SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH \
-  SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
+  SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES && \
+pass vmem SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_WR SQ_VMEM_WR_TA_DATA_FIFO_FULL \
+  SQ_VMEM_TA_ADDR_FIFO_FULL SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS && \
+pass tc TA_BUSY_avr TA_DATA_STALLED_BY_TC_CYCLES_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
+  GRBM_GUI_ACTIVE
