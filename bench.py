@@ -363,32 +363,51 @@ class Configs2:
                         "the driver's 8-GPU run measures the real curve"}
 
     def index_allgather_timing(self, torch):
-        """What the north star's 'all-gather the shared k-mer index at setup' would cost on
-        this node: an RCCL all_gather of a 1/N slice per rank of a buffer the size of the
-        full index (keys, positions, table) -- timed here, beside the index build each rank
-        does instead (Multi-GPU)."""
+        """The north star's shared index, measured on this node: rank 0 builds the index over
+        every read (1..n), and its buffers (ovl_export_index) go to the other ranks over RCCL
+        (broadcast), which import them (ovl_import_index; dist.share_index) -- timed beside
+        the index build each rank does instead over its shard's reads lo..n.  Then every rank
+        searches its shard with the shared index: the records must equal its own step's."""
+        from canu_amd import digest
+        from canu_amd.dist import share_index
         st = self.oic.stats()
-        # the full index of 50k x 10 kb: 8 B positions + 8 B keys per window + the 16 GiB
-        # table (DESIGN.md data layout) -- scaled by this run's bases
-        windows = self.total_bases
-        nbytes = int(16 * windows + (16 << 30) * self.total_bases / 500e6)
-        per = (nbytes // self.world) & ~255
-        src = torch.empty(per, dtype=torch.uint8, device=self.dev)
-        dst = torch.empty(per * self.world, dtype=torch.uint8, device=self.dev)
-        self.dist.all_gather_into_tensor(dst, src)           # warm the communicator
+        own_mh = digest.multiset_hash(self.oic.fetch())
+        from canu_amd.dist import _agree
         torch.cuda.synchronize()
         self.dist.barrier()
         t0 = time.perf_counter()
-        self.dist.all_gather_into_tensor(dst, src)
+        ok = True
+        if self.rank == 0:
+            try:
+                self.oic.build_hash_index(1, self.n)
+            except Exception:                # noqa: BLE001 -- every rank raises below
+                ok = False
+        if not _agree(ok, self.dist, self.dev):
+            raise RuntimeError("shared index: rank 0's build failed")
         torch.cuda.synchronize()
-        ms = 1000.0 * (time.perf_counter() - t0)
-        del src, dst
-        ms_t = torch.tensor([ms], dtype=torch.float64, device=self.dev)
-        self.dist.all_reduce(ms_t, op=self.dist.ReduceOp.MAX)
-        return {"index_bytes": nbytes, "allgather_ms": round(float(ms_t.item()), 2),
+        t1 = time.perf_counter()
+        nbytes = share_index(self.oic, [] if self.rank == 0 else [self.oic], self.dist,
+                             self.dev)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        same = False
+        try:
+            self.oic.find_overlaps(self.q_lo, self.q_hi)
+            same = digest.multiset_hash(self.oic.fetch()) == own_mh
+        except Exception:                    # noqa: BLE001 -- reported as a mismatch
+            same = False
+        t = torch.tensor([1000.0 * (t1 - t0), 1000.0 * (t2 - t1), 0.0 if same else 1.0],
+                         dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        build_ms, share_ms, bad = (float(x) for x in t.tolist())
+        return {"index_bytes": nbytes, "rank0_full_build_ms": round(build_ms, 2),
+                "broadcast_import_ms": round(share_ms, 2),
+                "shared_index_ms": round(build_ms + share_ms, 2),
                 "rank_index_build_ms": round(st["ms_index"], 2),
-                "note": "RCCL all_gather of an index-sized buffer (each rank 1/N of it) vs "
-                        "the index build each rank runs over its shard's reads lo..n"}
+                "records_equal_own_index": bad == 0.0,
+                "note": "shared: rank 0 builds the whole index, RCCL broadcast of its buffers, "
+                        "import on every rank (max over ranks); own: each rank's build over its "
+                        "shard's reads lo..n (this rank's last step)"}
 
 
 class Configs4Rank(Configs2):

@@ -13,9 +13,9 @@ from __future__ import annotations
 import numpy as np
 
 
-# The cost model of one rank's job, from the 1-GPU step on 50k x 10 kb (1 MI355X): index
-# 37 ms over every hashed read, probe 37 ms and chain 87 ms over every query, extension
-# 1,146 ms over the n^2/2 (a, b > a) pairs.  A query shard [lo, hi] only ever pairs with reads
+# The cost model of one rank's job, from the 1-GPU step on 50k x 10 kb (1 MI355X; the
+# driver's round-4 run, BENCH_r04: index 29 ms over every hashed read, probe 29 ms and chain
+# 62 ms over every query, extension 1,063 ms over the n^2/2 (a, b > a) pairs).  A query shard [lo, hi] only ever pairs with reads
 # b > a >= lo (Find_Overlaps.C:328 keeps targets with a larger ID), so its rank indexes
 # reads lo..n only: the same records and counters, a smaller index, and occurrence lists
 # (chain work) shortened by (n - lo) / n.
@@ -24,8 +24,8 @@ import numpy as np
 # (Find_Overlaps.C:158-200), so a shard indexing lo..n reproduces the reference's
 # `-h lo-n -r lo-hi` job exactly, not `-h 1-n`: once a limit is reached, other overlaps may
 # be kept.  canu never passes -l to overlapInCore; bench.py does not use it.
-SHARD_COSTS = {"index_per_read": 37.0 / 50_000, "probe_per_query": 37.0 / 50_000,
-               "chain_per_query": 87.0 / 50_000, "pair": 1146.0 / (50_000 ** 2 / 2)}
+SHARD_COSTS = {"index_per_read": 29.0 / 50_000, "probe_per_query": 29.0 / 50_000,
+               "chain_per_query": 62.0 / 50_000, "pair": 1063.0 / (50_000 ** 2 / 2)}
 
 
 def shard_cost(n: int, lo: int, hi: int, costs: dict | None = None) -> float:
@@ -203,3 +203,96 @@ def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
         jobs.append({"h": (lo, hi), "r": (1, hi), "est_s": round(cost(lo, hi), 2)})
         lo = hi + 1
     return jobs
+
+
+# ---- one index shared by the ranks (the north star's "all-gather the index over xGMI") ----
+_INDEX_PARTS = ("table", "occ", "bloom", "read_flags")
+_INDEX_META = ("bgn_iid", "end_iid", "first_iid", "nreads", "kmer_len", "tab_bits",
+               "slice_bits", "bloom_w", "hash_lib_lo", "hash_lib_hi", "records")
+
+
+def _hip():
+    """The process's HIP runtime (already loaded by torch / libcanu_ovl)."""
+    import ctypes
+    for name in ("libamdhip64.so.7", "libamdhip64.so.6", "libamdhip64.so"):
+        try:
+            lib = ctypes.CDLL(name)
+            lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_int]
+            return lib
+        except OSError:
+            continue
+    raise OSError("libamdhip64 not found")
+
+
+def _agree(ok: bool, dist, dev) -> bool:
+    """All ranks' ok flags combined (min), so that a failure on one rank is raised on every
+    rank instead of leaving the others waiting in the next collective."""
+    if not dist:
+        return ok
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def share_index(src, dsts, dist, dev, src_rank: int = 0):
+    """Give every rank the index the context `src` built on rank `src_rank`: its buffers
+    (ovl_export_index) are copied into torch tensors, broadcast over the process group
+    (RCCL over xGMI on the GPUs; dist None: one process, no collective) and imported
+    (ovl_import_index) into each context of `dsts` (this rank's contexts holding the same
+    reads).  A failure on any rank is raised on all of them.  Returns the bytes moved per
+    rank."""
+    import torch
+    from canu_amd.overlap_in_core import _IndexDesc
+    rank = dist.get_rank() if dist else src_rank
+    meta = torch.zeros(len(_INDEX_META) + len(_INDEX_PARTS), dtype=torch.int64, device=dev)
+    desc, err = None, None
+    if rank == src_rank:
+        try:
+            desc = src.export_index()
+            vals = [getattr(desc, f) for f in _INDEX_META] + \
+                   [getattr(desc, p + "_bytes") for p in _INDEX_PARTS]
+            meta.copy_(torch.tensor(vals, dtype=torch.int64))
+        except Exception as e:            # noqa: BLE001 -- re-raised below on every rank
+            err = e
+    if not _agree(err is None, dist, dev):
+        raise RuntimeError(f"share_index: export failed on rank {src_rank}: {err}")
+    if dist:
+        dist.broadcast(meta, src_rank)
+    m = [int(x) for x in meta.tolist()]
+    sizes = dict(zip(_INDEX_PARTS, m[len(_INDEX_META):]))
+    bufs = {p: torch.empty(max(n, 1), dtype=torch.uint8, device=dev) for p, n in sizes.items()}
+    if rank == src_rank:
+        try:
+            hip = _hip()
+            for p in _INDEX_PARTS:
+                if sizes[p]:
+                    rc = hip.hipMemcpy(bufs[p].data_ptr(), getattr(desc, p), sizes[p], 4)
+                    if rc != 0:
+                        raise RuntimeError(f"hipMemcpy of the index {p}: error {rc}")
+            torch.cuda.synchronize(dev)
+        except Exception as e:            # noqa: BLE001
+            err = e
+    if not _agree(err is None, dist, dev):
+        raise RuntimeError(f"share_index: copy failed on rank {src_rank}: {err}")
+    if dist:
+        for p in _INDEX_PARTS:
+            if sizes[p]:
+                dist.broadcast(bufs[p], src_rank)
+    d = _IndexDesc()
+    for f, v in zip(_INDEX_META, m):
+        setattr(d, f, v)
+    for p in _INDEX_PARTS:
+        setattr(d, p, bufs[p].data_ptr() if sizes[p] else None)
+        setattr(d, p + "_bytes", sizes[p])
+    try:
+        for ctx in dsts:
+            ctx.import_index(d)
+    except Exception as e:                # noqa: BLE001
+        err = e
+    torch.cuda.synchronize(dev)
+    del bufs
+    if not _agree(err is None, dist, dev):
+        raise RuntimeError(f"share_index: import failed on rank {rank}: {err}")
+    return sum(sizes.values())

@@ -92,3 +92,34 @@ def test_gpu_import_rejects_another_read_store(built):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_share_index_through_torch_buffers(built):
+    """dist.share_index, the path bench.py --gpus N takes over RCCL: the exported buffers are
+    copied into torch tensors (what a broadcast would fill on every rank) and imported from
+    there; without a process group it runs on one GPU.  Same records and counters."""
+    import torch
+    from canu_amd.dist import share_index
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    rs = synth_reads(n_reads=200, read_len=3000, genome_len=50_000, error_rate=0.03, seed=43)
+    O = OicParameters(Kmer_Len=22, maxErate=0.06, Min_Olap_Len=500).finalize()
+    a = OverlapInCore(O, device=0)
+    b = OverlapInCore(O, device=0)
+    try:
+        a.load_reads(rs)
+        a.build_hash_index(41, rs.nreads)
+        b.load_reads(rs)
+        moved = share_index(a, [b], None, torch.device("cuda", 0))
+        assert moved > 0
+        got_b = b.fetch(b.find_overlaps(41, 120))
+        st_b = b.stats()
+        got_a = a.fetch(a.find_overlaps(41, 120))
+        st_a = a.stats()
+    finally:
+        a.close()
+        b.close()
+    assert got_a.shape[0] > 100
+    assert np.array_equal(got_b, got_a)
+    for key in STAT_KEYS:
+        assert st_b[key] == st_a[key], key
