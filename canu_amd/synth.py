@@ -173,8 +173,14 @@ def synth_reads_parallel(n_reads: int, read_len: int, genome_len: int, error_rat
     """synth_reads over [lo, hi) in `workers` forked processes (read i depends only on
     (seed, i), so the slices concatenate to exactly what one synth_reads call returns)."""
     import multiprocessing as mp
+    import sys
     lo, hi = read_range if read_range else (0, n_reads)
     genome = random_genome(np.random.default_rng(seed), genome_len)
+    # no worker pool is forked from a process that has initialised the GPU (its children
+    # would inherit the device state); such a caller generates serially
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        workers = 1
     if workers <= 1 or hi - lo < 1024:
         return synth_reads(n_reads, read_len, genome_len, error_rate, seed=seed,
                            len_jitter=len_jitter, genome=genome, read_range=(lo, hi))

@@ -7,6 +7,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
+# torch first: it and libcanu_ovl.so both need libamdhip64.so.7, and the process keeps the
+# first one loaded.  bench.py and smoke() load torch's before the library; so do the tests
+# (with the library's /opt/rocm runtime loaded first, torch's HIP init fails)
+import torch  # noqa: E402,F401
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 device (runs on the GPU box)")

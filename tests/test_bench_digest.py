@@ -58,8 +58,9 @@ def test_gpu_bench_job_matches_reference_digest(built):
     from canu_amd.overlap_in_core import OicParameters, OverlapInCore
     import torch
     g = json.load(open(GOLDEN))
-    job = Configs2(parse_args([]), 0, 1, None, torch.device("cuda", 0))
+    job = Configs2(parse_args([]), 0, 1, torch.device("cuda", 0))
     assert job.workload_key()["reads"] == g["workload"]["reads"]
+    job.generate()
     job.setup(OicParameters, OverlapInCore)
     try:
         n = job.step()
