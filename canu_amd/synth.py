@@ -179,7 +179,9 @@ def synth_reads_parallel(n_reads: int, read_len: int, genome_len: int, error_rat
     # no worker pool is forked from a process that has initialised the GPU (its children
     # would inherit the device state); such a caller generates serially
     torch = sys.modules.get("torch")
-    if torch is not None and torch.cuda.is_initialized():
+    oic = sys.modules.get("canu_amd.overlap_in_core")
+    if (torch is not None and torch.cuda.is_initialized()) or \
+            (oic is not None and getattr(oic, "_lib", None) is not None):
         workers = 1
     if workers <= 1 or hi - lo < 1024:
         return synth_reads(n_reads, read_len, genome_len, error_rate, seed=seed,
