@@ -451,12 +451,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #define OVL_RJ 8
 #endif
 #define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
-// OVL_LOG_REL: row e's cells are logged relative to its window base B_e (cell 64j + lane
-// for chunk j, so every chunk store is one aligned 128-B line) and B_e goes to a per-row
-// array the traceback reads; 0: cell = d mod LW (chunk stores straddle lines)
-#ifndef OVL_LOG_REL
-#define OVL_LOG_REL 0
-#endif
 // Cost attribution (A/B builds only): each knob runs one phase of the extension twice, its
 // results identical, so the time added is that phase's cost (tools/ext_evidence.sh)
 #ifndef OVL_X2_ARGMAX
@@ -594,9 +588,8 @@ typedef __attribute__((address_space(1))) const uint64_t g_cu64;
 #define OVL_TB_G 1
 #endif
 template <bool L16, int LW = OVL_LOGW>
-__device__ __forceinline__ void ped_traceback_codes(int32_t *log, const int32_t *rowb,
-                                                    int32_t tb_e, int32_t tb_d, int32_t last,
-                                                    int32_t *dst, uint32_t lane,
+__device__ __forceinline__ void ped_traceback_codes(int32_t *log, int32_t tb_e, int32_t tb_d,
+                                                    int32_t last, int32_t *dst, uint32_t lane,
                                                     int32_t &last_out, int32_t &nd_out) {
   constexpr int W = LW;                        // cells per logged row, cell = d mod W
   // rows per window (lanes cover dc-31..dc+31): 16 keeps the unrolled walk and its code
@@ -617,21 +610,11 @@ __device__ __forceinline__ void ped_traceback_codes(int32_t *log, const int32_t 
     const int32_t dc = d;
     const int32_t cell = (dc - 31 + (int32_t)(lane < 63 ? lane : 62)) & (W - 1);
     int32_t V[G * TBR];
-#if OVL_LOG_REL
-    // the rows' window bases: lane i holds B of row kh-1-i
-    typedef __attribute__((address_space(1))) const int32_t g_cb;
-    const int32_t bl = (lane < G * TBR && (int32_t)lane < kh) ? ((g_cb *)rowb)[kh - 1 - (int32_t)lane] : 0;
-#endif
 #pragma unroll
     for (int i = 0; i < G * TBR; i++) {
       const int32_t kk = kh - 1 - i < 0 ? 0 : kh - 1 - i;   // row k-1 for k = kh - i
-#if OVL_LOG_REL
-      const int32_t ci = (cell - __builtin_amdgcn_readlane(bl, i)) & (W - 1);
-#else
-      const int32_t ci = cell;
-#endif
-      if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + ci];
-      else               V[i] = rows[(size_t)kk * W + ci];
+      if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
+      else               V[i] = rows[(size_t)kk * W + cell];
     }
 #pragma unroll 1
     for (int g = 0; g < G; g++) {
@@ -714,17 +697,11 @@ __device__ __forceinline__ double uni(double v) {
 // kernel's scratch made every call start with flat loads from scratch and a full vmcnt(0)
 // wait (which also waited for the caller's spill stores and the row-0 log store).  X is
 // only read by the OVL_PROFILE build.
-// DIR = 0: one function for both directions, the direction a runtime argument (rdir = +1 or
-// -1): half the row-loop code in the instruction cache, for a few more VALU per chunk
-// (OVL_ONE_DIR A/B)
-#ifndef OVL_ONE_DIR
-#define OVL_ONE_DIR 0
-#endif
 template <int DIR, typename SS, bool L16, int RJ = OVL_RJ>
 __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
-    const ExtendArgs &X, int32_t rdir, int32_t e_cap, int32_t partial_i, int32_t mbed, double bmv_in,
+    const ExtendArgs &X, int32_t e_cap, int32_t partial_i, int32_t mbed, double bmv_in,
     double mbts, const lds_u64 *aw, int32_t a0, int32_t m, const lds_u64 *tw, int32_t t0,
-    int32_t n, int32_t limit, int32_t *rows, int32_t *rowb, ml_t *mlim, int32_t *dst,
+    int32_t n, int32_t limit, int32_t *rows, ml_t *mlim, int32_t *dst,
     uint32_t lane) {
   SS A, T;
   A.w = aw; A.len = 0;
@@ -737,15 +714,9 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   static_assert(64 * J <= (1 << WB) && 64 * J <= LW, "key and log layout hold the window");
   static_assert(!SS::kExc, "the register kernel runs on exception-free LDS strands");
   limit = uni(limit);
-  // the direction: compile-time (DIR = +-1) or a wave-uniform runtime value (DIR = 0)
-  const bool fwd = DIR != 0 ? DIR > 0 : uni(rdir) > 0;
   auto slide_d = [&](int32_t r, int32_t d, int32_t lim) -> int32_t {
-    if constexpr (DIR != 0) return slide_any<DIR>(A, a0, T, t0, r, d, lim);
-    else return fwd ? slide_any<1>(A, a0, T, t0, r, d, lim) : slide_any<-1>(A, a0, T, t0, r, d, lim);
+    return slide_any<DIR>(A, a0, T, t0, r, d, lim);
   };
-  // pa = sa + (+-q), pt = st + (+-(q + d)): (x ^ ms) - ms negates when ms = -1
-  const int32_t ms = fwd ? 0 : -1;
-  const int32_t sa = fwd ? a0 + 1 : a0 - 32, st = fwd ? t0 + 1 : t0 - 32;
   const int32_t NONE = 0x7fffffff, NEG = (int32_t)0x80000000;
   PedOut out;
   out.leftover = 0;
@@ -802,15 +773,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   // of the next row would wait for the log stores too
   typedef __attribute__((address_space(1))) cell_t g_cell_t;
   g_cell_t *clog = uni_ptr((g_cell_t *)rows);     // scalar base: stores use saddr + offset
-#if OVL_LOG_REL
-  clog[lane] = (cell_t)R[0];                   // row 0: window base B = -3
-  typedef __attribute__((address_space(1))) int32_t g_rb_t;
-  g_rb_t *grb = uni_ptr((g_rb_t *)rowb);
-  if (lane == 0) grb[0] = B;
-#else
-  (void)rowb;
   clog[(B + (int32_t)lane) & (LW - 1)] = (cell_t)R[0];
-#endif
   typedef __attribute__((address_space(1))) uint8_t g_u8;
   g_u8 *clogb = (g_u8 *)clog;
   // chunks 0..JU-1 are processed unconditionally (straight-line code the compiler can
@@ -858,14 +821,8 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       const int32_t lmin = l1 < l2 ? l1 : l2;
       const int32_t lim = q >= -1 ? lmin : -(1 << 30);
 
-      int32_t pa, pt;
-      if constexpr (DIR != 0) {
-        pa = (DIR > 0) ? (a0 + 1) + q : (a0 - 32) - q;
-        pt = (DIR > 0) ? (t0 + 1) + q + d : (t0 - 32) - q - d;
-      } else {
-        pa = ((q ^ ms) - ms) + sa;
-        pt = (((q + d) ^ ms) - ms) + st;
-      }
+      const int32_t pa = (DIR > 0) ? (a0 + 1) + q : (a0 - 32) - q;
+      const int32_t pt = (DIR > 0) ? (t0 + 1) + q + d : (t0 - 32) - q - d;
       const int32_t ia = pa >> 5, it = pt >> 5;
       const uint64_t wa0 = A.w[ia], wa1 = A.w[ia + 1];
       const uint64_t wt0 = T.w[it], wt1 = T.w[it + 1];
@@ -879,11 +836,8 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       const uint32_t mm = (xa0 ^ xt0) | (xa1 ^ xt1);
       // the first step examines 31 bases (a sentinel mismatch in the 32nd: no clamp of
       // the bit scan), lanes that matched all 31 with more left continue below
-      int32_t run;
-      if constexpr (DIR != 0)
-        run = (DIR > 0) ? (int32_t)__builtin_ctz(mm | 0x80000000u) : (int32_t)__builtin_clz(mm | 1u);
-      else   // reverse: the 32 bases run downwards, bit 31 first
-        run = (int32_t)__builtin_ctz((fwd ? mm : __builtin_bitreverse32(mm)) | 0x80000000u);
+      const int32_t run = (DIR > 0) ? (int32_t)__builtin_ctz(mm | 0x80000000u)
+                                    : (int32_t)__builtin_clz(mm | 1u);
       // k = min(run, lim): lim >= 0 (run >= 0), so the row only moves forward
       const int32_t k = run < lim ? run : lim;
       NR[j] = q + 1 + k;                       // lim >= 0 inside the band
@@ -1021,21 +975,13 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
         R[j] = v;
         const int32_t key = (int32_t)(((uint32_t)v << WB) | (uint32_t)(lkey - 64 * j));
         kmx = key > kmx ? key : kmx;
-#if OVL_LOG_REL
-        *(g_cell_t *)(clogb + (erow | ((uint32_t)(64 * j) + lane) * (uint32_t)sizeof(cell_t))) =
-            (cell_t)v;
-#else
         *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
             (cell_t)v;
 #if OVL_X2_LOG
         *(volatile g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
             (cell_t)v;
 #endif
-#endif
       }
-#if OVL_LOG_REL
-      if (lane == 0) grb[e] = B;                 // the row's window base, for the traceback
-#endif
       const int32_t K = wave_max(kmx);
       const int32_t M = K >> WB;
       if (M > longest) {                         // Longest, Best_d, Best_e of this row
@@ -1122,7 +1068,7 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
     } else {
       int32_t d = end_d;
       // forward.C:212 -- force the last error to be a mismatch rather than an insertion
-      if (fwd && end_row == m && 1 + end_pp == end_row && d < pr + 1) d++;
+      if (DIR > 0 && end_row == m && 1 + end_pp == end_row && d < pr + 1) d++;
       out.err = e;
       out.a_len = end_row;
       out.t_len = end_row + d;
@@ -1142,10 +1088,10 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
 #if OVL_X2_TB
-  ped_traceback_codes<L16, LW>(rows, rowb, tb_e, tb_d, tb_last, dst, lane, last, nd);
+  ped_traceback_codes<L16, LW>(rows, tb_e, tb_d, tb_last, dst, lane, last, nd);
   asm volatile("" ::: "memory");
 #endif
-  ped_traceback_codes<L16, LW>(rows, rowb, tb_e, tb_d, tb_last, dst, lane, last, nd);
+  ped_traceback_codes<L16, LW>(rows, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
 #ifdef OVL_PROFILE
@@ -1227,9 +1173,9 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     if constexpr (FAST) {
       for (int rep = 0; rep < (OVL_X2_FWD ? 2 : 1); rep++) {
         if (OVL_X2_FWD) asm volatile("" ::: "memory");
-        po = wave_ped_reg<OVL_ONE_DIR ? 0 : 1, SS, L16, RJ>(X, 1, X.e_cap, X.partial, X.min_branch_end_dist,
+        po = wave_ped_reg<1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
                                           X.branch_match_value, X.min_branch_tail_slope, A.w, a0,
-                                          am, B.w, b0, bn, error_limit, WM.rows, WM.rowdir, WM.rmlim, stk,
+                                          am, B.w, b0, bn, error_limit, WM.rows, WM.rmlim, stk,
                                           lane);
       }
     }
@@ -1276,9 +1222,9 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     PedOut po;
     PROF_T(pc2);
     if constexpr (FAST)
-      po = wave_ped_reg<OVL_ONE_DIR ? 0 : -1, SS, L16, RJ>(X, -1, X.e_cap, X.partial, X.min_branch_end_dist,
+      po = wave_ped_reg<-1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
                                          X.branch_match_value, X.min_branch_tail_slope, A.w,
-                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.rowdir, WM.rmlim, LD,
+                                         a0, a0 + 1, B.w, b0, b0 + 1, lim, WM.rows, WM.rmlim, LD,
                                          lane);
     else
       po = wave_ped<-1, SS, L16>(X, A, a0, a0 + 1, B, b0, b0 + 1, lim, WM, LD, lane);

@@ -5,6 +5,8 @@
 #   pass 2 (stall):  wait / active cycles beside the instruction mix
 #   pass 3 (vmem):   vector-memory write issue and its FIFO stalls, LDS / VALU / SALU busy
 #   pass 4 (tc):     texture-address busy and stalls, L2 -> fabric write requests
+#   pass 5 (lat):    LDS / vector-memory / scalar-memory instructions and their outstanding
+#                    levels (level / count = average latency in the counters' cycle unit)
 # usage: bash tools/ext_icache.sh TAG [reads]   (CANU_OVL_LIB may name a variant library)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -27,4 +29,6 @@ pass stall SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INST
 pass vmem SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_WR SQ_VMEM_WR_TA_DATA_FIFO_FULL \
   SQ_VMEM_TA_ADDR_FIFO_FULL SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS && \
 pass tc TA_BUSY_avr TA_DATA_STALLED_BY_TC_CYCLES_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
-  GRBM_GUI_ACTIVE
+  GRBM_GUI_ACTIVE && \
+pass lat SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_WR \
+  SQ_INSTS_FLAT SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM
