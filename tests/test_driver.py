@@ -372,3 +372,46 @@ def test_gpu_sorted_query_windows_are_exact(built, monkeypatch, mode):
     assert got.shape == ref.shape and np.array_equal(got, ref)
     for rk, ok in STAT_KEYS:
         assert st[ok] == rst[rk], (rk, st[ok], rst[rk])
+
+
+def _ref_last(rs, rr, threads):
+    nr = rs.first_iid + rs.nreads - 1
+    gbr, ger = (max(rr[0], 1), min(rr[1], nr)) if rr else (1, nr)
+    per = 1 + (ger - gbr) // max(threads, 1) // 8
+    return gbr, (ger - 1 if (ger - gbr) % per == 0 else ger)
+
+
+@pytest.mark.parametrize("case", sorted(CASES) + ["screened_ends"])
+@pytest.mark.parametrize("group", [2, 0])
+def test_oracle_super_batches_equal_batches(case, group):
+    """The driver's super-batches (ovl_overlap_driver): searching the UNION of consecutive
+    hash batches gives the records and every counter that searching them one by one gives --
+    a query meets, in any batch, exactly the hashed reads with larger IDs (Find_Overlaps.C:328)
+    and a pair's seeds, chain and screened ends depend on the pair alone.  Checked on the
+    oracle (pinned to the reference): batches joined two by two (group=2) and all into one
+    (group=0), against the batch-by-batch OverlapDriver restatement."""
+    if case == "screened_ends":
+        rs = synth_reads(n_reads=240, read_len=3000, genome_len=60_000, error_rate=0.035,
+                         seed=27, len_jitter=0.3)
+        batch, threads, rr, skip = dict(hashstrings=50), 4, None, _end_skip_kmers(rs)
+    else:
+        kw, batch, threads, rr = CASES[case]
+        rs = synth_reads(**kw)
+        skip = None
+    P = _params()
+    want, wst, batches = oracle.run_oracle_driver(
+        rs, P, ref_range=rr or (1, oracle.UINT32_MAX), threads=threads, with_stats=True,
+        skip_kmers=skip, **_driver_kw(batch))
+    assert len(batches) >= 3
+    gbr, ref_last = _ref_last(rs, rr, threads)
+    groups = [batches] if group == 0 else [batches[i:i + group] for i in range(0, len(batches), group)]
+    recs, tot = [], None
+    for g in groups:
+        rec, st = oracle.run_oracle(rs, P, hash_range=(g[0][0], g[-1][1]), ref_range=(gbr, ref_last),
+                                    skip_kmers=skip, with_stats=True)
+        recs.append(rec)
+        tot = st if tot is None else {f: tot[f] + st[f] for f in st}
+    got = oracle.sort_records(np.concatenate(recs))
+    assert got.shape == want.shape and np.array_equal(got, want)
+    for _, f in STAT_KEYS:
+        assert tot[f] == wst[f], (f, tot[f], wst[f])
