@@ -942,7 +942,11 @@ static int apply_hash_libs(ovl_ctx *c, uint32_t lo, uint32_t hi) {
 // The index over hash reads bgn..end (clipped to the loaded reads by the callers).
 // bloom: also build the batch's Bloom filter (OverlapDriver batches, whose searches are
 // mostly by reads outside the hash range; see use_bloom)
-static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = false) {
+// table = false: the records grouped into k-mer runs only (what the driver's first-read
+// histogram reads to find a load cut), no table, filter or screened-end flags: the index is
+// not searchable (have_index stays false)
+static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = false,
+                       bool table = true) {
   hipStream_t s = c->stream;
   uint32_t k = c->P.kmer_len;
   c->hash_bgn_iid = bgn;
@@ -1072,6 +1076,15 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = fals
                        big.p, sM.p, sP.p, n2, misc.p + 2);
     HIPC(hipMemcpyAsync(hm, misc.p, 16, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+  }
+  if (!table) {
+    HIPC(hipEventRecord(c->ev[1], s));
+    HIPC(hipStreamSynchronize(s));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+    c->stats.ms_index += ms;
+    c->index_records = hm[0];
+    return OVL_OK;
   }
   uint32_t maxd = std::max<uint32_t>(hm[2], 1);
 #ifndef OVL_SLICE_Q
@@ -1268,8 +1281,10 @@ static uint64_t index_window_cap(ovl_ctx *c) {
 // third needs the batch's k-mers, so the index is built over the first two's range and its
 // first-occurrence histogram decides -- rebuilding the shorter batch when the table load
 // stops it earlier.
+// boundaries_only: the batch's end alone (the driver's first phase, super-batches): no
+// build unless the table load may cut the batch, and then no table and no cut index
 static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_hash_limits *L,
-                            uint32_t *last_iid) {
+                            uint32_t *last_iid, bool boundaries_only = false) {
   int rc = clip_hash_range(c, bgn, end);
   if (rc) return rc;
   if (!L) return fail(OVL_ERR_BAD_PARAM, "null limits");
@@ -1316,6 +1331,10 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
   const uint64_t entry_limit =
       (uint64_t)(L->max_hash_load * (double)(1ull << L->hash_mask_bits) * (double)ENTRIES_PER_BUCKET);
   const bool load_may_cut = windows >= entry_limit && e > bgn;
+  if (boundaries_only && !load_may_cut) {
+    *last_iid = e;
+    return OVL_OK;
+  }
   // When the load may cut the batch, the first build covers only a prefix of about twice
   // the limit's windows (a read's new k-mers are at most its windows, so the cut lies past
   // the limit's windows; typical reads bring 0.3-0.7 new k-mers per window).  A prefix the
@@ -1353,11 +1372,11 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
         eb = id;
       }
     }
-    const bool bloom = !c->sq.on || sq_bloom();
-    if ((rc = build_index(c, bgn, eb, bloom)) == OVL_ERR_OOM) {
+    const bool bloom = !boundaries_only && (!c->sq.on || sq_bloom());
+    if ((rc = build_index(c, bgn, eb, bloom, !boundaries_only)) == OVL_ERR_OOM) {
       // the previous batch's search buffers make room (the next search grows them again)
       release_find_buffers(c);
-      rc = build_index(c, bgn, eb, bloom);
+      rc = build_index(c, bgn, eb, bloom, !boundaries_only);
     }
     if (rc) return rc;
     if (!load_may_cut) break;
@@ -1385,7 +1404,7 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
       if (entries >= entry_limit) { el = bgn + i; reached = true; break; }
     }
     if (reached) {
-      if (el < eb) {
+      if (el < eb && !boundaries_only) {
         // the prefix's index cut down to the batch (k_cut_index), or built again over it
         static const bool cut = !getenv("OVL_CUT_FILTER") || atoi(getenv("OVL_CUT_FILTER")) != 0;
         if (cut) {
@@ -2851,6 +2870,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   c->nout = 0;
   c->acc.nu = c->acc.nn = c->acc.np = 0;
   c->cut_windows_hint = 0;
+  c->have_index = false;                    // a job builds its own indexes (none is reused)
   uint32_t bgn = g_bgn_hash;
   uint32_t end = g_bgn_hash + L.max_hash_strings - 1;                    // inclusive
   uint64_t batches = 0;
@@ -2934,7 +2954,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     while (bgn < g_end_hash) {                                           // :222
       if (end > g_end_hash) end = g_end_hash;
       uint32_t loaded = 0;
-      int rc = build_batch_impl(c, bgn, end, &L, &loaded);
+      int rc = build_batch_impl(c, bgn, end, &L, &loaded, true);
       if (rc) return rc;
       end = loaded;
       batches++;

@@ -468,6 +468,12 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #ifndef OVL_X2_LOG
 #define OVL_X2_LOG 0             // every row-log store
 #endif
+#ifndef OVL_X2_CONV
+#define OVL_X2_CONV 0            // Set_Right_Delta's stack -> Right_Delta pass (and its syncs)
+#endif
+#ifndef OVL_X2_STAGE
+#define OVL_X2_STAGE 0           // staging both strands of a pair into LDS
+#endif
 static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 
 #ifdef OVL_PROFILE
@@ -978,7 +984,8 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
         *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
             (cell_t)v;
 #if OVL_X2_LOG
-        *(volatile g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
+        asm volatile("" ::: "memory");           // keeps both stores (plain, no waits)
+        *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
             (cell_t)v;
 #endif
       }
@@ -1198,14 +1205,17 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
       if (lane == 0) stk[n] = po.leftover + 1;     // "last + 1"
       vm_sync();
       n++;
-      for (int32_t i = lane; i < n - 1; i += 64) {
-        int32_t src = n - 1 - i;
-        int32_t a = stk[src], b = stk[src - 1];
-        int32_t v = (a < 0 ? -a : a) * ((b > 0) - (b < 0));
-        RD[i] = s_first ? -v : v;
+      for (int rep = 0; rep < (OVL_X2_CONV ? 2 : 1); rep++) {
+        if (OVL_X2_CONV) asm volatile("" ::: "memory");
+        for (int32_t i = lane; i < n - 1; i += 64) {
+          int32_t src = n - 1 - i;
+          int32_t a = stk[src], b = stk[src - 1];
+          int32_t v = (a < 0 ? -a : a) * ((b > 0) - (b < 0));
+          RD[i] = s_first ? -v : v;
+        }
+        vm_sync();
       }
       rd_len = n - 1;
-      vm_sync();
     }
   }
   S_Hi += S_Right_Begin - 1;
@@ -1937,9 +1947,13 @@ k_extend(ExtendArgs X) {
     if constexpr (STAGE) {
       bool ok = false;
       if (!(S.ex_wild || S.ex_nul || T.ex_wild) && S.len <= X.stage_len && T.len <= X.stage_len) {
-        StrandLP SL = stage_strand(S, sw, lane);
-        StrandLP TL = stage_strand(T, tw, lane);
-        lds_sync();
+        StrandLP SL, TL;
+        for (int rep = 0; rep < (OVL_X2_STAGE ? 2 : 1); rep++) {
+          if (OVL_X2_STAGE) asm volatile("" ::: "memory");
+          SL = stage_strand(S, sw, lane);
+          TL = stage_strand(T, tw, lane);
+          lds_sync();
+        }
         PROF_T(pp0);
         ok = process_pair<true, L16, false, RJ>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
 #ifdef OVL_PROFILE
