@@ -229,6 +229,11 @@ struct ovl_ctx {
   std::vector<uint32_t> ext_classes;       // read-length cap of each staged launch
   uint32_t stats_ext_waves = 0, stats_gen_waves = 0;
   uint64_t index_records = 0;    // records of the current index (windows + skip markers)
+  // an OverlapDriver job's phase 3 (ovl_overlap_driver): the index buffers are allocated for
+  // the largest super-batch at once, and the search buffers keep the size the first search
+  // gave them -- a hipFree / hipMalloc of tens of GB on a nearly full device costs ~0.5 s
+  uint64_t index_reserve = 0;
+  bool sticky_budgets = false;
 
   // pending extension work (see find_impl): chains of several probe chunks -- and of the
   // driver's hash batches -- are appended here and extended together in one launch
@@ -978,7 +983,10 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = fals
   uint32_t fb = std::min<uint32_t>(11, ceil_log2((per_cb + 127) / 128));   // ~128 per fine bucket
   uint32_t ncb = 1u << cb, nfb = 1u << fb, nfine = ncb * nfb;
 
-  if (c->d_tmpR.alloc(P) || c->d_midR.alloc(P) || c->d_tmpM2.alloc(P) || c->d_occ.alloc(P))
+  auto rec_alloc = [&](uint64_t n) {
+    return c->d_tmpR.alloc(n) || c->d_midR.alloc(n) || c->d_tmpM2.alloc(n) || c->d_occ.alloc(n);
+  };
+  if (!(c->index_reserve > P && !rec_alloc(c->index_reserve)) && rec_alloc(P))
     return fail(OVL_ERR_OOM, "index records (%llu)", (unsigned long long)P);
   DBuf<uint32_t> &hist = c->b_hist, &cstart = c->b_cstart, &cursor = c->b_cursor,
                  &fstart = c->b_fstart, &fcnt = c->b_fcnt, &misc = c->b_misc, &big = c->b_big;
@@ -1737,6 +1745,10 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       const uint64_t held = (c->fb.pool.n + c->fb.pnodes[0].n + c->fb.pnodes[1].n) * sizeof(Node);
       HIT_BUDGET = std::min<uint64_t>(HIT_BUDGET, (uint64_t)((fr + held) * 0.6) / 33);
     }
+    // a driver job's later searches chain within the buffers its first one sized (more hit
+    // chunks per run instead of a regrow of the pool and its copy)
+    if (c->sticky_budgets && c->fb.pnodes[0].n > (16ull << 20))
+      HIT_BUDGET = std::min<uint64_t>(HIT_BUDGET, c->fb.pnodes[0].n - 1);
   }
   if (const char *e = getenv("OVL_HIT_BUDGET_M"))             // experiments: millions of hits
     HIT_BUDGET = std::max<uint64_t>(16, strtoull(e, nullptr, 10)) << 20;
@@ -2220,6 +2232,17 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     pending[slot] = true;
     return OVL_OK;
   };
+  // Extend everything the accumulator holds; it is empty again for the next chunk (the
+  // stream orders the next appends after this launch's reads).
+  auto flush_acc = [&]() -> int {
+    if (int rc = collect(0)) return rc;
+    auto &A = c->acc;
+    const uint32_t np = (uint32_t)A.np;
+    slot_pairs[0] = np;
+    int rc = launch_ext(0, A.units.p, A.pairs.p, A.pnodes.p, np, (uint32_t)A.nu);
+    A.nu = A.nn = A.np = 0;
+    return rc;
+  };
   // Append a chunk's units, list nodes and pairs to the accumulator (device copies on s,
   // which the extension also runs on without OVL_PIPELINE: nothing is overwritten early).
   const uint64_t ACC_PAIRS = 4ull << 20, ACC_NODES = 1ull << 30;
@@ -2228,7 +2251,13 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     auto &A = c->acc;
     if (A.nu + nu_c >= 0xFFFFFFF0ull || A.nn + nn_c >= 0xFFFFFFF0ull)
       return fail(OVL_ERR_UNSUPPORTED, "extension accumulator past 2^32 entries");
-    if (A.units.n < A.nu + nu_c || A.pnodes.n < A.nn + nn_c || A.pairs.n < A.np + np_c) {
+    auto acc_fits = [&]() {
+      return A.units.n >= A.nu + nu_c && A.pnodes.n >= A.nn + nn_c && A.pairs.n >= A.np + np_c;
+    };
+    // what the accumulator holds is extended first rather than moved into bigger buffers
+    if (!acc_fits() && A.np)
+      if (int rc = flush_acc()) return rc;
+    if (!acc_fits()) {
       // growing moves the buffers: the pending extension (which reads them) must be done,
       // and what the accumulator holds is carried over
       HIPC(hipStreamSynchronize(xs));
@@ -2261,17 +2290,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     A.nn += nn_c;
     A.np += np_c;
     return OVL_OK;
-  };
-  // Extend everything the accumulator holds; it is empty again for the next chunk (the
-  // stream orders the next appends after this launch's reads).
-  auto flush_acc = [&]() -> int {
-    if (int rc = collect(0)) return rc;
-    auto &A = c->acc;
-    const uint32_t np = (uint32_t)A.np;
-    slot_pairs[0] = np;
-    int rc = launch_ext(0, A.units.p, A.pairs.p, A.pnodes.p, np, (uint32_t)A.nu);
-    A.nu = A.nn = A.np = 0;
-    return rc;
   };
   const bool bloom = nu > 0 && use_bloom(c, bgn, end);
   uint64_t chunk = 0;
@@ -2989,6 +3007,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   if (const char *e = getenv("OVL_SB_WINDOWS")) sb_cap = std::min<uint64_t>(sb_cap, strtoull(e, nullptr, 10));
   sb_cap = std::max<uint64_t>(sb_cap, 1);
   std::vector<std::pair<uint32_t, uint32_t>> sbs;
+  uint64_t sb_max = 0;                                         // the largest one's windows
   {
     uint64_t w = 0;
     for (const auto &b : bat) {
@@ -3000,8 +3019,17 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
         sbs.push_back(b);
         w = bw;
       }
+      sb_max = std::max(sb_max, w);
     }
   }
+  // the index buffers for the largest super-batch from the first build on, and search buffers
+  // that keep their first size (ovl_ctx::index_reserve / sticky_budgets), for this job only
+  struct Reserve {
+    ovl_ctx *c;
+    ~Reserve() { c->index_reserve = 0; c->sticky_budgets = false; }
+  } reserve_guard{c};
+  c->index_reserve = sb_max + c->h_skip.size();
+  c->sticky_budgets = true;
   // phase 3: the searches.  The first super-batch is built, then the query chunks are planned
   // with its index resident (plan_query_chunks: what the sorted windows may take).
   auto build_sb = [&](size_t si) -> int {
@@ -3030,10 +3058,14 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
                      (sq_mode == 3 && searches_of(g_bgn_ref) >= SQ_AUTO_SEARCHES);
   if (sq_on) qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref);
   if (qchunks.empty()) qchunks.push_back({g_bgn_ref, ref_last});
-  std::vector<std::pair<size_t, size_t>> plan;               // (chunk, super-batch)
+  // (chunk, super-batch), the super-batches of every other chunk in reverse order: a chunk
+  // then starts with the index its predecessor ended on when both reach the last super-batch
+  std::vector<std::pair<size_t, size_t>> plan;
   for (size_t qi = 0; qi < qchunks.size(); qi++)
-    for (size_t si = 0; si < sbs.size(); si++)
+    for (size_t i = 0; i < sbs.size(); i++) {
+      const size_t si = (qi & 1) ? sbs.size() - 1 - i : i;
       if (qchunks[qi].first < sbs[si].second) plan.push_back({qi, si});
+    }
   if (getenv("OVL_TIMING"))
     fprintf(stderr, "OVL_TIMING super-batches: %llu batches (phase 1 %.1f ms) -> %zu super-batches "
             "of <= %llu windows, %zu query chunks over refs %u-%u, %zu searches, sorted windows %s\n",

@@ -451,29 +451,6 @@ __device__ __attribute__((noinline)) PedOut wave_ped(const ExtendArgs &X, const 
 #define OVL_RJ 8
 #endif
 #define OVL_LOGW 512             // cells per logged row (>= 64 * OVL_RJ, a power of two)
-// Cost attribution (A/B builds only): each knob runs one phase of the extension twice, its
-// results identical, so the time added is that phase's cost (tools/ext_evidence.sh)
-#ifndef OVL_X2_ARGMAX
-#define OVL_X2_ARGMAX 0          // the longest-remaining-match search of Process_Matches
-#endif
-#ifndef OVL_X2_REMOVE
-#define OVL_X2_REMOVE 0          // the Lies_On_Alignment removal pass (a dry pass first)
-#endif
-#ifndef OVL_X2_TB
-#define OVL_X2_TB 0              // the traceback of every row-loop call
-#endif
-#ifndef OVL_X2_FWD
-#define OVL_X2_FWD 0             // the whole forward row-loop call (rows + traceback)
-#endif
-#ifndef OVL_X2_LOG
-#define OVL_X2_LOG 0             // every row-log store
-#endif
-#ifndef OVL_X2_CONV
-#define OVL_X2_CONV 0            // Set_Right_Delta's stack -> Right_Delta pass (and its syncs)
-#endif
-#ifndef OVL_X2_STAGE
-#define OVL_X2_STAGE 0           // staging both strands of a pair into LDS
-#endif
 static_assert(64 * OVL_RJ <= OVL_LOGW, "the row log's stripe holds the register window");
 
 #ifdef OVL_PROFILE
@@ -983,11 +960,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
         kmx = key > kmx ? key : kmx;
         *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
             (cell_t)v;
-#if OVL_X2_LOG
-        asm volatile("" ::: "memory");           // keeps both stores (plain, no waits)
-        *(g_cell_t *)(clogb + (erow | ((uint32_t)(d & (LW - 1)) * (uint32_t)sizeof(cell_t)))) =
-            (cell_t)v;
-#endif
       }
       const int32_t K = wave_max(kmx);
       const int32_t M = K >> WB;
@@ -1094,10 +1066,6 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
   if (!finished || out.mte == 0) tb_last = (tb_e == 0) ? row0 : max_score_len;
   int32_t last = 0, nd = 0;
   PROF_T(pt_tb0);
-#if OVL_X2_TB
-  ped_traceback_codes<L16, LW>(rows, tb_e, tb_d, tb_last, dst, lane, last, nd);
-  asm volatile("" ::: "memory");
-#endif
   ped_traceback_codes<L16, LW>(rows, tb_e, tb_d, tb_last, dst, lane, last, nd);
   out.leftover = last;
   out.nd = nd;
@@ -1178,13 +1146,10 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
     PedOut po;
     PROF_T(pc0);
     if constexpr (FAST) {
-      for (int rep = 0; rep < (OVL_X2_FWD ? 2 : 1); rep++) {
-        if (OVL_X2_FWD) asm volatile("" ::: "memory");
-        po = wave_ped_reg<1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
-                                          X.branch_match_value, X.min_branch_tail_slope, A.w, a0,
-                                          am, B.w, b0, bn, error_limit, WM.rows, WM.rmlim, stk,
-                                          lane);
-      }
+      po = wave_ped_reg<1, SS, L16, RJ>(X, X.e_cap, X.partial, X.min_branch_end_dist,
+                                        X.branch_match_value, X.min_branch_tail_slope, A.w, a0,
+                                        am, B.w, b0, bn, error_limit, WM.rows, WM.rmlim, stk,
+                                        lane);
     }
     else
       po = wave_ped<1, SS, L16>(X, A, a0, am, B, b0, bn, error_limit, WM, stk, lane);
@@ -1205,16 +1170,13 @@ __device__ ExtOut extend_alignment(const ExtendArgs &X, const Node &Mv, const SS
       if (lane == 0) stk[n] = po.leftover + 1;     // "last + 1"
       vm_sync();
       n++;
-      for (int rep = 0; rep < (OVL_X2_CONV ? 2 : 1); rep++) {
-        if (OVL_X2_CONV) asm volatile("" ::: "memory");
-        for (int32_t i = lane; i < n - 1; i += 64) {
-          int32_t src = n - 1 - i;
-          int32_t a = stk[src], b = stk[src - 1];
-          int32_t v = (a < 0 ? -a : a) * ((b > 0) - (b < 0));
-          RD[i] = s_first ? -v : v;
-        }
-        vm_sync();
+      for (int32_t i = lane; i < n - 1; i += 64) {
+        int32_t src = n - 1 - i;
+        int32_t a = stk[src], b = stk[src - 1];
+        int32_t v = (a < 0 ? -a : a) * ((b > 0) - (b < 0));
+        RD[i] = s_first ? -v : v;
       }
+      vm_sync();
       rd_len = n - 1;
     }
   }
@@ -1604,16 +1566,11 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     // longest remaining match, first in list order on ties (:473-480)
     PROF_T(pa0);
     int32_t bv = -1, bi = 0x7fffffff;
-    for (int rep = 0; rep < (OVL_X2_ARGMAX ? 2 : 1); rep++) {
-      if (OVL_X2_ARGMAX) asm volatile("" ::: "memory");
-      bv = -1; bi = 0x7fffffff;
-      for (int32_t i = lane; i < nn; i += 64) {
-        int32_t L = nodes[i].Len;
-        if (L > bv) { bv = L; bi = i; }
-      }
-      wave_argmax(bv, bi);
-      if (OVL_X2_ARGMAX) asm volatile("" :: "v"(bv), "v"(bi));
+    for (int32_t i = lane; i < nn; i += 64) {
+      int32_t L = nodes[i].Len;
+      if (L > bv) { bv = L; bi = i; }
     }
+    wave_argmax(bv, bi);
     Node M = nodes[bi];
     if (X.dbg && lane == 0) atomicAdd(&X.dbg[5], 1ull);
 #ifdef OVL_PROFILE
@@ -1668,7 +1625,7 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
     // with (s_i, diag_i); the walk stops at the first i with start < thr_i = s_i + |LD[i]|
     // and compares with diag_i (or with the final diag).  thr is non-decreasing.  The
     // thresholds live in the wave's LDS scratch.
-    auto by_search = [&](auto *thr, auto *dgl, auto sync, bool commit) {
+    auto by_search = [&](auto *thr, auto *dgl, auto sync) {
       int32_t cs = S_Lo, cd = T_Lo - S_Lo;
       for (int32_t i0 = 0; i0 < ld_len; i0 += 64) {
         const int32_t i = i0 + (int32_t)lane;
@@ -1702,15 +1659,13 @@ __device__ bool process_pair(const ExtendArgs &X, const PairRec &P, const Unit &
           const int32_t dd = (nd.Offset - nd.Start) - (int32_t)dgl[lo];
           rm = (dd < 0 ? -dd : dd) <= SHIFT_SLACK;
         }
-        if (rm && commit) { nodes[i].Len = ~nd.Len; removed++; }
-        if (rm && !commit) asm volatile("" :: "v"(nd.Len));
+        if (rm) { nodes[i].Len = ~nd.Len; removed++; }
       }
       sync();
     };
     if (on_aln && per * (ld_len + 1) <= WM.ldcap) {
       lds_t *thr = (lds_t *)WM.ldc;
-      if (OVL_X2_REMOVE) by_search(thr, thr + ld_len + 1, [] { lds_sync(); }, false);
-      by_search(thr, thr + ld_len + 1, [] { lds_sync(); }, true);
+      by_search(thr, thr + ld_len + 1, [] { lds_sync(); });
     } else {
       const int32_t *ldp = LD;
       if (ld_len <= WM.ldcap) {
@@ -1947,13 +1902,9 @@ k_extend(ExtendArgs X) {
     if constexpr (STAGE) {
       bool ok = false;
       if (!(S.ex_wild || S.ex_nul || T.ex_wild) && S.len <= X.stage_len && T.len <= X.stage_len) {
-        StrandLP SL, TL;
-        for (int rep = 0; rep < (OVL_X2_STAGE ? 2 : 1); rep++) {
-          if (OVL_X2_STAGE) asm volatile("" ::: "memory");
-          SL = stage_strand(S, sw, lane);
-          TL = stage_strand(T, tw, lane);
-          lds_sync();
-        }
+        StrandLP SL = stage_strand(S, sw, lane);
+        StrandLP TL = stage_strand(T, tw, lane);
+        lds_sync();
         PROF_T(pp0);
         ok = process_pair<true, L16, false, RJ>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);
 #ifdef OVL_PROFILE
