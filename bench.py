@@ -196,6 +196,12 @@ def main() -> None:
             "breakdown_ms": {"index": round(st["ms_index"], 2), "seed": round(st["ms_seed"], 2),
                              "extend": round(st["ms_extend"], 2)},
             "seed_hits": st["seed_hits"], "seed_nodes": st["seed_nodes"], "pairs": st["pairs"],
+            # overlapInCore's -s counters of the last step (rank 0's at N > 1) and the driver's
+            # batch structure (hash batches, super-batches, query chunks)
+            "counters": {k: st.get(k) for k in (
+                "total_overlaps", "kmer_hits_with_olap", "kmer_hits_without_olap",
+                "kmer_hits_skipped", "multi_overlaps", "contained_overlaps", "dovetail_overlaps",
+                "hash_batches", "super_batches", "query_chunks")},
             "pair_kernels": {"staged": st.get("staged_pairs"), "long": st.get("long_pairs"),
                              "generic": st.get("generic_pairs")},
             "setup_s": round(setup_s, 1),
@@ -498,8 +504,10 @@ class Configs4Rank(Configs2):
 
     def config(self, P_maxerate, world, backend):
         a = self.args
-        return {"workload": "configs[4] rank job at 1/8 scale: 500k ONT reads x 12 kb "
-                            "(+-20 %) at 15x, one `-h lo-hi -r 1-hi` OverlapDriver job of the "
+        scale = "full scale" if a.reads >= 4_000_000 else f"{a.reads / 4e6:g} scale"
+        return {"workload": f"configs[4] rank job at {scale}: {a.reads // 1000}k ONT reads x "
+                            f"{a.read_len // 1000} kb (+-20 %) at {a.coverage:g}x, one "
+                            "`-h lo-hi -r 1-hi` OverlapDriver job of the "
                             f"{len(self.jobs)}-rank plan, --hashbits {self.HASHBITS} "
                             f"--hashload {self.HASHLOAD}",
                 "reads": a.reads, "read_len": a.read_len, "coverage": a.coverage,

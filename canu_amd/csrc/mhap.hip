@@ -140,6 +140,34 @@ __device__ __forceinline__ void xs64(uint32_t &lo, uint32_t &hi) {
   hi = (uint32_t)(x >> 32);
 }
 
+// One xorshift64 step of N independent chains, each sub-step over all chains before the
+// next (shift results in their own registers): written chain by chain, the compiler emitted
+// every chain's 9 instructions back to back, each on the previous one's result.  On the
+// configs[3] sketch 845 -> 831 ms (profiles/r05h_mhap_xorshift_ab.txt, sketches equal); the
+// kernel is VALU-bound on the draws themselves (~9.5 VALU per draw, the PMC's count:
+// profiles/r05f_mhap_pmc.txt), so interleaving gains little
+template <int N>
+__device__ __forceinline__ void xs64_n(uint32_t (&lo)[N], uint32_t (&hi)[N]) {
+  uint64_t x[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = ((uint64_t)hi[i] << 32) | lo[i];
+  uint64_t t[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) t[i] = x[i] << 21;
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] ^= t[i];
+#pragma unroll
+  for (int i = 0; i < N; i++) t[i] = x[i] >> 35;
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] ^= t[i];
+#pragma unroll
+  for (int i = 0; i < N; i++) t[i] = x[i] << 4;
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] ^= t[i];
+#pragma unroll
+  for (int i = 0; i < N; i++) { lo[i] = (uint32_t)x[i]; hi[i] = (uint32_t)(x[i] >> 32); }
+}
+
 // Stage 1 (oracle: mhap_oracle.sketch)
 __global__ void __launch_bounds__(256) k_mh_sketch(SketchArgs A) {
   extern __shared__ int32_t s_min[];               // [4 waves][H]
@@ -408,16 +436,16 @@ __global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
       constexpr int WC = decltype(wc)::value;
       for (int32_t j = 0; j < H; j++) {
         int32_t m = I32MAX;
+        if constexpr (WC > 0) {
 #pragma unroll
-        for (int i = 0; i < RKW; i++) {
-          if constexpr (WC > 0) {
+          for (int t = 0; t < WC; t++) {
+            xs64_n<RKW>(XL, XH);
 #pragma unroll
-            for (int t = 0; t < WC; t++) {
-              xs64(XL[i], XH[i]);
-              const int32_t v = (int32_t)XL[i];
-              m = v < m ? v : m;
-            }
-          } else {
+            for (int i = 0; i < RKW; i++) m = (int32_t)XL[i] < m ? (int32_t)XL[i] : m;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < RKW; i++) {
             for (int32_t t = 0; t < W[i]; t++) {
               xs64(XL[i], XH[i]);
               const int32_t v = (int32_t)XL[i];

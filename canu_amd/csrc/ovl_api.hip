@@ -1561,8 +1561,16 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
             "%.1f GB needed, %.1f GB free\n", nu, (unsigned long long)total, Q.runs.size(),
             need / 1e9, fr / 1e9);
   // up to half the free HBM (the configs[4] rank-0 job at 1/8 scale: 3.8 G windows, 67 GB),
-  // counting what an earlier job's arrays hold as free
-  if (need > (fr + sq_held_bytes(c)) / 2) { sq_release(c); return OVL_OK; }
+  // counting what an earlier job's arrays hold as free.  A driver job's query chunks were
+  // planned against that rule before its search buffers existed (plan_query_chunks); from
+  // then on those buffers keep their size (sticky_budgets), so a later chunk needs only fit
+  // what is free beside them -- under the half rule the full-size configs[4] job sorted its
+  // first chunk only and probed the other five by random lookups (r05g: 120 launches)
+  const uint64_t avail = fr + sq_held_bytes(c);
+  if (c->sticky_budgets ? need + (4ull << 30) > avail : need > avail / 2) {
+    sq_release(c);
+    return OVL_OK;
+  }
   hipStream_t s = c->stream;
   const auto t0 = std::chrono::steady_clock::now();
   size_t tmpb = 0;
@@ -2254,8 +2262,11 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
     auto acc_fits = [&]() {
       return A.units.n >= A.nu + nu_c && A.pnodes.n >= A.nn + nn_c && A.pairs.n >= A.np + np_c;
     };
-    // what the accumulator holds is extended first rather than moved into bigger buffers
-    if (!acc_fits() && A.np)
+    // once it holds a launch's worth (a quarter of the flush thresholds), what the
+    // accumulator holds is extended rather than moved into bigger buffers: a regrow on a full
+    // device costs ~1 s (the full-size configs[4] job, r05e), while smaller launches lose to
+    // their tails (one launch per search: extension 8.4 -> 23 s, r05f)
+    if (!acc_fits() && (A.np >= ACC_PAIRS / 4 || A.nn >= ACC_NODES / 4))
       if (int rc = flush_acc()) return rc;
     if (!acc_fits()) {
       // growing moves the buffers: the pending extension (which reads them) must be done,
