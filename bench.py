@@ -165,7 +165,8 @@ def main() -> None:
     seed_only = job.seed_only() if world == 1 and not args.no_seed_only else None
     shard = job.shard_timing(ms_step) if world == 1 and not args.no_shard_timing else None
     xgmi = None
-    if world > 1 and backend == "nccl":
+    # over RCCL; on the one-GPU rehearsal (CANU_DEVICE, gloo) too, for the path's logic
+    if world > 1 and (backend == "nccl" or "CANU_DEVICE" in os.environ):
         try:
             xgmi = job.index_allgather_timing(torch)
         except Exception as e:          # a side measurement: never lose the bench line to it

@@ -232,7 +232,7 @@ struct ovl_ctx {
   // an OverlapDriver job's phase 3 (ovl_overlap_driver): the index buffers are allocated for
   // the largest super-batch at once, and the search buffers keep the size the first search
   // gave them -- a hipFree / hipMalloc of tens of GB on a nearly full device costs ~0.5 s
-  uint64_t index_reserve = 0;
+  uint64_t index_reserve = 0, sq_reserve = 0;
   bool sticky_budgets = false;
 
   // pending extension work (see find_impl): chains of several probe chunks -- and of the
@@ -1414,7 +1414,12 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
     if (reached) {
       if (el < eb && !boundaries_only) {
         // the prefix's index cut down to the batch (k_cut_index), or built again over it
-        static const bool cut = !getenv("OVL_CUT_FILTER") || atoi(getenv("OVL_CUT_FILTER")) != 0;
+        // (OVL_CUT_FILTER=0; read per build, so a test can compare the two in one process).
+        // After a cut, index_records stays the prefix's count on purpose: the occurrence array
+        // is the prefix's, and the cut table's runs point into it (an export copies all of it).
+        // Reads in (el, eb] keep the screened-end bits the prefix build set; they are no
+        // target of this batch, and the next build clears every read's bits (k_clear_screen)
+        const bool cut = !getenv("OVL_CUT_FILTER") || atoi(getenv("OVL_CUT_FILTER")) != 0;
         if (cut) {
           HIPC(hipEventRecord(c->ev[0], s));
           hipLaunchKernelGGL(k_cut_index, dim3(8 * c->n_cu), dim3(256), 0, s, c->d_tab.p,
@@ -1603,6 +1608,10 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
       ublk.push_back(x);
     }
   }
+  // a driver job's chunks differ by a few windows: the first one takes the largest chunk's
+  // size (ovl_ctx::sq_reserve), or the next would free and reallocate ~57 GB (~1.7 s here)
+  if (c->sq_reserve > total && (Q.key.n < c->sq_reserve || Q.wid.n < c->sq_reserve))
+    if (Q.key.alloc(c->sq_reserve) || Q.wid.alloc(c->sq_reserve)) { /* exact sizes below */ }
   if (Q.key.alloc(total) || Q.wid.alloc(total) || Q.key2.alloc(maxrun) || Q.wid2.alloc(maxrun) ||
       Q.tmp.alloc(std::max<size_t>(tmpb, 1)) || Q.dwbase.alloc(Q.wb.size()) ||
       Q.dunits.alloc(nu) || Q.ublk.alloc(std::max<size_t>(ublk.size(), 1)) ||
@@ -2817,7 +2826,8 @@ int ovl_find_overlaps(ovl_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
 // OVL_SQ_CHUNK_WINDOWS (tests) caps a chunk's windows.
 static std::vector<std::pair<uint32_t, uint32_t>> plan_query_chunks(ovl_ctx *c, uint32_t bgn,
                                                                     uint32_t end, uint32_t lib_lo,
-                                                                    uint32_t lib_hi) {
+                                                                    uint32_t lib_hi,
+                                                                    uint64_t *max_windows) {
   std::vector<std::pair<uint32_t, uint32_t>> out;
   const uint32_t k = c->P.kmer_len;
   size_t fr = 0, tot = 0;
@@ -2841,12 +2851,14 @@ static std::vector<std::pair<uint32_t, uint32_t>> plan_query_chunks(ovl_ctx *c, 
       add = 2ull * (uint64_t)(L - (int32_t)k + 1);
     if (w + add > wcap && a > lo) {
       out.push_back({lo, a - 1});
+      *max_windows = std::max(*max_windows, w);
       lo = a;
       w = 0;
     }
     w += add;
   }
   if (end >= bgn) out.push_back({lo, end});
+  *max_windows = std::max(*max_windows, w);
   return out;
 }
 
@@ -3037,7 +3049,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   // that keep their first size (ovl_ctx::index_reserve / sticky_budgets), for this job only
   struct Reserve {
     ovl_ctx *c;
-    ~Reserve() { c->index_reserve = 0; c->sticky_budgets = false; }
+    ~Reserve() { c->index_reserve = 0; c->sq_reserve = 0; c->sticky_budgets = false; }
   } reserve_guard{c};
   c->index_reserve = sb_max + c->h_skip.size();
   c->sticky_budgets = true;
@@ -3067,7 +3079,8 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   };
   const bool sq_on = sq_mode == 1 || (sq_mode == 2 && sbs.size() >= 2) ||
                      (sq_mode == 3 && searches_of(g_bgn_ref) >= SQ_AUTO_SEARCHES);
-  if (sq_on) qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref);
+  if (sq_on) qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref,
+                                         &c->sq_reserve);
   if (qchunks.empty()) qchunks.push_back({g_bgn_ref, ref_last});
   // (chunk, super-batch), the super-batches of every other chunk in reverse order: a chunk
   // then starts with the index its predecessor ended on when both reach the last super-batch

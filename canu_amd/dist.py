@@ -280,6 +280,9 @@ def share_index(src, dsts, dist, dev, src_rank: int = 0):
         for p in _INDEX_PARTS:
             if sizes[p]:
                 dist.broadcast(bufs[p], src_rank)
+    # the broadcasts run on torch's streams, the import's copies on the library's own: the
+    # buffers must be complete before ovl_import_index reads them
+    torch.cuda.synchronize(dev)
     d = _IndexDesc()
     for f, v in zip(_INDEX_META, m):
         setattr(d, f, v)

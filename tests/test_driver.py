@@ -415,3 +415,42 @@ def test_oracle_super_batches_equal_batches(case, group):
     assert got.shape == want.shape and np.array_equal(got, want)
     for _, f in STAT_KEYS:
         assert tot[f] == wst[f], (f, tot[f], wst[f])
+
+
+@pytest.mark.gpu
+def test_gpu_cut_index_equals_rebuild(built, monkeypatch):
+    """A hash batch the table load cuts inside its first build: the prefix's index cut down
+    to the batch by k_cut_index (the default) searches exactly like an index built again over
+    the batch's own reads (OVL_CUT_FILTER=0) -- same batch ends, records and every counter,
+    for two consecutive batches, with end skip k-mers (screened-end bits set by the prefix
+    build on reads past the cut, Build_Hash_Index.C:147-170)."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore
+    kw, batch, _, _ = CASES["table_load"]
+    rs = synth_reads(**kw)
+    skip = _end_skip_kmers(rs)
+    P = _params()
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("OVL_CUT_FILTER", mode)
+        O = OicParameters(Kmer_Len=22, maxErate=P["max_erate"], Min_Olap_Len=500,
+                          Hash_Mask_Bits=batch["hashbits"],
+                          Max_Hash_Load=batch["hashload"]).finalize()
+        oic = OverlapInCore(O, device=0)
+        try:
+            oic.load_reads(rs)
+            oic.set_skip_kmers(skip)
+            res = []
+            bgn = 1
+            for _ in range(2):
+                last = oic.build_hash_batch(bgn, rs.nreads)
+                got = oic.fetch(oic.find_overlaps(1, rs.nreads))
+                st = oic.stats()
+                res.append((last, got, {k: st[k] for _, k in STAT_KEYS}))
+                bgn = last + 1
+        finally:
+            oic.close()
+        out[mode] = res
+    for (l1, g1, s1), (l0, g0, s0) in zip(out["1"], out["0"]):
+        assert 1 < l1 < rs.nreads and l1 == l0
+        assert g1.shape[0] > 0 and g1.shape == g0.shape and np.array_equal(g1, g0)
+        assert s1 == s0
