@@ -683,8 +683,10 @@ def rooflines(args, job, st, world):
             probe_roof["sorted_launches"] = n_sorted
             probe_roof["note"] = ("k_probe_sorted (the job's windows sorted by k-mer, DESIGN.md "
                                   "round 4): bytes = 12 per sorted window + the table and "
-                                  "filter read once; it does no random table lookups, so "
-                                  "it is priced against HBM only")
+                                  "filter read once, or at most one 16-B entry and one 8-B "
+                                  "filter word per window when they are larger than the run "
+                                  "(round 5); it does no random table lookups, so it is "
+                                  "priced against HBM only")
             return roof, probe_roof, note
         if tb:
             probe_roof["traffic_gbs"] = round(tb / (avg_ms * 1e-3) / 1e9, 1)

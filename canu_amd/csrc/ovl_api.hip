@@ -2374,10 +2374,14 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         (void)hipEventElapsedTime(&tstep, c->ev[4], c->ev[5]);
         ms_probe += t;
         ms_probe_rest += tstep > t ? tstep - t : 0.f;  // zeroing + unit hit counts
-        // algorithmic bytes: the sorted windows (8-B key + 4-B id) and the table and its
-        // filter read once each (the hits' 8-B records on top are not counted)
-        probe_bytes += 12ull * R.n + 16ull * ((1ull << c->tab_bits)) +
-                       (SA.X.bloom ? 8ull * ((1ull << (c->tab_bits - c->slice_bits)) << c->bloom_w) : 0ull);
+        // algorithmic bytes: the sorted windows (8-B key + 4-B id), and the table and its
+        // filter read once each -- or, when they are larger than the run (a full-size
+        // configs[4] super-batch's 68.7 GB table against a run of 2^29 windows), at most one
+        // entry and one filter word per window (the hits' 8-B records are not counted)
+        const uint64_t tab_b = 16ull << c->tab_bits;
+        const uint64_t flt_b = SA.X.bloom ? 8ull * ((1ull << (c->tab_bits - c->slice_bits)) << c->bloom_w) : 0ull;
+        probe_bytes += 12ull * R.n + std::min<uint64_t>(tab_b, 16ull * R.n) +
+                       std::min<uint64_t>(flt_b, 8ull * R.n);
         Q.probed = (int)sq_run;
       }
       nb = ue - u0;
