@@ -28,10 +28,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "overlaps/sec + Gbp-vs-Gbp/sec, MHAP sketch+filter, 200k x 15 kb reads"
 HBM_PEAK_GBS = 8000.0
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 1024 SIMDs x 32 lanes/clk
+VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 2.0         # G wave64 VALU instructions/s: 1,024 SIMDs,
+                                                # one per 2 cycles
 
 
-def main() -> None:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); default: the launcher's WORLD_SIZE, else 1")
@@ -50,7 +51,45 @@ def main() -> None:
                     help="-f table size (16-mers sampled from the reads, graded fractions)")
     ap.add_argument("--cpu-sample-reads", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def workload_key(args) -> dict:
+    """What the PMC figures of profiles/traffic_mhap.json were taken on (tools/pmc_mhap.py)."""
+    return {"workload": "configs3", "reads": args.reads, "read_len": args.read_len,
+            "coverage": args.coverage, "read_error": args.read_error,
+            "sensitivity": args.sensitivity, "seed": args.seed, "weighting": args.weighting,
+            "freq_kmers": args.freq_kmers}
+
+
+def mhap_source_hash() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for rel in ("canu_amd/csrc/mhap.hip", "include/canu_mhap.h"):
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def load_pmc(args, world):
+    """profiles/traffic_mhap.json when taken on this workload and these sources, else None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic_mhap.json")) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, "profiles/traffic_mhap.json missing"
+    meta = t.get("_method", {})
+    if world != 1:
+        return None, "PMC figures are single-GPU: not used at N > 1"
+    if meta.get("workload") != workload_key(args):
+        return None, f"PMC passes ({meta.get('tag')}) were taken on another workload"
+    if meta.get("src_sha") != mhap_source_hash():
+        return None, f"PMC passes ({meta.get('tag')}) were taken on other MHAP sources"
+    return t, f"profiles/traffic_mhap.json ({meta.get('tag')}, same workload and sources)"
+
+
+def main() -> None:
+    args = parse_args()
 
     from canu_amd import launch
     # decide BEFORE anything touches the GPU: N ranks of this script in a child launcher
@@ -170,22 +209,43 @@ def main() -> None:
     value = total_ovl * args.steps / elapsed
     gbp = total_bases / 1e9
 
-    # Dominant kernel: the MinHash sketch (integer VALU: per k-mer and hash function one
-    # 64-bit xorshift = 3 shifts + 3 xors on 32-bit halves, plus a min).  HBM roofline:
-    # bases read once (1 B/base) + the sketch rows written (4 B x H per read).
+    # Dominant kernel: the MinHash sketch kernel (k_mh_sketch_w with canu's weighting, else
+    # k_mh_sketch), its launches timed live by the library's events (ms_sketch_kernel, ABI 5).
+    # It is bound by vector-instruction issue (~9.5 VALU per xorshift64 draw, DESIGN.md
+    # round 5): with the PMC pass of this workload and these sources (profiles/
+    # traffic_mhap.json) the roofline is VALU wave-instructions/s against 1,024 SIMDs x
+    # 2.4 GHz / 2 (wave64 over 2 cycles); its HBM figures beside: algorithmic bytes = the
+    # sorted k-mer keys read once (4 B per k-mer) + the sketch rows written (4 B x H per read).
     kmers = st["sketch_kmers"]
-    sk_ms = ms["sketch"] / args.steps
-    sk_bytes = total_bases / world + 4.0 * H * (hi - lo)
-    roof = {"bound": "hbm", "kernel": "k_mh_sketch + k_mh_ordered",
-            "achieved": round(sk_bytes / (sk_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "traffic": None,
-            "algorithmic_bytes_per_launch": int(sk_bytes), "avg_launch_ms": round(sk_ms, 3),
-            "limiter": "integer VALU (H xorshift64 hash functions per k-mer)",
-            "valu": {"lane_ops": int(kmers * H * 9),
-                     "achieved_tops": round(kmers * H * 9 / (sk_ms * 1e-3) / 1e12, 2),
-                     "peak_tops": round(VALU_PEAK_TOPS, 1),
-                     "frac": round(kmers * H * 9 / (sk_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}}
-    roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
+    nl = max(int(st.get("sketch_launches", 0)), 1)
+    k_ms = st.get("ms_sketch_kernel", 0.0) / nl
+    kname = "k_mh_sketch_w" if args.weighting == "canu" else "k_mh_sketch"
+    per_launch = (4.0 * kmers + 4.0 * H * (hi - lo)) / nl
+    pmc, pmc_note = load_pmc(args, world)
+    kp = (pmc or {}).get(kname, {})
+    hbm = {"achieved": round(per_launch / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "algorithmic_bytes_per_launch": int(per_launch),
+           "traffic": kp.get("hbm_bytes_per_launch")}
+    if hbm["achieved"] is not None:
+        hbm["frac"] = round(hbm["achieved"] / HBM_PEAK_GBS, 5)
+    roof = {"kernel": kname, "launches": nl, "avg_launch_ms": round(k_ms, 3),
+            "pmc_source": pmc_note}
+    if kp and k_ms > 0:
+        valu = kp["valu_insts"] / (k_ms * 1e-3) / 1e9
+        pk = VALU_ISSUE_PEAK_G
+        roof.update({"bound": "issue", "achieved": round(valu, 1), "peak": round(pk, 1),
+                     "unit": "G VALU wave-instructions/s", "frac": round(valu / pk, 4),
+                     "traffic": kp.get("hbm_bytes_per_launch"), "hbm": hbm,
+                     "wait_inst_any_frac": round(kp.get("wait_inst_any_frac", 0.0), 3),
+                     "limiter": "vector-instruction issue: the xorshift64 draws of the "
+                                "weighted MinHash (H functions x w draws per distinct k-mer)"})
+    else:
+        roof.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": hbm.get("frac"), "traffic": None,
+                     "algorithmic_bytes_per_launch": int(per_launch),
+                     "limiter": "VALU issue (see DESIGN.md); no PMC issue counters for this "
+                                "workload and these sources, so the HBM figure is given"})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

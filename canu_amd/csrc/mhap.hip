@@ -931,7 +931,7 @@ struct mhap_ctx {
   mhap_params P;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // [2..3]: the MinHash kernel
   uint32_t first_iid = 1, nreads = 0;
   std::vector<uint32_t> h_len;
   MBuf<uint8_t> bases_own;
@@ -1009,7 +1009,8 @@ int mhap_ctx_create(const mhap_params *p, int device, mhap_ctx **out) {
   c->P = *p;
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev[0]) != hipSuccess || hipEventCreate(&c->ev[1]) != hipSuccess) {
+      hipEventCreate(&c->ev[0]) != hipSuccess || hipEventCreate(&c->ev[1]) != hipSuccess ||
+      hipEventCreate(&c->ev[2]) != hipSuccess || hipEventCreate(&c->ev[3]) != hipSuccess) {
     delete c;
     return mfail(M_HIP, "stream/event creation failed");
   }
@@ -1029,6 +1030,14 @@ void mhap_ctx_destroy(mhap_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// the MinHash kernel's launch just completed (events ev[2] .. ev[3]): its time, summed
+static void sketch_kernel_time(mhap_ctx *c) {
+  float t = 0;
+  (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+  c->stats.ms_sketch_kernel += t;
+  c->stats.sketch_launches++;
 }
 
 static int alloc_sketches(mhap_ctx *c) {
@@ -1284,12 +1293,15 @@ static int sketch_weighted(mhap_ctx *c, uint32_t r0, uint32_t nr) {
     WSketchArgs WA{c->wkeys2.p, tot, d_koff.p, d_vcnt.p, r0 + a, nb, (int32_t)k,
                    (int32_t)c->P.num_hashes, c->nf ? c->ftab.p : nullptr, c->fmask, c->dmult,
                    c->W.no_tf, c->minhash.p};
+    MHC(hipEventRecord(c->ev[2], s));
     if (k32)
       hipLaunchKernelGGL(k_mh_sketch_w<uint32_t>, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
     else
       hipLaunchKernelGGL(k_mh_sketch_w<uint64_t>, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
     MHC(hipGetLastError());
+    MHC(hipEventRecord(c->ev[3], s));
     MHC(hipStreamSynchronize(s));                           // d_koff / d_vcnt are freed here
+    sketch_kernel_time(c);
     a = b;
   }
   return M_OK;
@@ -1305,6 +1317,8 @@ int mhap_sketch(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   hipStream_t s = c->stream;
   const uint32_t r0 = bgn - c->first_iid, nr = end - bgn + 1;
   MHC(hipMemsetAsync(c->kctr.p, 0, 8, s));
+  c->stats.ms_sketch_kernel = 0;
+  c->stats.sketch_launches = 0;
   MHC(hipEventRecord(c->ev[0], s));
   // one block per read; launches of <= 65535 * 16 reads keep grids modest
   if (c->weighted) {
@@ -1317,8 +1331,12 @@ int mhap_sketch(mhap_ctx *c, uint32_t bgn, uint32_t end) {
       SketchArgs SA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.k,
                     (int32_t)c->P.num_hashes, c->nfilter ? c->filter.p : nullptr, c->nfilter,
                     c->minhash.p, c->kctr.p};
+      MHC(hipEventRecord(c->ev[2], s));
       hipLaunchKernelGGL(k_mh_sketch, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, SA);
       MHC(hipGetLastError());
+      MHC(hipEventRecord(c->ev[3], s));
+      MHC(hipEventSynchronize(c->ev[3]));
+      sketch_kernel_time(c);
     }
     OrderedArgs OA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.ordered_k,
                    (int32_t)c->P.ordered_sketch, c->ordered.p, c->ocount.p};

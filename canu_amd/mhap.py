@@ -26,7 +26,7 @@ EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last
            "mhap_copy_sketches_host", "mhap_weighting_init", "mhap_set_kmer_frequencies",
            "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
 
-ABI_VERSION = 4          # MHAP_ABI_VERSION of include/canu_mhap.h
+ABI_VERSION = 5          # MHAP_ABI_VERSION of include/canu_mhap.h
 
 
 class MhapError(RuntimeError):
@@ -52,7 +52,8 @@ class _Stats(ctypes.Structure):
     _fields_ = [("sketched_reads", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
                 ("overlaps", ctypes.c_uint64), ("ms_sketch", ctypes.c_double),
                 ("ms_index", ctypes.c_double), ("ms_candidates", ctypes.c_double),
-                ("ms_compare", ctypes.c_double), ("sketch_kmers", ctypes.c_uint64)]
+                ("ms_compare", ctypes.c_double), ("sketch_kmers", ctypes.c_uint64),
+                ("ms_sketch_kernel", ctypes.c_double), ("sketch_launches", ctypes.c_uint64)]
 
 
 _lib = None

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MHAP_ABI_VERSION 4
+#define MHAP_ABI_VERSION 5
 
 typedef struct {
   uint32_t k;               /* -k                      MinHash k-mer size, 1..32        */
@@ -72,6 +72,9 @@ typedef struct {
   double   ms_candidates;   /* device time: first-stage lookups                         */
   double   ms_compare;      /* device time: second-stage filter                         */
   uint64_t sketch_kmers;    /* k-mers hashed by the MinHash kernel                      */
+  double   ms_sketch_kernel; /* device time of the MinHash kernel launches alone (ABI 5:
+                                the dominant kernel's live launch time, bench_mhap.py)   */
+  uint64_t sketch_launches; /* its launches                                              */
 } mhap_stats;
 
 typedef struct mhap_ctx mhap_ctx;

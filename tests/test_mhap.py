@@ -48,7 +48,7 @@ def test_header_declares_the_python_exports():
 def test_library_exports_every_declared_symbol(built):
     lib = mhap.load_library()
     assert [f for f in mhap.EXPORTS if not hasattr(lib, f)] == []
-    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 4
+    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 5
 
 
 def test_params_init_is_canu_normal(built):

@@ -3,7 +3,9 @@
 # k_mh_ordered: the ordered sketch), each pass a run of its own under its own time limit:
 #   issue:  VALU / SALU instructions, active / wait cycles, wave cycles
 #   bytes:  FETCH_SIZE, then WRITE_SIZE (HBM traffic, the guide's passes)
-# and a kernel trace.  usage: bash tools/mhap_pmc.sh TAG
+# and a kernel trace; then tools/pmc_mhap.py sums them per launch into
+# gpurun_out/TAG_traffic_mhap.json (copy it to profiles/traffic_mhap.json for bench_mhap.py).
+# usage: bash tools/mhap_pmc.sh TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-mh}
@@ -24,4 +26,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 pass issue SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY \
   SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
 pass fetch FETCH_SIZE && \
-pass write WRITE_SIZE
+pass write WRITE_SIZE && \
+python3 $R/tools/pmc_mhap.py $TAG $R/gpurun_out/${TAG}_traffic_mhap.json
