@@ -13,9 +13,9 @@ from __future__ import annotations
 import numpy as np
 
 
-# The cost model of one rank's job, from the 1-GPU step on 50k x 10 kb (1 MI355X; the
-# driver's round-4 run, BENCH_r04: index 29 ms over every hashed read, probe 29 ms and chain
-# 62 ms over every query, extension 1,063 ms over the n^2/2 (a, b > a) pairs).  A query shard [lo, hi] only ever pairs with reads
+# The cost model of one rank's job, from the 1-GPU step on 50k x 10 kb (1 MI355X; round 5,
+# profiles/r05c_bench.json: index 29 ms over every hashed read, probe 29 ms and chain
+# 62 ms over every query, extension 1,037 ms over the n^2/2 (a, b > a) pairs).  A query shard [lo, hi] only ever pairs with reads
 # b > a >= lo (Find_Overlaps.C:328 keeps targets with a larger ID), so its rank indexes
 # reads lo..n only: the same records and counters, a smaller index, and occurrence lists
 # (chain work) shortened by (n - lo) / n.
@@ -25,7 +25,7 @@ import numpy as np
 # `-h lo-n -r lo-hi` job exactly, not `-h 1-n`: once a limit is reached, other overlaps may
 # be kept.  canu never passes -l to overlapInCore; bench.py does not use it.
 SHARD_COSTS = {"index_per_read": 29.0 / 50_000, "probe_per_query": 29.0 / 50_000,
-               "chain_per_query": 62.0 / 50_000, "pair": 1063.0 / (50_000 ** 2 / 2)}
+               "chain_per_query": 62.0 / 50_000, "pair": 1037.0 / (50_000 ** 2 / 2)}
 
 
 def shard_cost(n: int, lo: int, hi: int, costs: dict | None = None) -> float:

@@ -128,7 +128,7 @@ def main():
     import bench
     bargs = bench.parse_args(sys.argv[2:])
     jcls = bench.Configs4Rank if bargs.workload == "configs4-rank" else bench.Configs2
-    traffic["_method"] = {"workload": jcls(bargs, 0, 1, None, None).workload_key(),
+    traffic["_method"] = {"workload": jcls(bargs, 0, 1, None).workload_key(),
                           "src_sha": bench.source_hash(),
                           "hbm_bytes": "(r * FETCH_SIZE + WRITE_SIZE) KiB",
                           "read_correction": {"default": 2.0, **READ_CORR},
