@@ -730,7 +730,8 @@ def side_runs(timeout_s: int = 300) -> dict:
                      the MHAP jar unpinned)"""
     import subprocess
     keep4 = ("value", "unit", "ms_per_step", "breakdown_ms", "pairs", "pair_kernels",
-             "roofline", "probe_roofline", "traffic_source", "config", "setup_s")
+             "roofline", "probe_roofline", "traffic_source", "config", "setup_s", "parity",
+             "counters")
     keep3 = ("value", "unit", "ms_per_step", "breakdown_ms", "config", "setup_s", "roofline",
              "candidates_per_step", "overlaps_per_step", "parity")
     runs = {"configs4_rank": ([sys.executable, os.path.join(ROOT, "bench.py"), "--workload",

@@ -234,6 +234,10 @@ struct ovl_ctx {
   // gave them -- a hipFree / hipMalloc of tens of GB on a nearly full device costs ~0.5 s
   uint64_t index_reserve = 0, sq_reserve = 0;
   bool sticky_budgets = false;
+  // an OverlapDriver job whose sorted query windows need several chunks: tables at half the
+  // slots (slices 1x the largest fine bucket's distinct k-mers instead of 2x), so that more
+  // of the HBM holds query windows (fewer chunks, fewer super-batch rebuilds and probes)
+  bool dense_tables = false;
 
   // pending extension work (see find_impl): chains of several probe chunks -- and of the
   // driver's hash batches -- are appended here and extended together in one launch
@@ -1105,7 +1109,8 @@ static int build_index(ovl_ctx *c, uint32_t bgn, uint32_t end, bool bloom = fals
   // ~6 GB) were measured in round 3 too: k_probe 12.4 -> 22.2 ms per launch, since the
   // per-slice {base, size} lookup is a second dependent random access per window
   // (profiles/r03d_bench_perslice.json); not kept
-  c->slice_bits = std::max<uint32_t>(1, ceil_log2((uint64_t)OVL_SLICE_Q * maxd / 4 + 1));
+  const uint64_t slice_q = c->dense_tables ? 4 : OVL_SLICE_Q;
+  c->slice_bits = std::max<uint32_t>(1, ceil_log2(slice_q * maxd / 4 + 1));
   c->tab_bits = cb + fb + c->slice_bits;
   if (c->d_tab.alloc(1ull << c->tab_bits)) return fail(OVL_ERR_OOM, "table 2^%u", c->tab_bits);
   TableArgs T;
@@ -3053,7 +3058,9 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   // that keep their first size (ovl_ctx::index_reserve / sticky_budgets), for this job only
   struct Reserve {
     ovl_ctx *c;
-    ~Reserve() { c->index_reserve = 0; c->sq_reserve = 0; c->sticky_budgets = false; }
+    ~Reserve() {
+      c->index_reserve = 0; c->sq_reserve = 0; c->sticky_budgets = false; c->dense_tables = false;
+    }
   } reserve_guard{c};
   c->index_reserve = sb_max + c->h_skip.size();
   c->sticky_budgets = true;
@@ -3071,10 +3078,6 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     }
     return rc;
   };
-  const auto t_sb0 = clk::now();
-  if (int rc = build_sb(0)) return rc;
-  const double sb0_ms = ms_since(t_sb0, clk::now());
-  std::vector<std::pair<uint32_t, uint32_t>> qchunks;
   // searches of one query chunk: the super-batches whose reads reach past its first read
   auto searches_of = [&](uint32_t qlo) {
     uint64_t n = 0;
@@ -3083,6 +3086,26 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
   };
   const bool sq_on = sq_mode == 1 || (sq_mode == 2 && sbs.size() >= 2) ||
                      (sq_mode == 3 && searches_of(g_bgn_ref) >= SQ_AUTO_SEARCHES);
+  if (sq_on) {
+    // sorted windows (12 B + unit arrays) past a quarter of the device will need chunks: the
+    // full-size configs[4] rank job (13.7 G windows, ~180 GB) does, its 1/8-scale side line
+    // (3.8 G, ~50 GB) does not.  OVL_DENSE_TABLES=0|1 overrides.
+    uint64_t qw = 0;
+    for (uint32_t a = g_bgn_ref; a <= ref_last && a >= g_bgn_ref; a++) {
+      const uint32_t r = a - c->first_iid;
+      const int32_t Lr = (int32_t)c->h_len[r];
+      const uint32_t lib = read_lib(c, r);
+      if (!(lib < d->min_lib_ref || lib > d->max_lib_ref || Lr < c->P.min_olap_len || Lr < (int32_t)k))
+        qw += 2ull * (uint64_t)(Lr - (int32_t)k + 1);
+    }
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) c->dense_tables = 13 * qw > tot / 4;
+    if (const char *e = getenv("OVL_DENSE_TABLES")) c->dense_tables = atoi(e) != 0;
+  }
+  const auto t_sb0 = clk::now();
+  if (int rc = build_sb(0)) return rc;
+  const double sb0_ms = ms_since(t_sb0, clk::now());
+  std::vector<std::pair<uint32_t, uint32_t>> qchunks;
   if (sq_on) qchunks = plan_query_chunks(c, g_bgn_ref, ref_last, d->min_lib_ref, d->max_lib_ref,
                                          &c->sq_reserve);
   if (qchunks.empty()) qchunks.push_back({g_bgn_ref, ref_last});
@@ -3096,9 +3119,9 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     }
   if (getenv("OVL_TIMING"))
     fprintf(stderr, "OVL_TIMING super-batches: %llu batches (phase 1 %.1f ms) -> %zu super-batches "
-            "of <= %llu windows, %zu query chunks over refs %u-%u, %zu searches, sorted windows %s\n",
+            "of <= %llu windows, %zu query chunks over refs %u-%u, %zu searches, sorted windows %s%s\n",
             (unsigned long long)batches, phase1_ms, sbs.size(), (unsigned long long)sb_cap,
-            qchunks.size(), g_bgn_ref, ref_last, plan.size(), sq_on ? "on" : "off");
+            qchunks.size(), g_bgn_ref, ref_last, plan.size(), sq_on ? "on" : "off", c->dense_tables ? ", dense tables" : "");
   c->sq_request = sq_on;
   for (size_t pi = 0; pi < plan.size(); pi++) {
     const auto [qi, si] = plan[pi];

@@ -117,17 +117,21 @@ def test_gpu_sorted_windows_corrupt_sort_falls_back(built, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk_w,sb_w", [("200000", None), ("200000", "300000"), (None, "250000")])
-def test_gpu_query_chunks_and_super_batches_are_exact(built, monkeypatch, chunk_w, sb_w):
+@pytest.mark.parametrize("chunk_w,sb_w,dense", [("200000", None, None), ("200000", "300000", "1"),
+                                                 (None, "250000", None)])
+def test_gpu_query_chunks_and_super_batches_are_exact(built, monkeypatch, chunk_w, sb_w, dense):
     """The driver's search plan (ovl_overlap_driver): the reference's hash batches found by
     its loading loop, consecutive batches joined into super-batches (OVL_SB_WINDOWS caps
     their k-mers), and the -r range searched in query chunks whose sorted windows fit
     (OVL_SQ_CHUNK_WINDOWS caps them), every (chunk, super-batch) pair whose reads can meet
     searched once.  On the small job the caps force ~7 chunks and / or ~5 super-batches: the
     same records and -s counters as the oracle's batch-by-batch OverlapDriver, with N bases
-    and poly-A stretches."""
+    and poly-A stretches.  dense: the half-size tables a chunked full-size job builds
+    (OVL_DENSE_TABLES forces them here)."""
     from canu_amd.overlap_in_core import OverlapInCore
     monkeypatch.setenv("OVL_SQ", "1" if chunk_w else "0")
+    if dense:
+        monkeypatch.setenv("OVL_DENSE_TABLES", dense)
     if chunk_w:
         monkeypatch.setenv("OVL_SQ_CHUNK_WINDOWS", chunk_w)
     if sb_w:
