@@ -51,6 +51,27 @@ def test_golden_digest_fixture():
                                                                              1, 22)
 
 
+def test_configs4_side_line_digest_fixture():
+    """tests/golden/c4rank500k.json: the reference overlapInCore's own run (47 min on 8
+    threads, tools/make_c4_digest.py --reads 500000 --jobs 0) of the configs4-rank side
+    line's job -- rank 0 of the 8-way plan at 1/8 scale, 14 hash batches -- which bench.py's
+    side line checks its records against.  Its workload and job are the ones bench.py runs."""
+    import bench
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "c4rank500k.json")))
+    a = bench.parse_args(["--workload", "configs4-rank"])
+    job = bench.Configs4Rank(a, 0, 1, None)
+    key = job.workload_key()
+    for k in ("reads", "read_len", "coverage", "read_error", "seed", "k", "minlength"):
+        assert float(g["workload"][k]) == float(key[k]), k
+    from canu_amd.dist import hash_block_jobs
+    load = job.HASHLOAD * (1 << job.HASHBITS) * 21             # Configs4Rank.generate's plan
+    plan = hash_block_jobs(a.reads, 8, a.read_len, 36.0, 3.0 * load)[a.rank_job]
+    (j,) = g["jobs"]
+    assert tuple(j["h"]) == tuple(plan["h"]) and tuple(j["r"]) == tuple(plan["r"])
+    assert j["records"] == j["stats"]["total"] == 719115
+    assert len(j["sha256_sorted"]) == 64 and len(j["multiset_hash"]) == 16
+
+
 @pytest.mark.gpu
 def test_gpu_bench_job_matches_reference_digest(built):
     """The full 50k x 10 kb job (bench.py's step) against the reference's own output."""
