@@ -1,4 +1,4 @@
-"""The chain kernel's run replay (OVL_CHAIN_RUNS, k_chain in canu_amd/csrc/ovl_seed.hip) is
+"""The chain kernel's run replay (k_chain in canu_amd/csrc/ovl_seed.hip) is
 exact: a model of Add_Match (overlapInCore-Find_Overlaps.C:79: extend the head node when the
 occurrence is the next window on its diagonal, else walk the list -- move-to-front, the
 consistency rule -- else push a new node) applied entry by entry gives the same node lists and
