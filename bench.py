@@ -430,7 +430,8 @@ class Configs4Rank(Configs2):
         return {"workload": "configs4-rank", "reads": a.reads, "read_len": a.read_len,
                 "coverage": a.coverage, "read_error": a.read_error, "seed": a.seed, "k": a.k,
                 "maxerate": float(np.float32(a.maxerate)), "minlength": a.minlength,
-                "rank_job": a.rank_job}
+                "rank_job": a.rank_job,
+                **({"plan": "r05"} if os.environ.get("CANU_C4_PLAN") == "r05" else {})}
 
     def generate(self):
         """This rank's slice of the read set, on the host before any GPU call (the
@@ -441,7 +442,11 @@ class Configs4Rank(Configs2):
         genome_len = int(n * a.read_len / a.coverage)
         plan_ranks = 8 if self.world == 1 else self.world
         load = self.HASHLOAD * (1 << self.HASHBITS) * 21
-        self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load)
+        # CANU_C4_PLAN=r05: the plan cut by round 5's measured driver costs
+        # (dist.DRIVER_COSTS); the default stays the one the committed digests pin
+        from canu_amd.dist import DRIVER_COSTS
+        costs = DRIVER_COSTS if os.environ.get("CANU_C4_PLAN") == "r05" else None
+        self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load, costs=costs)
         self.job = self.jobs[a.rank_job if self.world == 1 else self.rank]
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world

@@ -148,6 +148,21 @@ def all_gather_rows(local, n: int, dist):
 REHEARSAL_COSTS = {"pair_s": 19.7 / 9.0e6, "probe_window_s": 2.2 / 48e9,
                    "index_window_s": 1.4 / 6.0e9}
 
+# Round 5's driver (super-batches of consecutive hash batches, the query range in sorted
+# chunks), measured on the full-size plan's ranks 0 and 7 on one MI355X
+# (profiles/r05o_c4full.json, r05r7_c4full.json: 18.3 s and 33.7 s -- the rehearsal-cost plan
+# is unbalanced at full size):
+#   extension  0.68 us per (a < b) pair; the pairs are 2.19x the 36-per-read model's count
+#   seed       2.9e-11 s per query window and super-batch it is searched against
+#   index      7.0e-11 s per hashed window per build (one build per (chunk, super-batch))
+#   super-batches of ~0.9 G hashed windows, query chunks of ~4.8 G windows
+# The model gives rank 0 20.0 s and rank 7 30.2 s for that plan.  CANU_C4_PLAN=r05 selects
+# it in bench.py's configs4-rank workload (the default plan, which the committed reference
+# digests pin, stays the rehearsal one).
+DRIVER_COSTS = {"model": "driver", "pair_s": 0.68e-6, "pair_scale": 2.19,
+                "seed_window_s": 2.9e-11, "index_window_s": 7.0e-11,
+                "sb_windows": 0.9e9, "chunk_windows": 4.8e9}
+
 
 def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
                     batch_windows: float, costs: dict | None = None) -> list[dict]:
@@ -163,9 +178,26 @@ def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
     c = dict(REHEARSAL_COSTS if costs is None else costs)
     w = max(read_len - 21.0, 1.0)                 # windows per read and strand (k = 22)
 
+    def cost_driver(lo: int, hi: int) -> float:
+        m = hi - lo + 1
+        pairs = pairs_per_read * (lo + hi) / 2.0 * m / n * c["pair_scale"]
+        n_sb = max(1, int(np.ceil(m * w / c["sb_windows"])))
+        n_ch = max(1, int(np.ceil(2.0 * hi * w / c["chunk_windows"])))
+        # (chunk, super-batch) pairs whose reads can meet: the chunk starts below the
+        # super-batch's last read
+        q0 = 1.0 + np.arange(n_ch) * (hi / n_ch)
+        s_end = lo + (np.arange(n_sb) + 1.0) * (m / n_sb)
+        searched = np.add.outer(q0, -s_end) < 0
+        searches = int(searched.sum())
+        seed_windows = searches * 2.0 * w * hi / n_ch
+        return (pairs * c["pair_s"] + seed_windows * c["seed_window_s"] +
+                searches * (m * w / n_sb) * c["index_window_s"])
+
     def cost(lo: int, hi: int) -> float:
         if hi < lo:
             return 0.0
+        if c.get("model") == "driver":
+            return cost_driver(lo, hi)
         m = hi - lo + 1
         pairs = pairs_per_read * (lo + hi) / 2.0 * m / n    # sum over b of b * ppr / n
         batches = max(1.0, m * w / batch_windows)
