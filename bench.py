@@ -431,7 +431,17 @@ class Configs4Rank(Configs2):
                 "coverage": a.coverage, "read_error": a.read_error, "seed": a.seed, "k": a.k,
                 "maxerate": float(np.float32(a.maxerate)), "minlength": a.minlength,
                 "rank_job": a.rank_job,
-                **({"plan": "r05"} if os.environ.get("CANU_C4_PLAN") == "r05" else {})}
+                **({"plan": "r05"} if self.plan() == "r05" else {})}
+
+    def plan(self) -> str:
+        """Which cost model cuts the 8-rank plan: "r05" (dist.DRIVER_COSTS, fitted to round
+        5's full-size rank jobs) at the full 4M-read size, "r02" (the rehearsal costs, the
+        plan the committed 20k / 500k reference digests pin) below it; CANU_C4_PLAN
+        overrides."""
+        e = os.environ.get("CANU_C4_PLAN")
+        if e in ("r02", "r05"):
+            return e
+        return "r05" if self.args.reads >= 4_000_000 else "r02"
 
     def generate(self):
         """This rank's slice of the read set, on the host before any GPU call (the
@@ -442,10 +452,8 @@ class Configs4Rank(Configs2):
         genome_len = int(n * a.read_len / a.coverage)
         plan_ranks = 8 if self.world == 1 else self.world
         load = self.HASHLOAD * (1 << self.HASHBITS) * 21
-        # CANU_C4_PLAN=r05: the plan cut by round 5's measured driver costs
-        # (dist.DRIVER_COSTS); the default stays the one the committed digests pin
         from canu_amd.dist import DRIVER_COSTS
-        costs = DRIVER_COSTS if os.environ.get("CANU_C4_PLAN") == "r05" else None
+        costs = DRIVER_COSTS if self.plan() == "r05" else None
         self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load, costs=costs)
         self.job = self.jobs[a.rank_job if self.world == 1 else self.rank]
         lo = n * self.rank // self.world

@@ -149,19 +149,46 @@ REHEARSAL_COSTS = {"pair_s": 19.7 / 9.0e6, "probe_window_s": 2.2 / 48e9,
                    "index_window_s": 1.4 / 6.0e9}
 
 # Round 5's driver (super-batches of consecutive hash batches, the query range in sorted
-# chunks), measured on the full-size plan's ranks 0 and 7 on one MI355X
-# (profiles/r05o_c4full.json, r05r7_c4full.json: 18.3 s and 33.7 s -- the rehearsal-cost plan
-# is unbalanced at full size):
+# chunks), fitted to four full-size rank jobs on one MI355X
+# (profiles/r05o_c4full.json, r05r7_c4full.json: the rehearsal-cost plan's ranks 0 and 7,
+# 18.3 and 33.7 s; r05p0_c4full.json, r05p7_c4full.json: a first driver-cost plan's, 26.6
+# and 31.0 s; the fit is within 2 % of all four):
 #   extension  0.68 us per (a < b) pair; the pairs are 2.19x the 36-per-read model's count
 #   seed       2.9e-11 s per query window and super-batch it is searched against
-#   index      7.0e-11 s per hashed window per build (one build per (chunk, super-batch))
-#   super-batches of ~0.9 G hashed windows, query chunks of ~4.8 G windows
-# The model gives rank 0 20.0 s and rank 7 30.2 s for that plan.  CANU_C4_PLAN=r05 selects
-# it in bench.py's configs4-rank workload (the default plan, which the committed reference
-# digests pin, stays the rehearsal one).
+#   index      6.6e-11 s per hashed window per build (one build per (chunk, super-batch))
+#   super-batches of ~1.08 G hashed windows and query chunks of ~5.9 G windows at a job's
+#   hi = 1.2 M reads, both shrinking as hi grows (the read store and the query windows take
+#   more of the 288 GB): 125 and 464 windows less per read of hi
+# bench.py's configs4-rank workload cuts its plan with it at the full 4M-read size (ranks 0,
+# 3 and 7 of that plan measured 29.0, 27.7 and 30.8 s: profiles/r05s*_c4full.json); the 20k
+# and 500k plans, which the committed reference digests pin, stay the rehearsal ones.
 DRIVER_COSTS = {"model": "driver", "pair_s": 0.68e-6, "pair_scale": 2.19,
-                "seed_window_s": 2.9e-11, "index_window_s": 7.0e-11,
-                "sb_windows": 0.9e9, "chunk_windows": 4.8e9}
+                "seed_window_s": 2.9e-11, "index_window_s": 6.6e-11,
+                "sb_windows": 1.08e9, "sb_slope": 125.0, "chunk_windows": 5.9e9,
+                "chunk_slope": 464.0, "hi_ref": 1.2e6}
+
+
+def driver_job_cost(n: int, read_len: float, pairs_per_read: float, lo: int, hi: int,
+                    c: dict | None = None) -> float:
+    """Modelled seconds of one `-h lo-hi -r 1-hi` job on round 5's driver (DRIVER_COSTS):
+    its pairs' extension, plus per searched (query chunk, super-batch) pair the chunk's
+    probes and the super-batch's build."""
+    c = DRIVER_COSTS if c is None else c
+    w = max(read_len - 21.0, 1.0)
+    m = hi - lo + 1
+    pairs = pairs_per_read * (lo + hi) / 2.0 * m / n * c["pair_scale"]
+    sb_cap = c["sb_windows"] - c["sb_slope"] * (hi - c["hi_ref"])
+    ch_cap = c["chunk_windows"] - c["chunk_slope"] * (hi - c["hi_ref"])
+    n_sb = max(1, int(np.ceil(m * w / max(sb_cap, 1e8))))
+    n_ch = max(1, int(np.ceil(2.0 * hi * w / max(ch_cap, 1e8))))
+    # (chunk, super-batch) pairs whose reads can meet: the chunk starts below the
+    # super-batch's last read
+    q0 = 1.0 + np.arange(n_ch) * (hi / n_ch)
+    s_end = lo + (np.arange(n_sb) + 1.0) * (m / n_sb)
+    searches = int((np.add.outer(q0, -s_end) < 0).sum())
+    seed_windows = searches * 2.0 * w * hi / n_ch
+    return (pairs * c["pair_s"] + seed_windows * c["seed_window_s"] +
+            searches * (m * w / n_sb) * c["index_window_s"])
 
 
 def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
@@ -178,26 +205,11 @@ def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
     c = dict(REHEARSAL_COSTS if costs is None else costs)
     w = max(read_len - 21.0, 1.0)                 # windows per read and strand (k = 22)
 
-    def cost_driver(lo: int, hi: int) -> float:
-        m = hi - lo + 1
-        pairs = pairs_per_read * (lo + hi) / 2.0 * m / n * c["pair_scale"]
-        n_sb = max(1, int(np.ceil(m * w / c["sb_windows"])))
-        n_ch = max(1, int(np.ceil(2.0 * hi * w / c["chunk_windows"])))
-        # (chunk, super-batch) pairs whose reads can meet: the chunk starts below the
-        # super-batch's last read
-        q0 = 1.0 + np.arange(n_ch) * (hi / n_ch)
-        s_end = lo + (np.arange(n_sb) + 1.0) * (m / n_sb)
-        searched = np.add.outer(q0, -s_end) < 0
-        searches = int(searched.sum())
-        seed_windows = searches * 2.0 * w * hi / n_ch
-        return (pairs * c["pair_s"] + seed_windows * c["seed_window_s"] +
-                searches * (m * w / n_sb) * c["index_window_s"])
-
     def cost(lo: int, hi: int) -> float:
         if hi < lo:
             return 0.0
         if c.get("model") == "driver":
-            return cost_driver(lo, hi)
+            return driver_job_cost(n, read_len, pairs_per_read, lo, hi, c)
         m = hi - lo + 1
         pairs = pairs_per_read * (lo + hi) / 2.0 * m / n    # sum over b of b * ppr / n
         batches = max(1.0, m * w / batch_windows)

@@ -92,3 +92,25 @@ def test_hash_block_jobs_cover_and_balance():
     assert max(est) / min(est) < 1.02
     widths = [j["h"][1] - j["h"][0] for j in js]
     assert widths == sorted(widths, reverse=True)
+
+
+# full-size configs[4] rank jobs measured on one MI355X (profiles/r05{o,r7,p0,p7,s0,s3,s7}
+# _c4full.json): hash block -> seconds per job
+C4_FULL_RUNS = {(1, 1145091): 18.27, (3718142, 4000000): 33.69, (1, 1389603): 26.60,
+                (3744207, 4000000): 31.00, (1, 1448687): 29.02, (2513657, 2879216): 27.70,
+                (3756242, 4000000): 30.78}
+
+
+def test_driver_cost_plan_fits_full_size_runs():
+    """dist.DRIVER_COSTS (round 5's driver: super-batches x sorted query chunks) against the
+    seven full-size rank jobs measured on the GPU: every job within 11 %, and the plan it cuts
+    covers the reads in contiguous blocks with the first the widest."""
+    from canu_amd import dist
+    js = dist.hash_block_jobs(4_000_000, 8, 12_000, 36.0, 1.0, costs=dist.DRIVER_COSTS)
+    assert js[0]["h"][0] == 1 and js[-1]["h"][1] == 4_000_000
+    for a, b in zip(js, js[1:]):
+        assert b["h"][0] == a["h"][1] + 1
+    assert js[0]["h"][1] - js[0]["h"][0] == max(j["h"][1] - j["h"][0] for j in js)
+    for (lo, hi), meas in C4_FULL_RUNS.items():
+        est = dist.driver_job_cost(4_000_000, 12_000, 36.0, lo, hi)
+        assert abs(est - meas) / meas < 0.11, (lo, hi, est, meas)
