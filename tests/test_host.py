@@ -94,16 +94,18 @@ def test_hash_block_jobs_cover_and_balance():
     assert widths == sorted(widths, reverse=True)
 
 
-# full-size configs[4] rank jobs measured on one MI355X (profiles/r05{o,r7,p0,p7,s0,s3,s7}
-# _c4full.json): hash block -> seconds per job
+# full-size configs[4] rank jobs measured on one MI355X (profiles/r05{o,r7,p0,p7}_c4full.json
+# and r05s{0..7}_c4full.json): hash block -> seconds per job
 C4_FULL_RUNS = {(1, 1145091): 18.27, (3718142, 4000000): 33.69, (1, 1389603): 26.60,
-                (3744207, 4000000): 31.00, (1, 1448687): 29.02, (2513657, 2879216): 27.70,
-                (3756242, 4000000): 30.78}
+                (3744207, 4000000): 31.00, (1, 1448687): 29.02, (1448688, 2054957): 28.18,
+                (2054958, 2513656): 28.60, (2513657, 2879216): 27.70,
+                (2879217, 3217274): 28.88, (3217275, 3502307): 28.30,
+                (3502308, 3756241): 27.52, (3756242, 4000000): 30.78}
 
 
 def test_driver_cost_plan_fits_full_size_runs():
     """dist.DRIVER_COSTS (round 5's driver: super-batches x sorted query chunks) against the
-    seven full-size rank jobs measured on the GPU: every job within 11 %, and the plan it cuts
+    twelve full-size rank jobs measured on the GPU: every job within 11 %, and the plan it cuts
     covers the reads in contiguous blocks with the first the widest."""
     from canu_amd import dist
     js = dist.hash_block_jobs(4_000_000, 8, 12_000, 36.0, 1.0, costs=dist.DRIVER_COSTS)
