@@ -456,6 +456,9 @@ class Configs4Rank(Configs2):
         costs = DRIVER_COSTS if self.plan() == "r05" else None
         self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load, costs=costs)
         self.job = self.jobs[a.rank_job if self.world == 1 else self.rank]
+        if os.environ.get("CANU_C4_HBLOCK"):          # "lo-hi": one job outside the plan (A/B)
+            lo_h, hi_h = (int(x) for x in os.environ["CANU_C4_HBLOCK"].split("-"))
+            self.job = {"h": (lo_h, hi_h), "r": (1, hi_h), "est_s": None}
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world
         if self.world == 1:
