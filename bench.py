@@ -452,9 +452,13 @@ class Configs4Rank(Configs2):
         genome_len = int(n * a.read_len / a.coverage)
         plan_ranks = 8 if self.world == 1 else self.world
         load = self.HASHLOAD * (1 << self.HASHBITS) * 21
-        from canu_amd.dist import DRIVER_COSTS
+        from canu_amd.dist import DRIVER_COSTS, c4_full_plan
         costs = DRIVER_COSTS if self.plan() == "r05" else None
-        self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load, costs=costs)
+        if (self.plan() == "r05" and n == 4_000_000 and plan_ranks == 8 and
+                a.read_len == 12_000 and a.coverage == 15.0):
+            self.jobs = c4_full_plan()                 # configs[4] as run (dist.C4_FULL_PLAN_ENDS)
+        else:
+            self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load, costs=costs)
         self.job = self.jobs[a.rank_job if self.world == 1 else self.rank]
         if os.environ.get("CANU_C4_HBLOCK"):          # "lo-hi": one job outside the plan (A/B)
             lo_h, hi_h = (int(x) for x in os.environ["CANU_C4_HBLOCK"].split("-"))

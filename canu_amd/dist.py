@@ -168,6 +168,26 @@ DRIVER_COSTS = {"model": "driver", "pair_s": 0.68e-6, "pair_scale": 2.19,
                 "chunk_slope": 464.0, "hi_ref": 1.2e6}
 
 
+# configs[4]'s 8-rank plan at its real size (4M x 12 kb, 15x), as run: DRIVER_COSTS' cut with
+# the last three boundaries moved so that ranks 6 and 7 stay one super-batch below the
+# driver's packing step (rank 7's 244 k reads packed 5 super-batches, 220 k pack 4; DESIGN.md
+# configs[4]).  Every rank measured alone on one MI355X (profiles/r05s{0..4}_c4full.json,
+# r05w{5,6,7}_c4full.json): 29.0 28.2 28.6 27.7 28.9 29.4 28.1 27.2 s, 57,493,247 overlaps --
+# the same total as the unadjusted cut's eight jobs.  Hash-block upper ends:
+C4_FULL_PLAN_ENDS = (1448687, 2054957, 2513656, 2879216, 3217274, 3515000, 3780000, 4000000)
+
+
+def c4_full_plan() -> list[dict]:
+    """The measured 8-rank plan for configs[4] at 4M reads (C4_FULL_PLAN_ENDS), in
+    hash_block_jobs' format."""
+    jobs, lo = [], 1
+    for hi in C4_FULL_PLAN_ENDS:
+        jobs.append({"h": (lo, hi), "r": (1, hi), "est_s": round(driver_job_cost(
+            4_000_000, 12_000, 36.0, lo, hi), 2)})
+        lo = hi + 1
+    return jobs
+
+
 def driver_job_cost(n: int, read_len: float, pairs_per_read: float, lo: int, hi: int,
                     c: dict | None = None) -> float:
     """Modelled seconds of one `-h lo-hi -r 1-hi` job on round 5's driver (DRIVER_COSTS):

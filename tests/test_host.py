@@ -95,17 +95,18 @@ def test_hash_block_jobs_cover_and_balance():
 
 
 # full-size configs[4] rank jobs measured on one MI355X (profiles/r05{o,r7,p0,p7}_c4full.json
-# and r05s{0..7}_c4full.json): hash block -> seconds per job
+# r05s{0..7}_c4full.json and r05w{5,6,7}_c4full.json): hash block -> seconds per job
 C4_FULL_RUNS = {(1, 1145091): 18.27, (3718142, 4000000): 33.69, (1, 1389603): 26.60,
                 (3744207, 4000000): 31.00, (1, 1448687): 29.02, (1448688, 2054957): 28.18,
                 (2054958, 2513656): 28.60, (2513657, 2879216): 27.70,
                 (2879217, 3217274): 28.88, (3217275, 3502307): 28.30,
-                (3502308, 3756241): 27.52, (3756242, 4000000): 30.78}
+                (3502308, 3756241): 27.52, (3756242, 4000000): 30.78,
+                (3217275, 3515000): 29.37, (3515001, 3780000): 28.05, (3780001, 4000000): 27.25}
 
 
 def test_driver_cost_plan_fits_full_size_runs():
     """dist.DRIVER_COSTS (round 5's driver: super-batches x sorted query chunks) against the
-    twelve full-size rank jobs measured on the GPU: every job within 11 %, and the plan it cuts
+    fifteen full-size rank jobs measured on the GPU: every job within 11 %, and the plan it cuts
     covers the reads in contiguous blocks with the first the widest."""
     from canu_amd import dist
     js = dist.hash_block_jobs(4_000_000, 8, 12_000, 36.0, 1.0, costs=dist.DRIVER_COSTS)
@@ -116,3 +117,19 @@ def test_driver_cost_plan_fits_full_size_runs():
     for (lo, hi), meas in C4_FULL_RUNS.items():
         est = dist.driver_job_cost(4_000_000, 12_000, 36.0, lo, hi)
         assert abs(est - meas) / meas < 0.11, (lo, hi, est, meas)
+
+
+def test_c4_full_plan_covers_the_reads():
+    """The measured configs[4] plan (dist.C4_FULL_PLAN_ENDS): eight contiguous `-h lo-hi -r 1-hi`
+    blocks over 1..4M, and bench.py's configs4-rank workload runs it at that size."""
+    from canu_amd import dist
+    js = dist.c4_full_plan()
+    assert len(js) == 8 and js[0]["h"][0] == 1 and js[-1]["h"][1] == 4_000_000
+    for a, b in zip(js, js[1:]):
+        assert b["h"][0] == a["h"][1] + 1
+    for j in js:
+        assert j["r"] == (1, j["h"][1])
+    import bench
+    w = bench.Configs4Rank(bench.parse_args(["--workload", "configs4-rank", "--reads",
+                                             "4000000"]), 0, 1, None)
+    assert w.plan() == "r05"

@@ -1,5 +1,5 @@
 # configs[4] at its real size on one GPU: one rank job of the 8-GPU plan for 4M x 12 kb ONT
-# reads (dist.hash_block_jobs with round 5's driver costs, dist.DRIVER_COSTS: rank 0 is
+# reads (dist.c4_full_plan: the driver-cost cut as measured, rank 0 is
 # -h 1-1448687 -r 1-1448687; CANU_C4_PLAN=r02 gives the rehearsal-cost plan, rank 0
 # -h 1-1145091), canu's --hashbits 23 --hashload 0.75, the job's reads generated before GPU
 # init.  One timed job (no warm-up: its first-use allocations are inside it, OVL_TIMING shows
