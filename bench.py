@@ -128,6 +128,11 @@ def main() -> None:
 
     job.setup(OicParameters, OverlapInCore)
     setup_s = time.time() - t_setup
+    # what the setup leaves on the device before the first job plans its buffers from free
+    # HBM: torch should hold nothing (the staged bases are freed), the library its read store
+    free_b, tot_b = torch.cuda.mem_get_info(dev)
+    setup_hbm = {"device_free_gb": round(free_b / 1e9, 2), "device_total_gb": round(tot_b / 1e9, 2),
+                 "torch_reserved_gb": round(torch.cuda.memory_reserved(dev) / 1e9, 3)}
     oic = job.oic
 
     for _ in range(args.warmup):
@@ -202,10 +207,12 @@ def main() -> None:
             "counters": {k: st.get(k) for k in (
                 "total_overlaps", "kmer_hits_with_olap", "kmer_hits_without_olap",
                 "kmer_hits_skipped", "multi_overlaps", "contained_overlaps", "dovetail_overlaps",
-                "hash_batches", "super_batches", "query_chunks")},
+                "hash_batches", "super_batches", "query_chunks", "sq_declined",
+                "find_releases")},
             "pair_kernels": {"staged": st.get("staged_pairs"), "long": st.get("long_pairs"),
                              "generic": st.get("generic_pairs")},
             "setup_s": round(setup_s, 1),
+            "setup_hbm": setup_hbm,
             "roofline": roof,
             "probe_roofline": probe_roof,
             "traffic_source": traffic_note,
@@ -273,6 +280,8 @@ class Configs2:
         self.oic = OverlapInCore(self.P, device=self.dev.index)
         self.oic.load_reads_device(1, bases.data_ptr(), self._keep[1].data_ptr(), lengths)
         torch.cuda.synchronize()
+        self._keep = bases = None      # the library packed its own copy (load_common)
+        torch.cuda.empty_cache()
         self.q_lo, self.q_hi = query_shards(n, self.world)[self.rank]
 
     # each rank indexes reads q_lo..n only: its queries' targets all have larger IDs
@@ -443,13 +452,11 @@ class Configs4Rank(Configs2):
             return e
         return "r05" if self.args.reads >= 4_000_000 else "r02"
 
-    def generate(self):
-        """This rank's slice of the read set, on the host before any GPU call (the
-        generator's worker pool is forked here)."""
-        from canu_amd.synth import synth_reads_parallel
+    def plan_jobs(self):
+        """The plan's jobs and this rank's job (self.jobs, self.job), from the workload's
+        parameters alone (no reads, no GPU)."""
         from canu_amd.dist import hash_block_jobs
         a, n = self.args, self.args.reads
-        genome_len = int(n * a.read_len / a.coverage)
         plan_ranks = 8 if self.world == 1 else self.world
         load = self.HASHLOAD * (1 << self.HASHBITS) * 21
         from canu_amd.dist import DRIVER_COSTS, c4_full_plan
@@ -463,6 +470,15 @@ class Configs4Rank(Configs2):
         if os.environ.get("CANU_C4_HBLOCK"):          # "lo-hi": one job outside the plan (A/B)
             lo_h, hi_h = (int(x) for x in os.environ["CANU_C4_HBLOCK"].split("-"))
             self.job = {"h": (lo_h, hi_h), "r": (1, hi_h), "est_s": None}
+        return self.jobs, self.job
+
+    def generate(self):
+        """This rank's slice of the read set, on the host before any GPU call (the
+        generator's worker pool is forked here)."""
+        from canu_amd.synth import synth_reads_parallel
+        a, n = self.args, self.args.reads
+        genome_len = int(n * a.read_len / a.coverage)
+        self.plan_jobs()
         lo = n * self.rank // self.world
         hi = n * (self.rank + 1) // self.world
         if self.world == 1:
@@ -493,15 +509,19 @@ class Configs4Rank(Configs2):
 
     def setup(self, OicParameters, OverlapInCore):
         import torch
-        from canu_amd.dist import gather_read_store
+        from canu_amd.dist import gather_read_prefix
         a, n = self.args, self.args.reads
         part, self._part = self._part, None
         if self.world == 1:
             bases = torch.from_numpy(part.bases).to(self.dev)
             lengths = part.lengths
         else:
-            bases, lengths = gather_read_store(torch.from_numpy(part.bases).to(self.dev),
-                                               part.lengths, self.dist, self.dev)
+            # each rank receives only reads 1..max(h, r) -- what its job touches, as the
+            # one-GPU runs load -- point to point from the ranks that generated them
+            need = max(self.job["h"][1], self.job["r"][1])
+            local = torch.from_numpy(part.bases).to(self.dev)
+            bases, lengths = gather_read_prefix(local, part.lengths, need, self.dist, self.dev)
+            del local
         del part
         offsets = np.zeros(lengths.shape[0], dtype=np.uint64)
         offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
@@ -519,6 +539,11 @@ class Configs4Rank(Configs2):
         self.oic = OverlapInCore(self.P, device=self.dev.index)
         self.oic.load_reads_device(1, bases.data_ptr(), self._keep[1].data_ptr(), lengths)
         torch.cuda.synchronize()
+        # the library packed its own 2-bit copy (load_common) and never reads these bases
+        # again: the 1-B-per-base staging (48 GB at 4M x 12 kb) goes back to the device
+        # before the driver sizes its super-batches and query chunks from free HBM
+        self._keep = bases = None
+        torch.cuda.empty_cache()
 
     def step(self) -> int:
         return self.oic.overlap_driver(store_num_reads=self.n)
@@ -750,8 +775,8 @@ def side_runs(timeout_s: int = 300) -> dict:
                      the MHAP jar unpinned)"""
     import subprocess
     keep4 = ("value", "unit", "ms_per_step", "breakdown_ms", "pairs", "pair_kernels",
-             "roofline", "probe_roofline", "traffic_source", "config", "setup_s", "parity",
-             "counters")
+             "roofline", "probe_roofline", "traffic_source", "config", "setup_s", "setup_hbm",
+             "parity", "counters")
     keep3 = ("value", "unit", "ms_per_step", "breakdown_ms", "config", "setup_s", "roofline",
              "candidates_per_step", "overlaps_per_step", "parity")
     runs = {"configs4_rank": ([sys.executable, os.path.join(ROOT, "bench.py"), "--workload",

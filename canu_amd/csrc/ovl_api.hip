@@ -522,8 +522,16 @@ int ovl_import_index(ovl_ctx *c, const ovl_index_desc *in) {
       in->table_bytes != (sizeof(TabEntry) << in->tab_bits) || in->occ_bytes != 8ull * in->records ||
       in->read_flags_bytes != 4ull * in->nreads || !in->table || (in->records && !in->occ) ||
       !in->read_flags || (in->bloom_bytes && (!in->bloom ||
+      in->bloom_w > 6 ||
       in->bloom_bytes != 8ull * ((1ull << (in->tab_bits - in->slice_bits)) << in->bloom_w))))
     return fail(OVL_ERR_BAD_PARAM, "inconsistent index descriptor");
+  // the limits build_index keeps (and the table / probe kernels assume): 32-bit run offsets,
+  // a slice (and, with the filter, its filter region) within one wave's 64 KB of LDS
+  if (in->records >= 0xFFFFFFF0ull || in->slice_bits < 1 || (16ull << in->slice_bits) > 65536 ||
+      (in->bloom_bytes && (16ull << in->slice_bits) + (8ull << in->bloom_w) > 65536))
+    return fail(OVL_ERR_BAD_PARAM, "index descriptor past the build's limits (records %llu, "
+                "slice 2^%u, filter 2^%u words)", (unsigned long long)in->records,
+                in->slice_bits, in->bloom_w);
   if (in->end_iid < in->bgn_iid || in->bgn_iid < c->first_iid ||
       in->end_iid > c->first_iid + c->nreads - 1)
     return fail(OVL_ERR_BAD_PARAM, "index of hash reads %u-%u outside the loaded reads",
@@ -1344,7 +1352,18 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
   const uint64_t entry_limit =
       (uint64_t)(L->max_hash_load * (double)(1ull << L->hash_mask_bits) * (double)ENTRIES_PER_BUCKET);
   const bool load_may_cut = windows >= entry_limit && e > bgn;
+  auto too_big = [&](uint64_t wcap) {
+    return fail(OVL_ERR_UNSUPPORTED, "hash batch %u-%u holds %llu k-mers, more than one index "
+                "on this GPU (%llu: %.1f GB free or held by this context, %.1f GB kept for "
+                "the search buffers); lower --hashstrings", bgn, e,
+                (unsigned long long)windows, (unsigned long long)wcap, g_cap_free / 1e9,
+                g_cap_reserve / 1e9);
+  };
   if (boundaries_only && !load_may_cut) {
+    // the driver's first phase builds nothing here, but a batch no index can hold would
+    // become a super-batch of its own and fail later with a bare out-of-memory
+    const uint64_t wcap = index_window_cap(c);
+    if (windows > wcap) return too_big(wcap);
     *last_iid = e;
     return OVL_OK;
   }
@@ -1366,12 +1385,7 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
                                                             1u << 20));
   for (;;) {
     const uint64_t wcap = index_window_cap(c);
-    if (!load_may_cut && windows > wcap)
-      return fail(OVL_ERR_UNSUPPORTED, "hash batch %u-%u holds %llu k-mers, more than one index "
-                  "on this GPU (%llu: %.1f GB free or held by this context, %.1f GB kept for "
-                  "the search buffers); lower --hashstrings", bgn, e,
-                  (unsigned long long)windows, (unsigned long long)wcap, g_cap_free / 1e9,
-                  g_cap_reserve / 1e9);
+    if (!load_may_cut && windows > wcap) return too_big(wcap);
     const uint64_t tw = std::min(target, wcap);
     uint32_t eb = e;
     if (tw < windows) {
@@ -1389,6 +1403,7 @@ static int build_batch_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, const ovl_ha
     if ((rc = build_index(c, bgn, eb, bloom, !boundaries_only)) == OVL_ERR_OOM) {
       // the previous batch's search buffers make room (the next search grows them again)
       release_find_buffers(c);
+      c->stats.find_releases++;
       rc = build_index(c, bgn, eb, bloom, !boundaries_only);
     }
     if (rc) return rc;
@@ -1579,6 +1594,10 @@ static int sq_prepare(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, u
   const uint64_t avail = fr + sq_held_bytes(c);
   if (c->sticky_budgets ? need + (4ull << 30) > avail : need > avail / 2) {
     sq_release(c);
+    c->stats.sq_declined++;
+    if (getenv("OVL_TIMING"))
+      fprintf(stderr, "OVL_TIMING sorted query windows declined: %.1f GB needed, %.1f GB "
+              "available -> random-lookup probes\n", need / 1e9, avail / 1e9);
     return OVL_OK;
   }
   hipStream_t s = c->stream;
@@ -3074,6 +3093,7 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     const bool bloom = !c->sq.on || sq_bloom();
     if ((rc = build_index(c, hb, he, bloom)) == OVL_ERR_OOM) {
       release_find_buffers(c);
+      c->stats.find_releases++;
       rc = build_index(c, hb, he, bloom);
     }
     return rc;

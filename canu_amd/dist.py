@@ -120,6 +120,77 @@ def gather_read_store(bases_local, lengths_local: np.ndarray, dist, device):
     return bases, lengths
 
 
+def gather_read_prefix(bases_local, lengths_local: np.ndarray, need: int, dist, device):
+    """configs[4]'s setup exchange: every rank generated (or read) one slice of the store
+    (rank order = read order), and rank r needs only reads 1..need_r -- the reads its
+    `-h lo-hi -r 1-hi` job touches (a job never reads past its hash block's end).  Each slice
+    goes point to point to the ranks that need part of it, straight into their buffers
+    (RCCL send / recv over xGMI; gloo stages device tensors through host memory): no rank
+    holds reads it does not search, and nothing but the result stays allocated.
+
+    bases_local: 1-D uint8 torch tensor; lengths_local: uint32 numpy array; need: this rank's
+    read count from read 1 (clipped to the store).  Returns (bases, lengths) of reads
+    1..need: a uint8 tensor on `device` and a uint32 numpy array."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    cpu_stage = dist.get_backend() == "gloo" and bases_local.is_cuda
+    meta_dev = torch.device("cpu") if dist.get_backend() == "gloo" else device
+    m = torch.tensor([lengths_local.shape[0], need], dtype=torch.int64, device=meta_dev)
+    allm = [torch.zeros_like(m) for _ in range(world)]
+    dist.all_gather(allm, m)
+    nls = [int(x[0]) for x in allm]
+    needs = [int(x[1]) for x in allm]
+    total = sum(nls)
+    # every rank gets every read's length (4 B per read): the byte ranges follow from them
+    lb = torch.zeros(max(nls), dtype=torch.int64, device=meta_dev)
+    lb[:nls[rank]] = torch.from_numpy(lengths_local.astype(np.int64))
+    gl = [torch.empty_like(lb) for _ in range(world)]
+    dist.all_gather(gl, lb)
+    lengths = torch.cat([g[:k] for g, k in zip(gl, nls)]).cpu().numpy().astype(np.uint32)
+    del gl, lb
+    cum = np.zeros(total + 1, dtype=np.uint64)
+    cum[1:] = np.cumsum(lengths, dtype=np.uint64)
+    first = np.zeros(world + 1, dtype=np.int64)
+    first[1:] = np.cumsum(nls)
+    needs = [min(max(x, 0), total) for x in needs]
+
+    def part(s, r):            # bytes of slice s that rank r needs: [0, b) of s's bases
+        end = min(int(first[s + 1]), needs[r])
+        return int(cum[end] - cum[first[s]]) if end > first[s] else 0
+
+    mine = needs[rank]
+    out = torch.empty(int(cum[mine]), dtype=torch.uint8, device=device)
+    ops, staged = [], []
+    b = part(rank, rank)
+    if b:
+        out[int(cum[first[rank]]):int(cum[first[rank]]) + b].copy_(bases_local[:b])
+    for r in range(world):
+        b = part(rank, r)
+        if r != rank and b:
+            t = bases_local[:b]
+            if cpu_stage:
+                t = t.cpu()
+            ops.append(dist.P2POp(dist.isend, t, r))
+    for s in range(world):
+        b = part(s, rank)
+        if s != rank and b:
+            o = int(cum[first[s]])
+            dst = out[o:o + b]
+            if cpu_stage:
+                h = torch.empty(b, dtype=torch.uint8)
+                staged.append((dst, h))
+                dst = h
+            ops.append(dist.P2POp(dist.irecv, dst, s))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for dst, h in staged:
+        dst.copy_(h)
+    if out.is_cuda:
+        torch.cuda.synchronize(device)
+    return out, lengths[:mine]
+
+
 def read_slices(n: int, world: int) -> list[tuple[int, int]]:
     """[lo, hi) of the reads rank r generates / sketches: n * r // world .. n * (r+1) // world."""
     return [(n * r // world, n * (r + 1) // world) for r in range(world)]
@@ -300,6 +371,19 @@ def _agree(ok: bool, dist, dev) -> bool:
     return bool(t.item())
 
 
+def _first_failed(ok: bool, dist, dev):
+    """The lowest rank whose ok flag is False (None when every rank succeeded): one MIN
+    all-reduce of (rank if failed else world), so every rank names the same failing rank."""
+    if not dist:
+        return None if ok else 0
+    import torch
+    world = dist.get_world_size()
+    t = torch.tensor([world if ok else dist.get_rank()], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    v = int(t.item())
+    return None if v >= world else v
+
+
 def share_index(src, dsts, dist, dev, src_rank: int = 0):
     """Give every rank the index the context `src` built on rank `src_rank`: its buffers
     (ovl_export_index) are copied into torch tensors, broadcast over the process group
@@ -360,6 +444,8 @@ def share_index(src, dsts, dist, dev, src_rank: int = 0):
         err = e
     torch.cuda.synchronize(dev)
     del bufs
-    if not _agree(err is None, dist, dev):
-        raise RuntimeError(f"share_index: import failed on rank {rank}: {err}")
+    bad = _first_failed(err is None, dist, dev)
+    if bad is not None:
+        raise RuntimeError(f"share_index: import failed on rank {bad}"
+                           + (f": {err}" if bad == rank else " (its log has the error)"))
     return sum(sizes.values())

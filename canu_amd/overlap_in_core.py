@@ -64,11 +64,12 @@ class _Stats(ctypes.Structure):
          ("generic_waves", ctypes.c_uint32), ("stage_len", ctypes.c_uint32),
          ("long_stage_len", ctypes.c_uint32), ("seed_nodes", ctypes.c_uint64),
          ("probe_sorted_launches", ctypes.c_uint32), ("sq_resorted", ctypes.c_uint32),
-         ("query_chunks", ctypes.c_uint32), ("super_batches", ctypes.c_uint32)]
+         ("query_chunks", ctypes.c_uint32), ("super_batches", ctypes.c_uint32),
+         ("sq_declined", ctypes.c_uint32), ("find_releases", ctypes.c_uint32)]
 
 
 class _IndexDesc(ctypes.Structure):
-    """ovl_index_desc (include/canu_ovl.h, ABI 7): a built index as device buffers."""
+    """ovl_index_desc (include/canu_ovl.h, ABI 7+): a built index as device buffers."""
     _fields_ = [(n, ctypes.c_uint32) for n in (
         "bgn_iid", "end_iid", "first_iid", "nreads", "kmer_len", "tab_bits", "slice_bits",
         "bloom_w", "hash_lib_lo", "hash_lib_hi")] + \
@@ -106,7 +107,7 @@ EXPORTS = ["ovl_params_init", "ovl_params_finalize", "ovl_ctx_create", "ovl_ctx_
 _lib = None
 
 
-ABI_VERSION = 7          # OVL_ABI_VERSION of include/canu_ovl.h
+ABI_VERSION = 8          # OVL_ABI_VERSION of include/canu_ovl.h
 
 
 def load_library(path: str | None = None):

@@ -191,8 +191,17 @@ def synth_reads_parallel(n_reads: int, read_len: int, genome_len: int, error_rat
     pieces = max(workers * 4, 1)
     cuts = [(lo + (hi - lo) * i // pieces, lo + (hi - lo) * (i + 1) // pieces)
             for i in range(pieces)]
-    with mp.get_context("fork").Pool(workers) as pool:
+    # close + join (not the context manager's terminate): the workers exit on their own, so
+    # no SIGTERM reaches them (a profiler's inherited signal handler logs one as an abort)
+    pool = mp.get_context("fork").Pool(workers)
+    try:
         parts = pool.map(_par_slice, cuts)
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     _PAR.clear()
     return concat_read_sets(parts, first_iid=1 + lo)
 

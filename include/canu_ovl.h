@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 7
+#define OVL_ABI_VERSION 8
 
 typedef enum {
   OVL_OK               =  0,
@@ -245,6 +245,12 @@ typedef struct {
                                       whole -r range at once; ABI 7) */
   uint32_t super_batches;          /* indexes the last driver run searched: consecutive hash
                                       batches joined (0: batch by batch, as with -l; ABI 7) */
+  uint32_t sq_declined;            /* searches that asked for sorted query windows and fell
+                                      back to random-lookup probes: the windows did not fit
+                                      beside the buffers (ABI 8) */
+  uint32_t find_releases;          /* search buffers released because an index build ran out
+                                      of memory (the next search allocates them again; a
+                                      chunk's sorted windows go with them; ABI 8) */
 } ovl_stats;
 
 int         ovl_get_stats(ovl_ctx *ctx, ovl_stats *out);

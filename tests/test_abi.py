@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(built):
 
 
 def test_abi_version(built):
-    assert oic.load_library().ovl_abi_version() == 7
+    assert oic.load_library().ovl_abi_version() == 8
 
 
 def test_driver_defaults_match_reference(built):
@@ -137,13 +137,15 @@ def test_struct_layouts_match_header(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text(
         '#include <stddef.h>\n#include <stdio.h>\n#include "canu_ovl.h"\n'
-        'int main(void) { printf("%zu %zu %zu %zu %zu\\n", sizeof(ovl_stats), '
+        'int main(void) { printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(ovl_stats), '
         'offsetof(ovl_stats, sq_resorted), offsetof(ovl_stats, query_chunks), '
+        'offsetof(ovl_stats, find_releases), '
         'sizeof(ovl_index_desc), offsetof(ovl_index_desc, read_flags_bytes)); return 0; }\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-std=c99", "-I", inc, str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
                                           check=True).stdout.split()]
     assert got == [ctypes.sizeof(oic._Stats), oic._Stats.sq_resorted.offset,
-                   oic._Stats.query_chunks.offset, ctypes.sizeof(oic._IndexDesc),
+                   oic._Stats.query_chunks.offset, oic._Stats.find_releases.offset,
+                   ctypes.sizeof(oic._IndexDesc),
                    oic._IndexDesc.read_flags_bytes.offset]

@@ -117,3 +117,61 @@ def test_gloo_world2_mhap_sketch_gather_and_shards():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert ok_rows and ok_union and n > 0
+
+
+def _prefix_worker(rank, world, port, q):
+    """configs[4]'s setup exchange (dist.gather_read_prefix): rank r gets reads 1..need_r
+    only -- the reads its `-h lo-hi -r 1-hi` job touches -- point to point from the ranks
+    that generated them, and holds nothing more; and dist._first_failed names the same
+    failing rank on every rank."""
+    import torch
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from canu_amd.dist import _first_failed, gather_read_prefix, read_slices
+    from canu_amd.synth import random_genome, synth_reads
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, L, G = 61, 900, 8000
+    genome = random_genome(np.random.default_rng(7), G)
+    lo, hi = read_slices(n, world)[rank]
+    part = synth_reads(n, L, G, 0.02, seed=7, genome=genome, read_range=(lo, hi),
+                       len_jitter=0.3)
+    # a hash-block plan's needs: increasing with the rank, the last rank the whole store
+    needs = [int(n * (r + 1) ** 2 // world ** 2) for r in range(world)]
+    needs[0] = max(needs[0], 1)
+    bases, lengths = gather_read_prefix(torch.from_numpy(part.bases), part.lengths,
+                                        needs[rank], dist, torch.device("cpu"))
+    whole = synth_reads(n, L, G, 0.02, seed=7, genome=genome, len_jitter=0.3)
+    m = needs[rank]
+    ok = (lengths.shape[0] == m and np.array_equal(lengths, whole.lengths[:m]) and
+          bases.numel() == int(whole.lengths[:m].sum()) and
+          np.array_equal(bases.numpy(), whole.bases[:bases.numel()]))
+    fail_rank = world - 1
+    named = _first_failed(rank != fail_rank, dist, torch.device("cpu"))
+    none = _first_failed(True, dist, torch.device("cpu"))
+    res = [None] * world
+    dist.all_gather_object(res, (ok, named, none))
+    if rank == 0:
+        q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_read_prefix_per_rank(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prefix_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for ok, named, none in res:
+        assert ok
+        assert named == world - 1 and none is None

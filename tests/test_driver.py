@@ -221,6 +221,25 @@ def test_gpu_driver_load_cut_within_window_cap(built, monkeypatch):
         run()
 
 
+@pytest.mark.gpu
+def test_gpu_driver_batch_past_index_cap_fails_with_its_reason(built, monkeypatch):
+    """Super-batch mode (the default): a hash batch the table load cannot cut but no index on
+    this GPU could hold (OVL_TEST_INDEX_WINDOW_CAP stands in for the HBM cap) is refused in
+    the driver's first phase with the batch-by-batch path's message, not a bare out-of-memory
+    later."""
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore, OvlError
+    rs = synth_reads(n_reads=60, read_len=3000, genome_len=30_000, error_rate=0.02, seed=27)
+    O = OicParameters(Kmer_Len=22, maxErate=0.06, Min_Olap_Len=500, Hash_Mask_Bits=22,
+                      Max_Hash_Load=0.75, Max_Hash_Strings=30, Num_PThreads=4).finalize()
+    monkeypatch.setenv("OVL_TEST_INDEX_WINDOW_CAP", "20000")
+    oic = OverlapInCore(O, device=0)
+    try:
+        with pytest.raises(OvlError, match="lower --hashstrings"):
+            oic.run_driver(rs)
+    finally:
+        oic.close()
+
+
 def _lib_case():
     """Reads spread over three gkpStore libraries, -H 1-2 (hash libraries 1 and 2 only) and
     -R 2-3 (search from libraries 2 and 3 only), small hash batches (Build_Hash_Index.C:

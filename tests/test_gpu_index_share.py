@@ -123,3 +123,48 @@ def test_gpu_share_index_through_torch_buffers(built):
     assert np.array_equal(got_b, got_a)
     for key in STAT_KEYS:
         assert st_b[key] == st_a[key], key
+
+
+@pytest.mark.gpu
+def test_gpu_import_rejects_descriptor_past_build_limits(built):
+    """A descriptor the build could not have produced (a corrupted broadcast, another build)
+    is refused before any kernel reads it: a filter of more than 2^6 words per fine bucket,
+    2^32 or more occurrence records (the table's run offsets are 32-bit), or a slice whose
+    wave would not fit 64 KB of LDS."""
+    import ctypes
+    from canu_amd.overlap_in_core import OicParameters, OverlapInCore, OvlError
+    rs = synth_reads(n_reads=120, read_len=3000, genome_len=40_000, error_rate=0.02, seed=44)
+    O = OicParameters(Kmer_Len=22, maxErate=0.06, Min_Olap_Len=500,
+                      Max_Hash_Strings=60).finalize()
+    a = OverlapInCore(O, device=0)
+    b = OverlapInCore(O, device=0)
+    try:
+        a.load_reads(rs)
+        b.load_reads(rs)
+        assert a.build_hash_batch(1, rs.nreads) == 60
+        good = a.export_index()
+        assert good.bloom_bytes > 0
+
+        def bad(**kw):
+            d = type(good)()
+            ctypes.memmove(ctypes.addressof(d), ctypes.addressof(good), ctypes.sizeof(good))
+            for f, v in kw.items():
+                setattr(d, f, v)
+            return d
+
+        nfine = good.table_bytes // 16 >> good.slice_bits
+        cases = [
+            bad(bloom_w=7, bloom_bytes=8 * (nfine << 7)),
+            bad(records=1 << 32, occ_bytes=8 << 32),
+            bad(slice_bits=13, bloom_bytes=8 * ((good.table_bytes // 16 >> 13) << good.bloom_w)),
+        ]
+        for d in cases:
+            with pytest.raises(OvlError, match="inconsistent index descriptor|past the build's"):
+                b.import_index(d)
+        b.import_index(good)                 # the real one still imports and searches
+        got_b = b.fetch(b.find_overlaps(1, rs.nreads))
+        got_a = a.fetch(a.find_overlaps(1, rs.nreads))
+    finally:
+        a.close()
+        b.close()
+    assert np.array_equal(got_b, got_a)

@@ -119,7 +119,7 @@ def test_driver_cost_plan_fits_full_size_runs():
         assert abs(est - meas) / meas < 0.11, (lo, hi, est, meas)
 
 
-def test_c4_full_plan_covers_the_reads():
+def test_c4_full_plan_covers_the_reads(monkeypatch):
     """The measured configs[4] plan (dist.C4_FULL_PLAN_ENDS): eight contiguous `-h lo-hi -r 1-hi`
     blocks over 1..4M, and bench.py's configs4-rank workload runs it at that size."""
     from canu_amd import dist
@@ -130,6 +130,16 @@ def test_c4_full_plan_covers_the_reads():
     for j in js:
         assert j["r"] == (1, j["h"][1])
     import bench
+    monkeypatch.delenv("CANU_C4_PLAN", raising=False)
+    monkeypatch.delenv("CANU_C4_HBLOCK", raising=False)
+    for r in range(8):
+        w = bench.Configs4Rank(bench.parse_args(["--workload", "configs4-rank", "--reads",
+                                                 "4000000", "--rank-job", str(r)]), 0, 1, None)
+        assert w.plan() == "r05"
+        jobs, job = w.plan_jobs()            # what generate() runs, without reads or a GPU
+        assert [(j["h"], j["r"]) for j in jobs] == [(j["h"], j["r"]) for j in js]
+        assert (job["h"], job["r"]) == (js[r]["h"], js[r]["r"])
+    # at N ranks rank r runs job r of an N-job plan
     w = bench.Configs4Rank(bench.parse_args(["--workload", "configs4-rank", "--reads",
-                                             "4000000"]), 0, 1, None)
-    assert w.plan() == "r05"
+                                             "4000000"]), 7, 8, None)
+    assert w.plan_jobs()[1]["h"] == js[7]["h"]
