@@ -440,32 +440,29 @@ class Configs4Rank(Configs2):
                 "coverage": a.coverage, "read_error": a.read_error, "seed": a.seed, "k": a.k,
                 "maxerate": float(np.float32(a.maxerate)), "minlength": a.minlength,
                 "rank_job": a.rank_job,
-                **({"plan": "r05"} if self.plan() == "r05" else {})}
+                **({"plan": "r06"} if self.plan() == "r06" else {})}
 
     def plan(self) -> str:
-        """Which cost model cuts the 8-rank plan: "r05" (dist.DRIVER_COSTS, fitted to round
-        5's full-size rank jobs) at the full 4M-read size, "r02" (the rehearsal costs, the
-        plan the committed 20k / 500k reference digests pin) below it; CANU_C4_PLAN
-        overrides."""
+        """Which cost model cuts the rank plan: "r06" (dist.DRIVER6: the driver's own
+        super-batch / query-chunk planning replayed per job, round 6) at the full 4M-read
+        size, "r02" (the rehearsal costs, the plan the committed 20k / 500k reference digests
+        pin) below it; CANU_C4_PLAN overrides."""
         e = os.environ.get("CANU_C4_PLAN")
-        if e in ("r02", "r05"):
+        if e in ("r02", "r06"):
             return e
-        return "r05" if self.args.reads >= 4_000_000 else "r02"
+        return "r06" if self.args.reads >= 4_000_000 else "r02"
 
     def plan_jobs(self):
         """The plan's jobs and this rank's job (self.jobs, self.job), from the workload's
         parameters alone (no reads, no GPU)."""
-        from canu_amd.dist import hash_block_jobs
+        from canu_amd.dist import c4_plan, hash_block_jobs
         a, n = self.args, self.args.reads
         plan_ranks = 8 if self.world == 1 else self.world
         load = self.HASHLOAD * (1 << self.HASHBITS) * 21
-        from canu_amd.dist import DRIVER_COSTS, c4_full_plan
-        costs = DRIVER_COSTS if self.plan() == "r05" else None
-        if (self.plan() == "r05" and n == 4_000_000 and plan_ranks == 8 and
-                a.read_len == 12_000 and a.coverage == 15.0):
-            self.jobs = c4_full_plan()                 # configs[4] as run (dist.C4_FULL_PLAN_ENDS)
+        if self.plan() == "r06":
+            self.jobs = c4_plan(n, plan_ranks, a.read_len)
         else:
-            self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load, costs=costs)
+            self.jobs = hash_block_jobs(n, plan_ranks, a.read_len, 36.0, 3.0 * load)
         self.job = self.jobs[a.rank_job if self.world == 1 else self.rank]
         if os.environ.get("CANU_C4_HBLOCK"):          # "lo-hi": one job outside the plan (A/B)
             lo_h, hi_h = (int(x) for x in os.environ["CANU_C4_HBLOCK"].split("-"))

@@ -2361,6 +2361,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         HIPC(hipEventRecord(c->ev[4], s));           // the probe step: seed-phase time
         HIPC(hipMemsetAsync(d_probe.p, 0, 8ull * wlim, s));
         HIPC(hipMemsetAsync(Q.uflags.p + R.u0, 0, 4ull * (ue - R.u0), s));
+        HIPC(hipMemsetAsync(Q.uhits.p + R.u0, 0, 4ull * (ue - R.u0), s));
         SqProbeArgs SA;
         SA.X = index_dev(c);
         if (c->bloom_ok && sq_bloom()) {        // the filter in front of the table
@@ -2378,6 +2379,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         SA.k = k;
         SA.out = d_probe.p;
         SA.unit_flags = Q.uflags.p + R.u0;
+        SA.unit_hits = Q.uhits.p + R.u0;
         // the kernel alone is timed (the records' zeroing and the unit hit counts around it
         // are not the probe's bytes)
         HIPC(hipEventRecord(c->ev[2], s));
@@ -2385,8 +2387,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         HIPC(hipEventRecord(c->ev[3], s));
         n_probe_launch++;
         n_probe_sorted++;
-        hipLaunchKernelGGL(k_sq_unit_hits, dim3((ue - R.u0 + 3) / 4), dim3(256), 0, s, d_probe.p,
-                           Q.dwbase.p + R.wb0, ue - R.u0, Q.uhits.p + R.u0);
         HIPC(hipGetLastError());
         HIPC(hipEventRecord(c->ev[5], s));
         sq_uh.resize(ue - R.u0);
@@ -2397,7 +2397,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
         (void)hipEventElapsedTime(&tstep, c->ev[4], c->ev[5]);
         ms_probe += t;
-        ms_probe_rest += tstep > t ? tstep - t : 0.f;  // zeroing + unit hit counts
+        ms_probe_rest += tstep > t ? tstep - t : 0.f;  // the records' zeroing
         // algorithmic bytes: the sorted windows (8-B key + 4-B id), and the table and its
         // filter read once each -- or, when they are larger than the run (a full-size
         // configs[4] super-batch's 68.7 GB table against a run of 2^29 windows), at most one
@@ -3054,7 +3054,9 @@ int ovl_overlap_driver(ovl_ctx *c, const ovl_driver_params *d, uint64_t *n_out) 
     }
     return w;
   };
-  uint64_t sb_cap = index_window_cap(c) * 11 / 20;
+  uint64_t sb_pct = 55;
+  if (const char *e = getenv("OVL_SB_PCT")) sb_pct = std::min<uint64_t>(95, std::max(5, atoi(e)));
+  uint64_t sb_cap = index_window_cap(c) * sb_pct / 100;
   if (const char *e = getenv("OVL_SB_WINDOWS")) sb_cap = std::min<uint64_t>(sb_cap, strtoull(e, nullptr, 10));
   sb_cap = std::max<uint64_t>(sb_cap, 1);
   std::vector<std::pair<uint32_t, uint32_t>> sbs;

@@ -263,6 +263,7 @@ struct SqProbeArgs {
   uint32_t k;
   Probe *out;                   // run-local window id -> its record (zeroed up to wlim)
   uint32_t *unit_flags;         // per run unit (zeroed)
+  uint32_t *unit_hits;          // per run unit: occurrences of its windows' k-mers (zeroed)
 };
 
 __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
@@ -283,10 +284,12 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
     }
     if (!found) return;
     const uint32_t c = t.cnt;
+    // the window's unit: the 512-window block's first unit, then at most a unit or two on
+    // (units hold ~L windows); ublk, wbase and the per-unit counters are L2-resident
+    uint32_t u = A.ublk[w >> 9];
+    while (A.wbase[u + 1] <= w) u++;
     if (c & OVL_FLAG_SKIP) {
       // Hash_Find found an Empty entry: hi_hits (Find_Overlaps.C:321-366)
-      uint32_t u = A.ublk[w >> 9];
-      while (A.wbase[u + 1] <= w) u++;
       const uint32_t o = w - (uint32_t)A.wbase[u];
       const int32_t L = (int32_t)A.R.len[A.units[u].r];
       uint32_t f = 0;
@@ -298,6 +301,9 @@ __global__ void __launch_bounds__(256) k_probe_sorted(SqProbeArgs A) {
       pr.off = t.off;
       pr.cnt = c & OVL_CNT_MASK;
       A.out[w] = pr;
+      // the unit's hit count (k_probe's unit_hits) here rather than by a second pass over
+      // every record of the run: only the windows that hit pay, once
+      if (pr.cnt) atomicAdd(&A.unit_hits[u], pr.cnt);
     }
   };
   // 4 sorted windows per thread per step: their ids, keys and first table entries are
@@ -356,19 +362,6 @@ __global__ void __launch_bounds__(256) k_sq_sorted_check(const uint64_t *key, co
   }
   sq_sig_flush(s1, s2, threadIdx.x & 63, sig + 2);
   if (!ordered) atomicOr(bad, 1u);
-}
-
-// the units' hit counts (k_probe's unit_hits) from the records: one wave per unit, its
-// windows' records read once (a random atomic per hit would cost more)
-__global__ void __launch_bounds__(256) k_sq_unit_hits(const Probe *rec, const uint64_t *wbase,
-                                                      uint32_t nunits, uint32_t *unit_hits) {
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t u = blockIdx.x * 4 + wave;
-  if (u >= nunits) return;
-  uint32_t h = 0;
-  for (uint64_t w = wbase[u] + lane; w < wbase[u + 1]; w += 64) h += rec[w].cnt;
-  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
-  if (lane == 0) unit_hits[u] = h;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -219,67 +219,77 @@ def all_gather_rows(local, n: int, dist):
 REHEARSAL_COSTS = {"pair_s": 19.7 / 9.0e6, "probe_window_s": 2.2 / 48e9,
                    "index_window_s": 1.4 / 6.0e9}
 
-# Round 5's driver (super-batches of consecutive hash batches, the query range in sorted
-# chunks), fitted to four full-size rank jobs on one MI355X
-# (profiles/r05o_c4full.json, r05r7_c4full.json: the rehearsal-cost plan's ranks 0 and 7,
-# 18.3 and 33.7 s; r05p0_c4full.json, r05p7_c4full.json: a first driver-cost plan's, 26.6
-# and 31.0 s; the fit is within 2 % of all four):
-#   extension  0.68 us per (a < b) pair; the pairs are 2.19x the 36-per-read model's count
-#   seed       2.9e-11 s per query window and super-batch it is searched against
-#   index      6.6e-11 s per hashed window per build (one build per (chunk, super-batch))
-#   super-batches of ~1.08 G hashed windows and query chunks of ~5.9 G windows at a job's
-#   hi = 1.2 M reads, both shrinking as hi grows (the read store and the query windows take
-#   more of the 288 GB): 125 and 464 windows less per read of hi
-# bench.py's configs4-rank workload cuts its plan with it at the full 4M-read size (ranks 0,
-# 3 and 7 of that plan measured 29.0, 27.7 and 30.8 s: profiles/r05s*_c4full.json); the 20k
-# and 500k plans, which the committed reference digests pin, stay the rehearsal ones.
-DRIVER_COSTS = {"model": "driver", "pair_s": 0.68e-6, "pair_scale": 2.19,
-                "seed_window_s": 2.9e-11, "index_window_s": 6.6e-11,
-                "sb_windows": 1.08e9, "sb_slope": 125.0, "chunk_windows": 5.9e9,
-                "chunk_slope": 464.0, "hi_ref": 1.2e6}
+# Round 6: the driver's own planning rules replayed per job (ovl_overlap_driver, ovl_api.hip),
+# so that a plan sees the discrete steps -- hash batches packed whole into super-batches, the
+# query range cut into chunks -- that round 5's continuous fit smoothed over (its last three
+# boundaries were moved by hand below a packing step).  HBM figures are the device's and the library's own:
+#   device 309.2 GB (hipMemGetInfo's total), read store 1.0 GB + 0.75 B per base
+#     (r06a: 272.2 GB free after loading 4M reads, 295.3 GB after 1.449M)
+#   hash batch: the table load, 0.75 x 2^23 x 21 = 132.1 M windows (distinct k-mers ~ windows
+#     at 15x over 12 kb reads: 20 batches for 220 k reads, 131 for 1.449 M)
+#   super-batch cap = 0.55 x (free - 64 GB) / 112 windows (index_window_cap, phase 2), batches
+#     packed whole: r06a 1.033 G at 4M reads loaded (7 per super-batch), 1.146 G at 1.449M (8)
+#   an index holds 86 B per window of its largest super-batch (r06a: 80 GB for 0.93 G)
+#   query chunk cap = ((free at planning) / 2 - one run's sort scratch) x 0.9 / 13 windows
+#     (plan_query_chunks: 5.75 G windows at rank 7 of 4M, 6.33 G at 1.449 M)
+# and per-unit device costs from the per-search OVL_TIMING lines of the same two jobs
+# (profiles/r06a{0,7}_c4full_timing.log): a chunk's keys + sort 3.0e-11 s per window, a search
+# 2.3e-11 s per window of the runs it touches + 10 ms, a super-batch build 4.5e-11 s per
+# hashed window, phase 1 8 ms per hash batch, extension 0.68 us per pair (78.9 candidate pairs
+# per hashed read b, times b / n, at 15x).
+DRIVER6 = {"model": "driver6", "hbm": 309.2e9, "store_fixed": 1.0e9, "store_per_base": 0.75,
+           "batch_windows": 0.75 * (1 << 23) * 21, "sb_frac": 0.55, "sb_reserve": 64.0 * (1 << 30),
+           "sb_b_per_window": 112.0, "index_b_per_window": 86.0,
+           "sort_scratch": 24.0 * (1 << 29) + 8.0 * (1 << 20), "chunk_b_per_window": 13.0,
+           "run_windows": float(1 << 29),
+           "pair_s": 0.68e-6, "pairs_per_read": 78.9, "sort_s": 3.0e-11, "probe_s": 2.3e-11,
+           "search_s": 0.010, "build_s": 4.5e-11, "batch_s": 0.008, "job_s": 1.0}
 
 
-# configs[4]'s 8-rank plan at its real size (4M x 12 kb, 15x), as run: DRIVER_COSTS' cut with
-# the last three boundaries moved so that ranks 6 and 7 stay one super-batch below the
-# driver's packing step (rank 7's 244 k reads packed 5 super-batches, 220 k pack 4; DESIGN.md
-# configs[4]).  Every rank measured alone on one MI355X (profiles/r05s{0..4}_c4full.json,
-# r05w{5,6,7}_c4full.json): 29.0 28.2 28.6 27.7 28.9 29.4 28.1 27.2 s, 57,493,247 overlaps --
-# the same total as the unadjusted cut's eight jobs.  Hash-block upper ends:
-C4_FULL_PLAN_ENDS = (1448687, 2054957, 2513656, 2879216, 3217274, 3515000, 3780000, 4000000)
-
-
-def c4_full_plan() -> list[dict]:
-    """The measured 8-rank plan for configs[4] at 4M reads (C4_FULL_PLAN_ENDS), in
-    hash_block_jobs' format."""
-    jobs, lo = [], 1
-    for hi in C4_FULL_PLAN_ENDS:
-        jobs.append({"h": (lo, hi), "r": (1, hi), "est_s": round(driver_job_cost(
-            4_000_000, 12_000, 36.0, lo, hi), 2)})
-        lo = hi + 1
-    return jobs
-
-
-def driver_job_cost(n: int, read_len: float, pairs_per_read: float, lo: int, hi: int,
-                    c: dict | None = None) -> float:
-    """Modelled seconds of one `-h lo-hi -r 1-hi` job on round 5's driver (DRIVER_COSTS):
-    its pairs' extension, plus per searched (query chunk, super-batch) pair the chunk's
-    probes and the super-batch's build."""
-    c = DRIVER_COSTS if c is None else c
-    w = max(read_len - 21.0, 1.0)
+def driver_plan(n: int, read_len: float, lo: int, hi: int, c: dict | None = None,
+                k: int = 22) -> dict:
+    """The batch structure ovl_overlap_driver gives a `-h lo-hi -r 1-hi` job over reads of
+    about read_len (1..hi loaded), and its modelled seconds (DRIVER6)."""
+    c = DRIVER6 if c is None else c
+    w = max(read_len - k + 1, 1.0)                   # windows per read and strand
     m = hi - lo + 1
-    pairs = pairs_per_read * (lo + hi) / 2.0 * m / n * c["pair_scale"]
-    sb_cap = c["sb_windows"] - c["sb_slope"] * (hi - c["hi_ref"])
-    ch_cap = c["chunk_windows"] - c["chunk_slope"] * (hi - c["hi_ref"])
-    n_sb = max(1, int(np.ceil(m * w / max(sb_cap, 1e8))))
-    n_ch = max(1, int(np.ceil(2.0 * hi * w / max(ch_cap, 1e8))))
-    # (chunk, super-batch) pairs whose reads can meet: the chunk starts below the
-    # super-batch's last read
-    q0 = 1.0 + np.arange(n_ch) * (hi / n_ch)
-    s_end = lo + (np.arange(n_sb) + 1.0) * (m / n_sb)
-    searches = int((np.add.outer(q0, -s_end) < 0).sum())
-    seed_windows = searches * 2.0 * w * hi / n_ch
-    return (pairs * c["pair_s"] + seed_windows * c["seed_window_s"] +
-            searches * (m * w / n_sb) * c["index_window_s"])
+    free = c["hbm"] - c["store_fixed"] - c["store_per_base"] * read_len * hi
+    bw = c["batch_windows"]
+    n_batch = max(1, int(np.ceil(m * w / bw)))
+    sb_cap = c["sb_frac"] * max(free - c["sb_reserve"], 0.0) / c["sb_b_per_window"]
+    per_sb = max(1, int(sb_cap // bw))
+    n_sb = -(-n_batch // per_sb)
+    sb_reads = per_sb * bw / w                       # hashed reads per super-batch
+    sb_max = min(per_sb, n_batch) * bw
+    free_plan = free - c["index_b_per_window"] * sb_max
+    budget = max((free_plan / 2.0 - c["sort_scratch"]) * 0.9, 0.0)
+    ch_cap = max(budget / c["chunk_b_per_window"], 2.0 * w)
+    ch_reads = max(1, int(ch_cap // (2.0 * w)))
+    n_ch = -(-hi // ch_reads)
+    searches, searched, built = 0, 0.0, 0.0
+    for q in range(n_ch):
+        q0, q1 = 1 + q * ch_reads, min(hi, (q + 1) * ch_reads)
+        for s in range(n_sb):
+            s0 = lo + int(s * sb_reads)
+            s1 = min(hi, lo + int((s + 1) * sb_reads) - 1)
+            if q0 < s1:
+                searches += 1
+                # the runs holding the chunk's reads below the super-batch's last read
+                win = 2.0 * w * (min(q1, s1 - 1) - q0 + 1)
+                searched += min(2.0 * w * (q1 - q0 + 1), win + c["run_windows"] / 2.0)
+                built += w * (s1 - s0 + 1)
+    pairs = c["pairs_per_read"] * m * (lo + hi) / 2.0 / n
+    secs = (pairs * c["pair_s"] + 2.0 * w * hi * c["sort_s"] + searched * c["probe_s"] +
+            searches * c["search_s"] + built * c["build_s"] + n_batch * c["batch_s"] + c["job_s"])
+    return {"hash_batches": n_batch, "super_batches": n_sb, "query_chunks": n_ch,
+            "searches": searches, "sb_cap": sb_cap, "chunk_cap": ch_cap, "pairs": pairs,
+            "est_s": secs}
+
+
+def c4_plan(n: int, world: int, read_len: float) -> list[dict]:
+    """configs[4]'s plan at its real size: the blocks cut on DRIVER6 (the driver's packing
+    replayed per job), in hash_block_jobs' format."""
+    return hash_block_jobs(n, world, read_len, 36.0, 1.0, costs=DRIVER6)
 
 
 def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
@@ -299,8 +309,8 @@ def hash_block_jobs(n: int, world: int, read_len: float, pairs_per_read: float,
     def cost(lo: int, hi: int) -> float:
         if hi < lo:
             return 0.0
-        if c.get("model") == "driver":
-            return driver_job_cost(n, read_len, pairs_per_read, lo, hi, c)
+        if c.get("model") == "driver6":
+            return driver_plan(n, read_len, lo, hi, c)["est_s"]
         m = hi - lo + 1
         pairs = pairs_per_read * (lo + hi) / 2.0 * m / n    # sum over b of b * ppr / n
         batches = max(1.0, m * w / batch_windows)

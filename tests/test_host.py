@@ -94,48 +94,44 @@ def test_hash_block_jobs_cover_and_balance():
     assert widths == sorted(widths, reverse=True)
 
 
-# full-size configs[4] rank jobs measured on one MI355X (profiles/r05{o,r7,p0,p7}_c4full.json
-# r05s{0..7}_c4full.json and r05w{5,6,7}_c4full.json): hash block -> seconds per job
-C4_FULL_RUNS = {(1, 1145091): 18.27, (3718142, 4000000): 33.69, (1, 1389603): 26.60,
-                (3744207, 4000000): 31.00, (1, 1448687): 29.02, (1448688, 2054957): 28.18,
-                (2054958, 2513656): 28.60, (2513657, 2879216): 27.70,
-                (2879217, 3217274): 28.88, (3217275, 3502307): 28.30,
-                (3502308, 3756241): 27.52, (3756242, 4000000): 30.78,
-                (3217275, 3515000): 29.37, (3515001, 3780000): 28.05, (3780001, 4000000): 27.25}
+# full-size configs[4] rank jobs measured on one MI355X with round 6's harness (the staged bases
+# freed before the job): hash block -> (seconds, hash batches, super-batches, query chunks)
+# (profiles/r06a{7,0}_c4full.json)
+C4_FULL_RUNS = {(3780001, 4000000): (24.97, 20, 3, 17), (1, 1448687): (28.04, 131, 17, 6)}
 
 
-def test_driver_cost_plan_fits_full_size_runs():
-    """dist.DRIVER_COSTS (round 5's driver: super-batches x sorted query chunks) against the
-    fifteen full-size rank jobs measured on the GPU: every job within 11 %, and the plan it cuts
-    covers the reads in contiguous blocks with the first the widest."""
+def test_driver6_replays_the_driver_plans():
+    """dist.driver_plan (the driver's packing rules replayed per job) against full-size rank
+    jobs measured on the GPU: the same super-batches and query chunks, the hash batches within
+    one, the time within 6 %."""
     from canu_amd import dist
-    js = dist.hash_block_jobs(4_000_000, 8, 12_000, 36.0, 1.0, costs=dist.DRIVER_COSTS)
-    assert js[0]["h"][0] == 1 and js[-1]["h"][1] == 4_000_000
-    for a, b in zip(js, js[1:]):
-        assert b["h"][0] == a["h"][1] + 1
-    assert js[0]["h"][1] - js[0]["h"][0] == max(j["h"][1] - j["h"][0] for j in js)
-    for (lo, hi), meas in C4_FULL_RUNS.items():
-        est = dist.driver_job_cost(4_000_000, 12_000, 36.0, lo, hi)
-        assert abs(est - meas) / meas < 0.11, (lo, hi, est, meas)
+    for (lo, hi), (secs, nb, nsb, nch) in C4_FULL_RUNS.items():
+        p = dist.driver_plan(4_000_000, 12_000, lo, hi)
+        assert abs(p["hash_batches"] - nb) <= 1, (lo, hi, p)
+        assert (p["super_batches"], p["query_chunks"]) == (nsb, nch), (lo, hi, p)
+        assert abs(p["est_s"] - secs) / secs < 0.06, (lo, hi, p["est_s"], secs)
 
 
 def test_c4_full_plan_covers_the_reads(monkeypatch):
-    """The measured configs[4] plan (dist.C4_FULL_PLAN_ENDS): eight contiguous `-h lo-hi -r 1-hi`
-    blocks over 1..4M, and bench.py's configs4-rank workload runs it at that size."""
+    """configs[4]'s plan at 4M reads (dist.c4_plan, cut on DRIVER6): eight contiguous
+    `-h lo-hi -r 1-hi` blocks over 1..4M with equal modelled time, and bench.py's
+    configs4-rank workload runs exactly those jobs (checked without reads or a GPU)."""
     from canu_amd import dist
-    js = dist.c4_full_plan()
+    js = dist.c4_plan(4_000_000, 8, 12_000)
     assert len(js) == 8 and js[0]["h"][0] == 1 and js[-1]["h"][1] == 4_000_000
     for a, b in zip(js, js[1:]):
         assert b["h"][0] == a["h"][1] + 1
     for j in js:
         assert j["r"] == (1, j["h"][1])
+    est = [j["est_s"] for j in js]
+    assert max(est) / min(est) < 1.03
     import bench
     monkeypatch.delenv("CANU_C4_PLAN", raising=False)
     monkeypatch.delenv("CANU_C4_HBLOCK", raising=False)
     for r in range(8):
         w = bench.Configs4Rank(bench.parse_args(["--workload", "configs4-rank", "--reads",
                                                  "4000000", "--rank-job", str(r)]), 0, 1, None)
-        assert w.plan() == "r05"
+        assert w.plan() == "r06"
         jobs, job = w.plan_jobs()            # what generate() runs, without reads or a GPU
         assert [(j["h"], j["r"]) for j in jobs] == [(j["h"], j["r"]) for j in js]
         assert (job["h"], job["r"]) == (js[r]["h"], js[r]["r"])

@@ -1,7 +1,6 @@
 # configs[4] at its real size on one GPU: one rank job of the 8-GPU plan for 4M x 12 kb ONT
-# reads (dist.c4_full_plan: the driver-cost cut as measured, rank 0 is
-# -h 1-1448687 -r 1-1448687; CANU_C4_PLAN=r02 gives the rehearsal-cost plan, rank 0
-# -h 1-1145091), canu's --hashbits 23 --hashload 0.75, the job's reads generated before GPU
+# reads (dist.c4_plan: the blocks cut on DRIVER6, the driver's own packing replayed per job;
+# CANU_C4_PLAN=r02 gives the rehearsal-cost plan, rank 0 -h 1-1145091), canu's --hashbits 23 --hashload 0.75, the job's reads generated before GPU
 # init.  One timed job (no warm-up: its first-use allocations are inside it, OVL_TIMING shows
 # them), per-search timing lines, and the HBM high-water from rocm-smi beside it.
 # usage: bash tools/c4_full.sh TAG [rank_job] [extra bench.py args]
