@@ -209,6 +209,7 @@ struct ovl_ctx {
     DBuf<uint64_t> rbase;
     DBuf<Probe> probe;
     DBuf<uint32_t> uhits, uflags, ctr, done, dset, big, defer, defer2, okey, oidx, okey2, oidx2;
+    DBuf<uint32_t> live;          // the chain's units with at least one hit
     DBuf<uint32_t> xctr[2], xnout;
     DBuf<unsigned long long> chits;
     DBuf<uint8_t> otmp;
@@ -1250,7 +1251,7 @@ static void release_find_buffers(ovl_ctx *c) {
     f.units[i].release(); f.pnodes[i].release(); f.pairs[i].release();
   }
   f.rbase.release(); f.probe.release(); f.uhits.release();
-  f.uflags.release(); f.done.release(); f.dset.release(); f.big.release();
+  f.uflags.release(); f.done.release(); f.dset.release(); f.big.release(); f.live.release();
   f.defer.release(); f.defer2.release(); f.okey.release(); f.oidx.release();
   f.okey2.release(); f.oidx2.release(); f.otmp.release(); f.pool.release();
   f.ok64a.release(); f.ok64b.release(); f.dkey.release(); f.oa.release(); f.ob.release();
@@ -2500,6 +2501,18 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       pnodes_cap = hsum + 1;
     };
     set_caps();
+    // only units with hits are chained: a unit without one adds no pair, node, counter or
+    // flag, yet its wave would read every window's record (a full-size configs[4] search
+    // against a super-batch of ~2 % of the reads: about half its units)
+    std::vector<uint32_t> live;
+    live.reserve(nc);
+    for (uint32_t i = 0; i < nc; i++)
+      if (uh[i]) live.push_back(i);
+    const bool all_live = live.size() == nc;
+    if (!all_live && !live.empty()) {
+      if (c->fb.live.grow(live.size())) return fail(OVL_ERR_OOM, "unit list");
+      HIPC(hipMemcpyAsync(c->fb.live.p, live.data(), 4ull * live.size(), hipMemcpyHostToDevice, s));
+    }
     const uint32_t hash_reads = c->hash_end_iid - c->hash_bgn_iid + 1;
     uint32_t hc[16];
     unsigned long long chain_hits = 0;
@@ -2534,7 +2547,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       CA.rbase = d_rbase.p;
       CA.probes = d_probe.p;
       CA.unit_flags = chain_uflags;
-      CA.nunits = nc;
+      CA.nunits = all_live ? nc : (uint32_t)live.size();
       CA.k = k;
       CA.unit_next = d_ctr.p + 0;
       CA.pool = d_pool.p;
@@ -2547,7 +2560,7 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
       CA.npairs = d_ctr.p + 3;
       CA.pairs_cap = (uint32_t)pairs_cap;
       CA.overflow = d_ctr.p + 4;
-      CA.unit_list = nullptr;
+      CA.unit_list = all_live ? nullptr : c->fb.live.p;
       CA.big_units = c->fb.big.p;
       CA.n_big = d_ctr.p + 10;
       CA.done_slots = nullptr;
