@@ -2317,9 +2317,19 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         return OVL_OK;
       };
       if (regrow(A.units, A.nu, A.nu + nu_c) || regrow(A.pnodes, A.nn, A.nn + nn_c) ||
-          regrow(A.pairs, A.np, A.np + np_c))
-        return fail(OVL_ERR_OOM, "extension accumulator (%llu nodes)",
-                    (unsigned long long)(A.nn + nn_c));
+          regrow(A.pairs, A.np, A.np + np_c)) {
+        // no room for bigger buffers beside the ones being copied (a device nearly full of
+        // sorted windows, index and search buffers): what the accumulator holds is extended
+        // now, and the emptied buffers are freed before this chunk's own are allocated
+        if (A.nu || A.nn || A.np) {
+          if (int rc = flush_acc()) return rc;
+          HIPC(hipStreamSynchronize(xs));
+          HIPC(hipStreamSynchronize(s));
+        }
+        if ((A.units.n < nu_c && A.units.alloc(nu_c)) ||
+            (A.pnodes.n < nn_c && A.pnodes.alloc(nn_c)) || (A.pairs.n < np_c && A.pairs.alloc(np_c)))
+          return fail(OVL_ERR_OOM, "extension accumulator (%llu nodes)", (unsigned long long)nn_c);
+      }
     }
     if (nu_c)
       HIPC(hipMemcpyAsync(A.units.p + A.nu, u, sizeof(Unit) * nu_c, hipMemcpyDeviceToDevice, s));

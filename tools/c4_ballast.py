@@ -50,7 +50,11 @@ def main():
             if free > tgt * 1e9:
                 ballast = torch.empty(int(free - tgt * 1e9), dtype=torch.uint8, device="cuda:0")
             t1 = time.time()
-            nrec = oic.overlap_driver(store_num_reads=n)
+            try:
+                nrec = oic.overlap_driver(store_num_reads=n)
+            except Exception as e:                      # reported, the next target runs
+                print(json.dumps({"free_gb_at_start": tgt, "error": str(e)[:300]}), flush=True)
+                continue
             dt = time.time() - t1
             st = oic.stats()
             rec = oic.fetch(nrec)
