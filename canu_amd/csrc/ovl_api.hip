@@ -1907,18 +1907,18 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
   };
   c->ext_classes.clear();
   // occupancy tiers of the staged kernel: 3 blocks of 8 waves per CU (the register limit),
-  // 3 blocks of 6, then blocks of up to 8 waves within 160 KB (as many as fit a CU).  A class's length is the
-  // longest loaded read inside its tier, so its scratch (and a short-read job's launch) is
-  // exactly what a job without the longer reads would get.
+  // 3 blocks of 6, then blocks of up to 8 waves within 160 KB (as many as fit a CU).  A
+  // class's length is the span it stages (k_extend stages a pair's overlap span, not its
+  // whole reads): the tier's limit, or the longest loaded read when that is shorter, so a
+  // short-read job's launch is exactly what it was and a long-read job's pairs with shorter
+  // spans run at the higher occupancy.
   {
     uint32_t prev = 0;
     const size_t tier_cap[3] = {52 * 1024, 52 * 1024, 160 * 1024};
     const uint32_t tier_wpb[3] = {8, 6, 1};
     for (int t = 0; t < 3; t++) {
       const uint32_t T = longest_fitting(tier_wpb[t], tier_cap[t]);
-      uint32_t L = 0;
-      for (uint32_t x : c->h_len)
-        if (x <= T && x > L) L = x;
+      const uint32_t L = std::min<uint32_t>(T, c->max_len);
       if (L < 64 || L <= prev) continue;
       if (make_stage(L, tier_cap[t], t == 0)) return fail(OVL_ERR_HIP, "staged kernel setup");
       prev = L;
@@ -2188,7 +2188,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         EA.e_cap = gen.ecap;
         EA.rows_cap = gen.stride;
         EA.sw_words = 0;
-        EA.stage_len = 0;
         EA.pair_next = x_ctr.p + 9;
         n_ext_launch++;
         if (gen.l16)
@@ -2208,7 +2207,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
           EA.e_cap = g.ecap;
           EA.rows_cap = g.stride;
           EA.sw_words = g.sw;
-          EA.stage_len = (int32_t)g.len;
           EA.pair_next = x_ctr.p + ctr_next[ci];
           EA.defer = defer_buf[ci & 1];
           EA.ndefer = x_ctr.p + ctr_defer[ci];
@@ -2245,7 +2243,6 @@ static int find_impl(ovl_ctx *c, uint32_t bgn, uint32_t end, uint32_t lib_lo, ui
         EA.e_cap = gen.ecap;
         EA.rows_cap = gen.stride;
         EA.sw_words = 0;
-        EA.stage_len = 0;
         EA.pair_next = x_ctr.p + 9;
         EA.defer = nullptr;
         EA.ndefer = nullptr;

@@ -47,7 +47,6 @@ struct ExtendArgs {
   int32_t *rowdir;              // per wave: (offset, lo) per error level
   int32_t *deltas;              // per wave: stack | right | left
   int32_t e_cap;                // error levels the scratch holds
-  int32_t stage_len;            // staged kernel: pairs with a longer read are deferred
   int32_t sw_words;             // staged kernel: LDS words per strand (even)
   Rec *out;
   uint32_t *nout;
@@ -1784,6 +1783,28 @@ __device__ __forceinline__ StrandLP stage_strand(const Strand &G, lds_u64 *dst, 
   return L;
 }
 
+// Words w0..w1 of a strand only (a pair's span, below): the returned strand keeps absolute
+// positions (its base pointer is dst - w0), and only words in w0..w1 are ever read.
+__device__ __forceinline__ StrandLP stage_strand_span(const Strand &G, lds_u64 *dst, int32_t w0,
+                                                      int32_t w1, uint32_t lane) {
+  for (int32_t i = w0 + (int32_t)lane; i <= w1; i += 64) {
+    const uint64_t w = G.w[i];
+    dst[i - w0] = (uint64_t)compact_even(w) | ((uint64_t)compact_even(w >> 1) << 32);
+  }
+  StrandLP L;
+  L.w = dst - w0;
+  L.len = G.len;
+  return L;
+}
+
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t t = __shfl_xor(v, o);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+
 #define OVL_SCR_STAGE 256        // the staged kernel's per-wave LDS scratch ints
                                  // (Lies_On_Alignment thresholds, Left_Delta cache)
 
@@ -1901,9 +1922,35 @@ k_extend(ExtendArgs X) {
     }
     if constexpr (STAGE) {
       bool ok = false;
-      if (!(S.ex_wild || S.ex_nul || T.ex_wild) && S.len <= X.stage_len && T.len <= X.stage_len) {
-        StrandLP SL = stage_strand(S, sw, lane);
-        StrandLP TL = stage_strand(T, tw, lane);
+      // The pair's span: every extension of Process_Matches starts on one of its matches'
+      // diagonals (a - b), and the greedy rows of e errors stay within e diagonals of it
+      // (at most the class's e_cap), sliding at most to the reads' ends along them; the row
+      // slides read 64 bases from a 32-base word.  So A is read only inside
+      // [max(0, dmin), min(La, Lb + dmax)] and B inside [max(0, -dmax), min(Lb, La - dmin)],
+      // each widened by e_cap + 128 bases: those words are staged, not the whole reads, and a
+      // pair of long reads whose overlap span fits this class's LDS runs at its occupancy.
+      int32_t dmin = 0x7fffffff, dmax = (int32_t)0x80000000;
+      {
+        const Node *nodes = X.pnodes + P.node_off;
+        for (uint32_t i = lane; i < P.node_cnt; i += 64) {
+          const Node nd = nodes[i];
+          const int32_t d = nd.Start - nd.Offset;
+          dmin = d < dmin ? d : dmin;
+          dmax = d > dmax ? d : dmax;
+        }
+        dmin = __builtin_amdgcn_readfirstlane(wave_min_i32(dmin));
+        dmax = __builtin_amdgcn_readfirstlane(-wave_min_i32(-dmax));
+      }
+      const int32_t La = S.len, Lb = T.len, mg = X.e_cap + 128;
+      const int32_t a_lo = max(0, max(0, dmin) - mg), a_hi = min(La, min(La, Lb + dmax) + mg);
+      const int32_t b_lo = max(0, max(0, -dmax) - mg), b_hi = min(Lb, min(Lb, La - dmin) + mg);
+      // words of the span, the guard word (index (L + 31) / 32) included at a read's end
+      const int32_t aw0 = a_lo >> 5, aw1 = min((La + 31) >> 5, (a_hi >> 5) + 1);
+      const int32_t bw0 = b_lo >> 5, bw1 = min((Lb + 31) >> 5, (b_hi >> 5) + 1);
+      if (!(S.ex_wild || S.ex_nul || T.ex_wild) && P.node_cnt > 0 &&
+          aw1 - aw0 + 1 <= X.sw_words && bw1 - bw0 + 1 <= X.sw_words) {
+        StrandLP SL = stage_strand_span(S, sw, aw0, aw1, lane);
+        StrandLP TL = stage_strand_span(T, tw, bw0, bw1, lane);
         lds_sync();
         PROF_T(pp0);
         ok = process_pair<true, L16, false, RJ>(X, P, un, SL, TL, WM, stk, RD, LD, st, lane, nullptr);

@@ -255,12 +255,23 @@ def driver_plan(n: int, read_len: float, lo: int, hi: int, c: dict | None = None
     m = hi - lo + 1
     free = c["hbm"] - c["store_fixed"] - c["store_per_base"] * read_len * hi
     bw = c["batch_windows"]
-    n_batch = max(1, int(np.ceil(m * w / bw)))
+    # the table load cuts full batches of bw windows; the last one holds what is left
+    full, tail = divmod(m * w, bw)
+    sizes = [bw] * int(full) + ([tail] if tail > 0 else [])
+    n_batch = max(1, len(sizes))
     sb_cap = c["sb_frac"] * max(free - c["sb_reserve"], 0.0) / c["sb_b_per_window"]
-    per_sb = max(1, int(sb_cap // bw))
-    n_sb = -(-n_batch // per_sb)
-    sb_reads = per_sb * bw / w                       # hashed reads per super-batch
-    sb_max = min(per_sb, n_batch) * bw
+    # phase 2's greedy packing of whole batches (a batch past the cap is a super-batch alone)
+    sbs, cur = [], 0.0
+    for b in sizes:
+        if sbs and cur + b <= sb_cap:
+            sbs[-1] += b
+            cur += b
+        else:
+            sbs.append(b)
+            cur = b
+    n_sb = max(1, len(sbs))
+    sb_max = max(sbs) if sbs else 0.0
+    sb_ends = np.cumsum(sbs) / w if sbs else np.array([float(m)])   # hashed reads, cumulative
     free_plan = free - c["index_b_per_window"] * sb_max
     budget = max((free_plan / 2.0 - c["sort_scratch"]) * 0.9, 0.0)
     ch_cap = max(budget / c["chunk_b_per_window"], 2.0 * w)
@@ -270,8 +281,8 @@ def driver_plan(n: int, read_len: float, lo: int, hi: int, c: dict | None = None
     for q in range(n_ch):
         q0, q1 = 1 + q * ch_reads, min(hi, (q + 1) * ch_reads)
         for s in range(n_sb):
-            s0 = lo + int(s * sb_reads)
-            s1 = min(hi, lo + int((s + 1) * sb_reads) - 1)
+            s0 = lo + (int(sb_ends[s - 1]) if s else 0)
+            s1 = min(hi, lo + int(sb_ends[s]) - 1) if s + 1 < n_sb else hi
             if q0 < s1:
                 searches += 1
                 # the runs holding the chunk's reads below the super-batch's last read

@@ -245,10 +245,10 @@ def main():
     cf = load(sys.argv[1])
     pick = sys.argv[2] if len(sys.argv) > 2 else None
     for m in cf.methods:
-        if pick and pick not in m["name"]:
+        if pick is not None and pick not in m["name"]:      # "" disassembles every method
             continue
         print(f"{m['name']}{m['desc']}")
-        if pick:
+        if pick is not None:
             print("\n".join(cf.disassemble(m)))
 
 
