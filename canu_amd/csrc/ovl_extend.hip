@@ -1939,7 +1939,7 @@ k_extend(ExtendArgs X) {
           dmax = d > dmax ? d : dmax;
         }
         dmin = __builtin_amdgcn_readfirstlane(wave_min_i32(dmin));
-        dmax = __builtin_amdgcn_readfirstlane(-wave_min_i32(-dmax));
+        dmax = wave_max(dmax);                 // lanes without a node hold the identities
       }
       const int32_t La = S.len, Lb = T.len, mg = X.e_cap + 128;
       const int32_t a_lo = max(0, max(0, dmin) - mg), a_hi = min(La, min(La, Lb + dmax) + mg);
