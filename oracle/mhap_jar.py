@@ -1,0 +1,593 @@
+"""CPU restatement of MHAP 2.1.2 as the jar canu runs executes it (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench_mhap.py's cpu_baseline leg use this module.
+
+The reference ships MHAP only as compiled classes (src/mhap/mhap-2.1.2.tar ->
+mhap-2.1.2.jar; third party: MHAP 2.1.2, Berlin et al. 2015).  The jar is never run or loaded
+here and no JVM exists; its class files were READ as data with tools/classfile.py (a
+constant-pool + bytecode disassembler) and the methods below restate what that bytecode
+does, method by method.  Each function names the class, method and bytecode offsets it
+follows ("MinHashSketch.computeNgramMinHashesWeighted @243-328").  The two library hashes
+the jar calls are Guava's published Murmur3 functions (com.google.common.hash.Hashing
+.murmur3_128(0) / murmur3_32(0), Hasher.putUnencodedChars: each char as 2 little-endian
+bytes), restated here from MurmurHash3 (x64_128 / x86_32).  PARITY IS PINNED TO THE
+BYTECODE'S MEANING, NOT TO JAR OUTPUTS: no output of the jar exists in the reference and the
+jar cannot be run, so a misreading would not be caught by a fixture.
+
+Pipeline (MhapMain -> MinHashSearch), canu's options (OverlapMhap.pm:381-392):
+  * every read of at least --min-olap-length bases (SequenceSketchStreamer.enqueue @16-30)
+    is sketched forward AND reverse-complemented (enqueue @67-95; Utils.rc is the IUPAC
+    complement); a read with no k-mer is skipped (enqueueUntilFound's catch)
+  * MinHash sketch of a sequence string (SequenceSketch.<init> @20-39: doRC false):
+    MinHashSketch.computeNgramMinHashesWeighted
+  * ordered sketch: BottomOverlapSketch.<init>(seq, k', S, false)
+  * the index stores both strands of every read (MinHashSearch.<init> @97-175 -> addData:
+    dequeue(fwdOnly = !doRC)); queries are forward sketches
+  * MinHashSearch.findMatches: shared min-mer count per stored sketch >= --num-min-matches,
+    then BottomOverlapSketch.getOverlapInfo >= --threshold -> MatchResult
+  * MatchResult.toString: "%s %s %.6f %.6f %d %d %d %d %d %d %d %d"
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
+LONG_MAX = (1 << 63) - 1
+
+# Utils$Translate.<clinit>: the complement table Utils.rc uses (IUPAC)
+_COMP = {ord(a): ord(b) for a, b in zip("ABCDGHKMNRSTVWY", "TVGHCDMKNYSABWR")}
+_COMP_TAB = np.zeros(256, dtype=np.uint8)
+for _a, _b in _COMP.items():
+    _COMP_TAB[_a] = _b
+
+
+def default_params(**kw) -> dict:
+    """MhapMain's option defaults (<init> option table @100-271) with canu's 'normal'
+    correction settings where canu passes them (OverlapMhap.pm:109-150, :381-392)."""
+    p = dict(k=16, num_hashes=512, min_matches=3, threshold=0.78, ordered_sketch=1536,
+             ordered_k=12, min_olap=500, max_shift=0.2, min_store=0, repeat_weight=0.9,
+             repeat_idf_scale=10.0, filter_threshold=1e-5, no_tf=False, no_rc=False)
+    p.update(kw)
+    return p
+
+
+# ---- Guava Murmur3 (Hashing.murmur3_128(0) / murmur3_32(0)) ---------------------------
+def _rotl64(x, r):
+    return ((x << r) | (x >> (64 - r))) & M64
+
+
+def _fmix64(k):
+    k ^= k >> 33
+    k = (k * 0xFF51AFD7ED558CCD) & M64
+    k ^= k >> 33
+    k = (k * 0xC4CEB9FE1A85EC53) & M64
+    k ^= k >> 33
+    return k
+
+
+def murmur3_128_h1(data: bytes, seed: int = 0) -> int:
+    """MurmurHash3_x64_128's first 64 bits (Guava HashCode.asLong: the first 8 bytes of the
+    hash, little-endian = h1), as a signed Java long."""
+    c1, c2 = 0x87C37B91114253D5, 0x4CF5AD432745937F
+    h1 = h2 = seed & M64
+    n = len(data)
+    nb = n // 16
+    for i in range(nb):
+        k1 = int.from_bytes(data[16 * i:16 * i + 8], "little")
+        k2 = int.from_bytes(data[16 * i + 8:16 * i + 16], "little")
+        k1 = (k1 * c1) & M64
+        k1 = _rotl64(k1, 31)
+        k1 = (k1 * c2) & M64
+        h1 ^= k1
+        h1 = _rotl64(h1, 27)
+        h1 = (h1 + h2) & M64
+        h1 = (h1 * 5 + 0x52DCE729) & M64
+        k2 = (k2 * c2) & M64
+        k2 = _rotl64(k2, 33)
+        k2 = (k2 * c1) & M64
+        h2 ^= k2
+        h2 = _rotl64(h2, 31)
+        h2 = (h2 + h1) & M64
+        h2 = (h2 * 5 + 0x38495AB5) & M64
+    tail = data[16 * nb:]
+    k1 = k2 = 0
+    t = len(tail)
+    if t > 8:
+        k2 = int.from_bytes(tail[8:], "little")
+        k2 = (k2 * c2) & M64
+        k2 = _rotl64(k2, 33)
+        k2 = (k2 * c1) & M64
+        h2 ^= k2
+    if t > 0:
+        k1 = int.from_bytes(tail[:8], "little")
+        k1 = (k1 * c1) & M64
+        k1 = _rotl64(k1, 31)
+        k1 = (k1 * c2) & M64
+        h1 ^= k1
+    h1 ^= n
+    h2 ^= n
+    h1 = (h1 + h2) & M64
+    h2 = (h2 + h1) & M64
+    h1 = _fmix64(h1)
+    h2 = _fmix64(h2)
+    h1 = (h1 + h2) & M64
+    return h1 - (1 << 64) if h1 >> 63 else h1
+
+
+def murmur3_32(data: bytes, seed: int = 0) -> int:
+    """MurmurHash3_x86_32 (Guava HashCode.asInt), as a signed Java int."""
+    c1, c2 = 0xCC9E2D51, 0x1B873593
+    h = seed & M32
+    n = len(data)
+    nb = n // 4
+    for i in range(nb):
+        k = int.from_bytes(data[4 * i:4 * i + 4], "little")
+        k = (k * c1) & M32
+        k = ((k << 15) | (k >> 17)) & M32
+        k = (k * c2) & M32
+        h ^= k
+        h = ((h << 13) | (h >> 19)) & M32
+        h = (h * 5 + 0xE6546B64) & M32
+    tail = data[4 * nb:]
+    if tail:
+        k = int.from_bytes(tail, "little")
+        k = (k * c1) & M32
+        k = ((k << 15) | (k >> 17)) & M32
+        k = (k * c2) & M32
+        h ^= k
+    h ^= n
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    return h - (1 << 32) if h >> 31 else h
+
+
+def _chars(s: bytes) -> bytes:
+    """putUnencodedChars: every char as 2 little-endian bytes (ASCII: the byte, then 0)."""
+    out = bytearray(2 * len(s))
+    out[0::2] = s
+    return bytes(out)
+
+
+def rc(s: bytes) -> bytes:
+    """Utils.rc @0-54: reverse, upper case, IUPAC complement (Utils$Translate)."""
+    return bytes(_COMP_TAB[np.frombuffer(s.upper()[::-1], dtype=np.uint8)])
+
+
+def seq_hashes_long(s: bytes, k: int, do_rc: bool = False) -> list[int]:
+    """HashUtils.computeSequenceHashesLong(s, k, seed 0, doRC) @0-108: per k-mer the
+    murmur3_128 h1 of its chars; with doRC the lexicographically smaller of the k-mer and
+    its reverse complement (String.compareTo) is hashed."""
+    out = []
+    for i in range(len(s) - k + 1):
+        km = s[i:i + k]
+        if do_rc:
+            r = rc(km)
+            if r < km:
+                km = r
+        out.append(murmur3_128_h1(_chars(km)))
+    return out
+
+
+def seq_hashes_int(s: bytes, k: int) -> np.ndarray:
+    """HashUtils.computeSequenceHashes(s, k, false) @0-106: murmur3_32 of each k-mer."""
+    return np.array([murmur3_32(_chars(s[i:i + k])) for i in range(len(s) - k + 1)],
+                    dtype=np.int32)
+
+
+# ---- FrequencyCounts (-f) ----------------------------------------------------------------
+class FrequencyCounts:
+    """FrequencyCounts.<init>(reader, filterCutoff, offset, removeUnique, noTf, threads,
+    range, doRC) @0-429 and its lambda$1 @0-206: line 1 the k-mer count, then "kmer frac"
+    lines; a k-mer's key is computeSequenceHashesLong(kmer, len, 0, doRC)[0]; lines with
+    frac >= filterCutoff enter fractionCounts (key -> frac) and raise maxValue.
+    MhapMain passes offset = --repeat-weight when it lies in [0, 1) (else 0), range =
+    --repeat-idf-scale, doRC = !--no-rc.  removeUnique (--supress-noise) > 0 builds a Guava
+    Bloom filter of the keys; it is not restated (canu passes it only with
+    mhapFilterUnique) and is refused."""
+
+    def __init__(self, kmers, fractions, p: dict):
+        if int(p.get("supress_noise", 0)):
+            raise NotImplementedError("--supress-noise (Guava BloomFilter) is not restated")
+        rw = float(p["repeat_weight"])
+        self.offset = rw if 0.0 <= rw < 1.0 else 0.0
+        self.range = float(p["repeat_idf_scale"])
+        self.filter_cutoff = float(p["filter_threshold"])
+        self.no_tf = bool(p.get("no_tf", False))
+        do_rc = not p.get("no_rc", False)
+        self.counts = {}
+        self.max_value = -math.inf
+        for km, f in zip(kmers, fractions):
+            km = km.encode() if isinstance(km, str) else bytes(km)
+            key = seq_hashes_long(km, len(km), do_rc)[0]
+            f = float(f)
+            if f >= self.filter_cutoff:
+                self.max_value = max(self.max_value, f)
+                self.counts[key] = f
+        self.min_value = self.filter_cutoff
+        self.min_idf = self.idf(self.max_value)
+        self.max_idf = self.idf(self.min_value)
+
+    def idf(self, x: float) -> float:               # idf(D) @0-14
+        return math.log(self.max_value / x - self.offset)
+
+    def is_popular(self, key: int) -> bool:          # isPopular @0-13
+        return key in self.counts
+
+    def tf_weight(self, c: int) -> float:            # tfWeight @0-11
+        return 1.0 if self.no_tf else float(c)
+
+    def scaled_idf(self, key: int) -> float:         # scaledIdf(J, D) @31-94
+        f = self.counts.get(key)
+        if f is None:
+            return self.range
+        idf = self.idf(f)
+        scale = (self.max_idf - self.min_idf) / (self.range - 1.0)
+        return 1.0 + (idf - self.min_idf) / scale
+
+
+def java_round(x: float) -> int:
+    """Math.round(double): the closest long, ties toward positive infinity."""
+    r = math.floor(x)
+    return int(r + 1) if x - r >= 0.5 else int(r)
+
+
+# ---- MinHashSketch.computeNgramMinHashesWeighted -----------------------------------------
+def _xorshift_steps(x: np.ndarray, n: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        for _ in range(n):
+            x ^= x << np.uint64(21)
+            x ^= x >> np.uint64(35)
+            x ^= x << np.uint64(4)
+    return x
+
+
+def minhash(s: bytes, p: dict, fc: FrequencyCounts | None):
+    """MinHashSketch.computeNgramMinHashesWeighted(s, k, H, filter, false, repeatWeight)
+    @0-476: None when the sequence has no k-mer (@10-26 / @142-160 / @458-473: the read is
+    skipped).  Otherwise int32[H]:
+      keys = computeSequenceHashesLong(s, k, 0, false); a LinkedOpenHashMap counts each key
+        (insertion order = first occurrence)                                  @27-139
+      weight: repeatWeight < 0 -> 1 (0 for a popular -f key); a -f table and
+        0 <= repeatWeight < 1 -> max(1, round(tfWeight(count) * scaledIdf(key))); else
+        the count                                                             @241-324
+      per key with weight > 0, x = key; for word 0..H-1, weight times:
+        x ^= x << 21; x ^= x >>> 35; x ^= x << 4 (longs); if x < best[word] (signed):
+        best[word] = x, hash[word] = (int) key (even word) or (int) (key >>> 32) (odd)
+                                                                              @334-445"""
+    k, H = p["k"], p["num_hashes"]
+    if len(s) - k + 1 < 1:
+        return None
+    keys = seq_hashes_long(s, k, False)
+    counts = {}
+    for key in keys:                                 # dict keeps insertion order
+        counts[key] = counts.get(key, 0) + 1
+    if not counts:
+        return None
+    rw = float(p["repeat_weight"])
+    ks, ws = [], []
+    for key, c in counts.items():
+        w = c
+        if rw < 0.0:
+            w = 1
+            if fc is not None and fc.is_popular(key):
+                w = 0
+        elif fc is not None and 0.0 <= rw < 1.0:
+            w = java_round(fc.tf_weight(w) * fc.scaled_idf(key))
+            if w < 1:
+                w = 1
+        if w <= 0:
+            continue
+        ks.append(key)
+        ws.append(w)
+    if not ks:
+        return None
+    key_u = np.array([kk & M64 for kk in ks], dtype=np.uint64)
+    w = np.array(ws, dtype=np.int64)
+    x = key_u.copy()
+    out = np.zeros(max(1, H), dtype=np.int32)
+    lo = (key_u & np.uint64(M32)).astype(np.uint32).view(np.int32)
+    hi = (key_u >> np.uint64(32)).astype(np.uint32).view(np.int32)
+    wmax = int(w.max())
+    for j in range(H):
+        best = np.full(x.shape[0], LONG_MAX, dtype=np.int64)
+        for t in range(wmax):
+            act = t < w
+            xa = _xorshift_steps(x[act], 1)
+            x[act] = xa
+            v = xa.view(np.int64)
+            cur = best[act]
+            best[act] = np.where(v < cur, v, cur)
+        # strictly smaller wins: the first key (insertion order) among equal minima
+        i = int(np.argmin(best))
+        if best[i] < LONG_MAX:
+            out[j] = lo[i] if j % 2 == 0 else hi[i]
+    return out
+
+
+# ---- BottomOverlapSketch ----------------------------------------------------------------
+def ordered_sketch(s: bytes, p: dict):
+    """BottomOverlapSketch.<init>(s, k', S, false) @0-177: (hashes int32, positions int32) of
+    the S smallest k'-mer murmur3_32 hashes, in signed order; equal hashes keep position
+    order (IntArrays.radixSortIndirect(perm, hashes, stable)); duplicates stay.  Its
+    seqLength = len - k' + 1 (None when < 1)."""
+    kk, S = p["ordered_k"], p["ordered_sketch"]
+    n = len(s) - kk + 1
+    if n <= 0:
+        return None
+    h = seq_hashes_int(s, kk)
+    perm = np.argsort(h, kind="stable")[:min(S, n)]
+    return h[perm].astype(np.int32), perm.astype(np.int32), n
+
+
+class _MatchData:
+    """BottomOverlapSketch$MatchData: the recorded (pos1, pos2, shift) matches."""
+
+    def __init__(self, sl1: int, sl2: int, max_shift: float):
+        self.sl1, self.sl2, self.msp = sl1, sl2, max_shift
+        self.p1, self.p2, self.sh = [], [], []
+        self._upd = True
+        self.median = 0
+        self.absmax = 0
+
+    def reset(self):                                 # reset @0-10
+        self.p1, self.p2, self.sh = [], [], []
+        self._upd = True
+
+    def record(self, a, b, s):                       # recordMatch @66-111
+        self.p1.append(a)
+        self.p2.append(b)
+        self.sh.append(s)
+        self._upd = True
+
+    def update(self):                                # performUpdate @0-134
+        if not self._upd:
+            return
+        n = len(self.sh)
+        if n > 0:
+            # Utils.quickSelect(copy, n / 2, n): the (n/2)-th smallest
+            self.median = sorted(self.sh)[n // 2]
+            lo = max(0, -self.median)
+            hi = min(self.sl1, self.sl2 - self.median)
+            olap = max(10, hi - lo)
+            self.absmax = min(max(self.sl1, self.sl2), int(olap * self.msp))
+        else:
+            self.median = 0
+            self.absmax = max(self.sl1, self.sl2) + 1
+        self._upd = False
+
+    def valid(self):                                 # valid1/2 Lower/Upper
+        self.update()
+        m, a = self.median, self.absmax
+        return (max(0, -m - a), max(0, m - a),
+                min(self.sl1, self.sl2 - m + a), min(self.sl2, self.sl1 + m + a))
+
+    def optimize(self):                              # optimizeShifts @0-165
+        if not self.sh:
+            return
+        self.update()
+        m = self.median
+        p1, p2, sh = self.p1, self.p2, self.sh
+        prev = -1
+        for i in range(len(sh)):
+            if prev >= 0 and p1[prev] == p1[i]:
+                if abs(sh[prev] - m) > abs(sh[i] - m):
+                    p1[prev], p2[prev], sh[prev] = p1[i], p2[i], sh[i]
+            else:
+                prev += 1
+                p1[prev], p2[prev], sh[prev] = p1[i], p2[i], sh[i]
+        del p1[prev + 1:], p2[prev + 1:], sh[prev + 1:]
+        self._upd = True
+
+    def edges(self):                                 # computeEdges @0-255
+        self.update()
+        m, a = self.median, self.absmax
+        l1 = l2 = 0x7FFFFFFF
+        r1 = r2 = -0x80000000
+        c = 0
+        for x1, x2, s in zip(self.p1, self.p2, self.sh):
+            if abs(s - m) > a:
+                continue
+            l1, l2, r1, r2 = min(l1, x1), min(l2, x2), max(r1, x1), max(r2, x2)
+            c += 1
+        if c < 3:
+            return None
+        a1 = max(0, java_round((c * l1 - r1) / float(c - 1)))
+        a2 = min(self.sl1, java_round((c * r1 - l1) / float(c - 1)))
+        b1 = max(0, java_round((c * l2 - r2) / float(c - 1)))
+        b2 = min(self.sl2, java_round((c * r2 - l2) / float(c - 1)))
+        return a1, a2, b1, b2, c
+
+
+def _record_matching(md: _MatchData, s1, s2):
+    """BottomOverlapSketch.recordMatchingKmers @0-450: a merge of the two sorted sketches
+    within the valid windows of the current median shift; of a run of equal hashes on both
+    sides the first and the last pairs are recorded."""
+    v1lo, v2lo, v1hi, v2hi = md.valid()
+    m, amax = md.median, md.absmax
+    h1s, p1s = s1
+    h2s, p2s = s2
+    n1, n2 = len(h1s), len(h2s)
+    i1 = i2 = 0
+    md.reset()
+    while i1 < n1 and i2 < n2:
+        h1, p1 = int(h1s[i1]), int(p1s[i1])
+        h2, p2 = int(h2s[i2]), int(p2s[i2])
+        if h1 < h2 or p1 < v1lo or p1 >= v1hi:
+            i1 += 1
+            continue
+        if h2 < h1 or p2 < v2lo or p2 >= v2hi:
+            i2 += 1
+            continue
+        s = p2 - p1
+        d = s - m
+        if d > amax:
+            i1 += 1
+            continue
+        if d < -amax:
+            i2 += 1
+            continue
+        md.record(p1, p2, s)
+        l1 = i1
+        j = i1 + 1
+        while j < n1 and int(h1s[j]) == h1 and v1lo <= int(p1s[j]) < v1hi:
+            l1 = j
+            j += 1
+        l2 = i2
+        j = i2 + 1
+        while j < n2 and int(h2s[j]) == h2 and v2lo <= int(p2s[j]) < v2hi:
+            l2 = j
+            j += 1
+        if i1 == l1 and i2 == l2:
+            i1 += 1
+            i2 += 1
+        else:
+            a, b = int(p1s[l1]), int(p2s[l2])
+            md.record(a, b, b - a)
+            i1, i2 = l1 + 1, l2 + 1
+
+
+def overlap_info(A, B, max_shift: float, kk: int):
+    """BottomOverlapSketch.getOverlapInfo(other, maxShift) @0-211: None (EMPTY) or
+    (score, raw, a1, a2, b1, b2).  A, B = (hashes, positions, seqLength)."""
+    md = _MatchData(A[2], B[2], max_shift)
+    _record_matching(md, A[:2], B[:2])
+    if not md.sh:
+        return None
+    _record_matching(md, A[:2], B[:2])
+    if not md.sh:
+        return None
+    md.optimize()
+    if not md.sh:
+        return None
+    e = md.edges()
+    if e is None:
+        return None
+    a1, a2, b1, b2, c = e
+    # computeKBottomSketchJaccard @0-227 (entries of each sketch inside its edge range)
+    sel1 = [(int(h), int(q)) for h, q in zip(A[0], A[1]) if a1 <= q <= a2]
+    sel2 = [(int(h), int(q)) for h, q in zip(B[0], B[1]) if b1 <= q <= b2]
+    n = min(len(sel1), len(sel2))
+    if n == 0:
+        J = 0.0
+    else:
+        i = j = inter = 0
+        for _ in range(n):
+            if sel1[i][0] < sel2[j][0]:
+                i += 1
+            elif sel1[i][0] > sel2[j][0]:
+                j += 1
+            else:
+                inter += 1
+                i += 1
+                j += 1
+        J = inter / float(n)
+    # jaccardToIdentity @0-25: exp(-(-1/k * ln(2J / (1 + J))))
+    if J > 0.0:
+        d = (-1.0 / kk) * math.log(2.0 * J / (1.0 + J))
+        score = math.exp(-d)
+    else:
+        score = 0.0
+    return score, float(c), a1, a2, b1, b2
+
+
+MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("raw", "<f8"),
+                       ("a_bgn", "<i4"), ("a_end", "<i4"), ("a_len", "<i4"), ("o", "<u4"),
+                       ("b_bgn", "<i4"), ("b_end", "<i4"), ("b_len", "<i4")])
+
+
+def sketch_read(s: bytes, p: dict, fc):
+    """SequenceSketch.<init> for one strand: (minhash, ordered) or None (skipped read)."""
+    mh = minhash(s, p, fc)
+    if mh is None:
+        return None
+    osk = ordered_sketch(s, p)
+    if osk is None:
+        return None
+    return mh, osk
+
+
+def read_bytes(rs, i: int) -> bytes:
+    o, L = int(rs.offsets[i]), int(rs.lengths[i])
+    return rs.bases[o:o + L].tobytes().upper()
+
+
+def sketches(rs, p: dict, fc=None, reads=None):
+    """{(read index, strand 0 fwd / 1 rc): (minhash, ordered, length)} for the reads the
+    streamer keeps (>= min_olap bases, sketchable)."""
+    out = {}
+    for i in (range(rs.nreads) if reads is None else reads):
+        L = int(rs.lengths[i])
+        if L < p["min_olap"]:
+            continue
+        s = read_bytes(rs, i)
+        f = sketch_read(s, p, fc)
+        if f is None:
+            continue
+        out[(i, 0)] = (f[0], f[1], L)
+        if not p.get("no_rc", False):
+            r = sketch_read(rc(s), p, fc)
+            if r is not None:
+                out[(i, 1)] = (r[0], r[1], L)
+    return out
+
+
+def find_matches(q_id, q, store: dict, p: dict, to_self: bool):
+    """MinHashSearch.findMatches(query, toSelf) @0-610: the stored sketches sharing at
+    least --num-min-matches min-mers with the query (per hash function j: query[j] equal
+    to the stored sketch's [j]), then the length / self rules and the second stage.
+    Returns [(target id, overlap info)] for accepted targets."""
+    out = []
+    qmh, qosk, qlen = q
+    ms = p["min_store"]
+    for t_id, (tmh, tosk, tlen) in store.items():
+        if to_self and t_id[0] == q_id[0]:
+            continue
+        cnt = int((qmh == tmh).sum())
+        if cnt < p["min_matches"]:
+            continue
+        if tlen < ms and qlen < ms:                          # @393-416
+            continue
+        if to_self and t_id[0] > q_id[0] and tlen >= ms and qlen >= ms:   # @419-462
+            continue
+        if to_self and tlen < ms and qlen >= ms:             # @465-492
+            continue
+        oi = overlap_info(qosk, tosk, p["max_shift"], p["ordered_k"])
+        if oi is None:
+            continue
+        if oi[0] >= p["threshold"]:
+            out.append((t_id, oi))
+    return out
+
+
+def match_record(q_id, t_id, oi, qlen: int, tlen: int, first_iid: int):
+    """MatchResult.<init> @0-179: reverse-strand coordinates mirrored as len - x - 1, the
+    score capped at 1; the row of MatchResult.toString."""
+    score, raw, a1, a2, b1, b2 = oi
+    if q_id[1]:
+        a1, a2 = qlen - a2 - 1, qlen - a1 - 1
+    if t_id[1]:
+        b1, b2 = tlen - b2 - 1, tlen - b1 - 1
+    score = min(score, 1.0)
+    return (first_iid + q_id[0], first_iid + t_id[0], 1.0 - score, raw, a1, a2, qlen,
+            t_id[1], b1, b2, tlen)
+
+
+def run_self(rs, p: dict, freq=None) -> np.ndarray:
+    """The jar's -s block against itself: every stored forward sketch as a query
+    (AbstractMatchSearch.findMatches() over getStoredForwardSequenceIds), toSelf = true.
+    Rows sorted by (a, b, o)."""
+    fc = FrequencyCounts(freq[0], freq[1], p) if freq is not None else None
+    store = sketches(rs, p, fc)
+    rows = []
+    for q_id in sorted(k for k in store if k[1] == 0):
+        for t_id, oi in find_matches(q_id, store[q_id], store, p, True):
+            rows.append(match_record(q_id, t_id, oi, store[q_id][2], store[t_id][2],
+                                     rs.first_iid))
+    a = np.array(rows, dtype=MHAP_DTYPE)
+    return a[np.lexsort((a["o"], a["b"], a["a"]))] if a.size else a

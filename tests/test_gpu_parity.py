@@ -215,7 +215,10 @@ def test_long_read_among_short(built):
     _, st_short = run(short)
     both = _concat(short, long_)
     got, st = run(both)
-    assert st["ext_waves"] == st_short["ext_waves"] and st["stage_len"] == st_short["stage_len"]
+    # the staged class holds overlap SPANS (not whole reads) since round 6: with the long
+    # read present its span cap grows to the class's LDS limit, at unchanged occupancy
+    assert st["ext_waves"] == st_short["ext_waves"]
+    assert st_short["stage_len"] == 3000 and st["stage_len"] >= st_short["stage_len"]
     assert st["generic_pairs"] > 0
     want = oracle.run_oracle(both, P.as_dict())
     assert got.shape == want.shape and np.array_equal(got, want)
