@@ -2,9 +2,10 @@
 """bench_mhap.py -- the MHAP stage on MI355X: overlaps/sec on BASELINE configs[3]
 (200k synthetic raw-ONT-like reads x 15 kb, MinHash sketch + two-stage filter).
 
-One step = one whole MHAP job over the resident read set: sketch every read (MinHash and
-ordered sketches), build the MinHash index, compare every query against every later read
-(each pair once).  With --gpus N (torchrun, one process per GPU): every rank generates 1/N
+One step = one whole MHAP job over the resident read set, the jar's self search (MHAP 2.1.2
+semantics, restated from its bytecode in oracle/mhap_jar.py): sketch both strands of every
+read (MinHash and ordered sketches), build the MinHash index over all strands, compare every
+read's forward strand against the stored strands of smaller IDs (each pair once).  With --gpus N (torchrun, one process per GPU): every rank generates 1/N
 of the reads and the read store is all-gathered at setup (as bench.py does); in the timed
 step each rank sketches its 1/N of the reads, the sketch rows are ALL-GATHERED over RCCL
 (xGMI) -- the shared MinHash index of BASELINE configs[3] -- every rank sorts the index and
@@ -46,10 +47,11 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--weighting", choices=("canu", "none"), default="canu",
                     help="canu: --repeat-weight 0.9 --repeat-idf-scale 10 with a -f table "
-                         "(OverlapMhap.pm:382); none: MHAP 1.x unweighted sketches")
+                         "(OverlapMhap.pm:382); none: --repeat-weight -1 (the jar's "
+                         "unweighted MinHash), no table")
     ap.add_argument("--freq-kmers", type=int, default=100_000,
                     help="-f table size (16-mers sampled from the reads, graded fractions)")
-    ap.add_argument("--cpu-sample-reads", type=int, default=300)
+    ap.add_argument("--cpu-sample-reads", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args(argv)
 
@@ -142,15 +144,19 @@ def main() -> None:
     if args.weighting == "canu":
         P.canu_weighting()
         freq = freq_table(genome, args.freq_kmers, P.k, args.seed)
+    else:
+        P.repeat_weight = -1.0
     m = Mhap(P, device=local)
     m.load_reads_device(1, bases.data_ptr(), d_offsets.data_ptr(), lengths)
     if freq is not None:
         m.set_kmer_frequencies(*freq)
+    else:
+        m.set_weighting()
     H, S = P.num_hashes, P.ordered_sketch_size
-    if world > 1:
-        mh_l = torch.empty((hi - lo, H), dtype=torch.int32, device=dev)
-        od_l = torch.empty((hi - lo, S), dtype=torch.int64, device=dev)
-        oc_l = torch.empty((hi - lo,), dtype=torch.int32, device=dev)
+    if world > 1:                       # rows per read: both strands (canu_mhap.h)
+        mh_l = torch.empty((hi - lo, 2 * H), dtype=torch.int32, device=dev)
+        od_l = torch.empty((hi - lo, 2 * S), dtype=torch.int64, device=dev)
+        oc_l = torch.empty((hi - lo, 2), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     q_lo, q_hi = query_shards(n, world)[rank]
     setup_s = time.time() - t_setup
@@ -209,18 +215,21 @@ def main() -> None:
     value = total_ovl * args.steps / elapsed
     gbp = total_bases / 1e9
 
-    # Dominant kernel: the MinHash sketch kernel (k_mh_sketch_w with canu's weighting, else
-    # k_mh_sketch), its launches timed live by the library's events (ms_sketch_kernel, ABI 5).
-    # It is bound by vector-instruction issue (~9.5 VALU per xorshift64 draw, DESIGN.md
-    # round 5): with the PMC pass of this workload and these sources (profiles/
-    # traffic_mhap.json) the roofline is VALU wave-instructions/s against 1,024 SIMDs x
-    # 2.4 GHz / 2 (wave64 over 2 cycles); its HBM figures beside: algorithmic bytes = the
-    # sorted k-mer keys read once (4 B per k-mer) + the sketch rows written (4 B x H per read).
-    kmers = st["sketch_kmers"]
+    # Dominant kernel: the MinHash draw kernel k_mh_minhash (its launches timed live by the
+    # library's events, ms_sketch_kernel).  It is bound by vector-instruction issue: every
+    # distinct k-mer of both strands makes w x H xorshift64 draws, each a 64-bit
+    # shift / xor chain and a signed 64-bit minimum.  With the PMC pass of this
+    # workload and these sources (profiles/traffic_mhap.json) the roofline is VALU
+    # wave-instructions/s against 1,024 SIMDs x 2.4 GHz / 2 (wave64 over 2 cycles); its HBM
+    # figures beside: algorithmic bytes = the sorted (key, position) pairs read once (12 B
+    # per k-mer position) + the sketch rows written (4 B x H per strand).
+    draws = int(st.get("sketch_draws", 0))
     nl = max(int(st.get("sketch_launches", 0)), 1)
     k_ms = st.get("ms_sketch_kernel", 0.0) / nl
-    kname = "k_mh_sketch_w" if args.weighting == "canu" else "k_mh_sketch"
-    per_launch = (4.0 * kmers + 4.0 * H * (hi - lo)) / nl
+    kname = "k_mh_minhash"
+    strands = 2 * (hi - lo)
+    positions = max(0, int(np.maximum(lengths[lo:hi].astype(np.int64) - P.k + 1, 0).sum())) * 2
+    per_launch = (12.0 * positions + 4.0 * H * strands) / nl
     pmc, pmc_note = load_pmc(args, world)
     kp = (pmc or {}).get(kname, {})
     hbm = {"achieved": round(per_launch / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,
@@ -230,6 +239,8 @@ def main() -> None:
     if hbm["achieved"] is not None:
         hbm["frac"] = round(hbm["achieved"] / HBM_PEAK_GBS, 5)
     roof = {"kernel": kname, "launches": nl, "avg_launch_ms": round(k_ms, 3),
+            "draws_per_launch": draws // nl,
+            "g_draws_per_s": round(draws / nl / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,
             "pmc_source": pmc_note}
     if kp and k_ms > 0:
         valu = kp["valu_insts"] / (k_ms * 1e-3) / 1e9
@@ -237,9 +248,10 @@ def main() -> None:
         roof.update({"bound": "issue", "achieved": round(valu, 1), "peak": round(pk, 1),
                      "unit": "G VALU wave-instructions/s", "frac": round(valu / pk, 4),
                      "traffic": kp.get("hbm_bytes_per_launch"), "hbm": hbm,
+                     "valu_per_draw": round(kp["valu_insts"] * 64.0 / max(draws / nl, 1.0), 2),
                      "wait_inst_any_frac": round(kp.get("wait_inst_any_frac", 0.0), 3),
                      "limiter": "vector-instruction issue: the xorshift64 draws of the "
-                                "weighted MinHash (H functions x w draws per distinct k-mer)"})
+                                "weighted MinHash (w x H per distinct k-mer and strand)"})
     else:
         roof.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": hbm.get("frac"), "traffic": None,
@@ -273,12 +285,13 @@ def main() -> None:
             "gbp_vs_gbp_per_sec": round(gbp * gbp / 2.0 * args.steps / elapsed, 3),
             "breakdown_ms": {k: round(v / args.steps, 2) for k, v in ms.items()},
             "setup_s": round(setup_s, 1), "roofline": roof, "cpu_baseline": cpu,
-            "parity": {"checked": False, "pinned": False,
-                       "reason": "parity with the MHAP jar is unpinned (the reference ships "
-                                 "only the prebuilt jar, no fixtures; no JVM here): the GPU is "
-                                 "bit-exact to the restatement oracle/mhap_oracle.py "
-                                 "(tests/test_mhap.py), whose weighted sketch is restated from "
-                                 "the published MHAP 2.x algorithm (DESIGN.md)"},
+            "sketch": {"kmers": int(st["sketch_kmers"]), "draws": draws,
+                       "reads_used": int(st["sketched_reads"])},
+            "parity": {"checked": False, "pinned": "bytecode",
+                       "reason": "the GPU is bit-exact to oracle/mhap_jar.py "
+                                 "(tests/test_mhap.py), the jar's bytecode restated method by "
+                                 "method; no jar output exists to pin against (no JVM, no "
+                                 "fixtures in the reference)"},
         }
         print(json.dumps(line), flush=True)
     m.close()
@@ -302,11 +315,11 @@ def freq_table(genome, n: int, k: int, seed: int):
 
 
 def cpu_baseline(args, P, freq=None) -> dict | None:
-    """The numpy restatement (oracle/mhap_oracle.py, one core) on a bounded sample of the
-    same workload: fewer reads, same read length / error / coverage."""
+    """The numpy restatement of the jar (oracle/mhap_jar.py, one core) on a bounded sample of
+    the same workload: fewer reads, same read length / error / coverage / weighting."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
-        import mhap_oracle
+        import mhap_jar
         from canu_amd.synth import synth_reads
     except Exception:
         return None
@@ -314,7 +327,7 @@ def cpu_baseline(args, P, freq=None) -> dict | None:
     gl = int(ns * args.read_len / args.coverage)
     rs = synth_reads(ns, args.read_len, gl, args.read_error, seed=args.seed + 1000)
     t0 = time.perf_counter()
-    rec = mhap_oracle.run(rs, P.as_oracle(), freq=freq)
+    rec = mhap_jar.run(rs, P.as_oracle(), freq=freq)
     secs = time.perf_counter() - t0
     return {"value": round(len(rec) / secs, 2), "unit": "overlaps/s", "cores": 1,
             "kind": "port",

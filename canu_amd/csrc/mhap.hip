@@ -1,31 +1,36 @@
-// mhap.hip -- MHAP's MinHash sketch / filter stage on gfx950, behind include/canu_mhap.h.
+// mhap.hip -- MHAP 2.1.2's sketch / two-stage filter on gfx950, behind include/canu_mhap.h.
 //
 // Replaces the MHAP jar canu runs for overlapper=mhap (src/pipelines/canu/OverlapMhap.pm:
-// precompute :374-399, compare :476-498); output keeps MHAP's text line, which
-// src/mhap/mhapConvert.C:114-150 converts to ovOverlap records.  The algorithm is
-// specified in oracle/mhap_oracle.py (the CPU restatement; parity against the jar itself is
-// unpinned -- see DESIGN.md), and implemented here with the same integer arithmetic:
+// precompute :374-399, compare :476-498); the text line it writes is MatchResult.toString's,
+// which src/mhap/mhapConvert.C:114-150 converts to ovOverlap records.  What the jar computes
+// was read from its bytecode and is restated, method by method, in oracle/mhap_jar.py (the
+// parity checker); the kernels below compute the same integers:
 //
-//   k_mh_sketch    one block per read: MinHash sketch.  Each thread rolls 16 consecutive
-//                  k-mers into registers (canonical 2-bit codes -> splitmix64), then walks the
-//                  H xorshift64 hash functions; per function the block's minimum is a DPP
-//                  wave reduction + one LDS update per wave.  Integer-VALU bound.
-//   k_mh_ordered   one block per read: the ordered (second-stage) sketch -- a 4096-bin
-//                  histogram of the k'-mer hashes picks the bins that hold the S smallest,
-//                  those entries are collected and bitonic-sorted in LDS, deduplicated,
-//                  the first S kept.
-//   index          (j, value) -> read pairs sorted by hipcub radix sort, per-table offsets.
-//   k_mh_candidates one wave per query: binary-search its H values in their tables, count
-//                  matches per target in an LDS open-addressing table, emit targets with
-//                  count >= min_matches.
-//   k_mh_compare   one wave per candidate: merge the two ordered sketches (binary search in
-//                  LDS), vote the orientation, radix-select the median offset, count the
-//                  sketch entries inside the implied overlap, Jaccard -> Mash distance.
+//   k_mh_ordered   one block per strand: BottomOverlapSketch -- Murmur3_x86_32 of every
+//                  k'-mer's UTF-16 chars; the S smallest (hash, position) keys by a 4096-bin
+//                  radix select (one histogram pass in practice, deeper digits when a bin
+//                  overflows LDS), then a bitonic sort of the selected keys in LDS.
+//   k_mh_keys      Murmur3_x64_128 h1 of every k-mer of every strand (the MinHash keys);
+//                  a segmented radix sort (hipcub) makes each strand's keys runs: a run is a
+//                  distinct k-mer, its length the count, its first value the first position.
+//   k_mh_minhash   one block per strand over its sorted keys: per distinct k-mer the weight
+//                  w (tf-idf), then for every hash function j, w xorshift64 draws of the
+//                  k-mer's chain; the signed-smallest draw (earliest first occurrence on ties)
+//                  stores the key's low / high 32 bits.  Integer-VALU bound (the draws).
+//   index          (j, value) -> stored strand, hipcub radix sort, per-function offsets.
+//   k_mh_candidates one wave per query: its forward row's H values looked up, matches counted
+//                  per stored strand in an LDS table, the self / length rules of
+//                  MinHashSearch.findMatches applied, >= min_matches emitted.
+//   k_mh_compare   one wave per candidate: BottomOverlapSketch.getOverlapInfo.  The jar's
+//                  sequential merge (recordMatchingKmers) decomposes into independent groups
+//                  of equal hashes, so lanes take groups; the three medians are radix
+//                  selects over regenerated records; the final bottom-sketch Jaccard merge is
+//                  evaluated in closed form from per-group counts and prefix sums.
 #include <hip/hip_runtime.h>
-#include <type_traits>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <charconv>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -39,670 +44,116 @@
 
 namespace mh {
 
-constexpr int32_t I32MAX = 0x7FFFFFFF;
-constexpr int RK = 32;            // k-mers per thread per round in k_mh_sketch
-constexpr int OCAP = 4096;        // collected ordered-sketch entries per read (LDS)
-constexpr int NBIN = 4096;        // histogram bins (hash >> 20)
-constexpr int TSLOTS = 1024;      // candidate table slots per wave
-constexpr int TSHIFT = 22;        // 32 - log2(TSLOTS)
+constexpr int64_t LMAX = 0x7FFFFFFFFFFFFFFFll;
+constexpr int OCAP = 4096;        // ordered-sketch keys collected per strand (LDS)
+constexpr int NBIN = 4096;        // radix-select bins (12-bit digits)
+constexpr int TSLOTS = 2048;      // candidate table slots per wave
+constexpr int TSHIFT = 21;        // 32 - log2(TSLOTS)
+constexpr int RKW = 8;            // distinct k-mers per thread per round in k_mh_minhash
+constexpr int RKK = 16;           // positions per thread in k_mh_keys
 
 struct Cand {
-  uint32_t q, t, cnt, pad;
+  uint32_t q, t, cnt, pad;        // query read, stored strand (2 r + rc), shared entries
 };
 
 struct RecDev {
-  uint32_t a, b;
-  double erate;
-  uint32_t count;
-  int32_t a_bgn, a_end, a_len;
-  uint32_t o;
-  int32_t b_bgn, b_end, b_len;
+  uint32_t a, b;                  // reads (0-based in the context)
+  uint32_t o, cnt;                // b strand, first-stage count
+  uint32_t inter, n, raw, pad;    // Jaccard numerator / denominator, edges count
+  int32_t a1, a2, a_len, b1, b2, b_len;
 };
 
-__device__ __host__ __forceinline__ uint64_t splitmix64(uint64_t c) {
-  uint64_t z = c + 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
+// Utils$Translate (Utils.rc): the complement of an upper-case IUPAC byte, 0 for the rest
+__constant__ uint8_t c_comp[256];
+
+__device__ __host__ __forceinline__ uint32_t upper_byte(uint32_t b) {
+  return (b >= 'a' && b <= 'z') ? b - 32u : b;
 }
 
-__device__ __forceinline__ uint32_t base_code(uint8_t b) {
-  b |= 0x20;
-  return b == 'a' ? 0u : b == 'c' ? 1u : b == 'g' ? 2u : b == 't' ? 3u : 255u;
-}
-
-__device__ __forceinline__ int32_t wave_min(int32_t v) {
-  int32_t t;
-  t = __builtin_amdgcn_update_dpp(I32MAX, v, 0x111, 0xf, 0xf, false); v = v < t ? v : t;
-  t = __builtin_amdgcn_update_dpp(I32MAX, v, 0x112, 0xf, 0xf, false); v = v < t ? v : t;
-  t = __builtin_amdgcn_update_dpp(I32MAX, v, 0x114, 0xf, 0xf, false); v = v < t ? v : t;
-  t = __builtin_amdgcn_update_dpp(I32MAX, v, 0x118, 0xf, 0xf, false); v = v < t ? v : t;
-  t = __builtin_amdgcn_update_dpp(I32MAX, v, 0x142, 0xa, 0xf, false); v = v < t ? v : t;
-  t = __builtin_amdgcn_update_dpp(I32MAX, v, 0x143, 0xc, 0xf, false); v = v < t ? v : t;
-  return __builtin_amdgcn_readlane(v, 63);
-}
-
-// Rolling canonical k-mer over a read: push one base, report whether the k-mer ending at
-// the pushed base is valid (no non-ACGT byte among its k bases).
-struct Roller {
-  uint64_t fwd = 0, rc = 0, mask;
-  int32_t k, since_bad;         // bases pushed since the last bad one
-  __device__ Roller(int32_t k_) : k(k_), since_bad(0) {
-    mask = (k_ >= 32) ? ~0ull : ((1ull << (2 * k_)) - 1);
+// One strand of a read as the jar sees it: the forward string, or Utils.rc of it
+struct Strand {
+  const uint8_t *s;
+  int32_t L;
+  int32_t rc;
+  __device__ __forceinline__ uint64_t ch(int32_t p) const {
+    return rc ? (uint64_t)c_comp[upper_byte(s[L - 1 - p])] : (uint64_t)upper_byte(s[p]);
   }
-  __device__ __forceinline__ bool push(uint32_t c) {
-    if (c > 3) {
-      since_bad = 0;
-      c = 0;
-    } else {
-      since_bad++;
-    }
-    fwd = ((fwd << 2) | c) & mask;
-    rc = (rc >> 2) | ((uint64_t)(3 - c) << (2 * (k - 1)));
-    return since_bad >= k;
-  }
-  __device__ __forceinline__ uint64_t canon() const { return fwd < rc ? fwd : rc; }
-  __device__ __forceinline__ uint32_t strand() const { return rc < fwd ? 1u : 0u; }
 };
 
-struct SketchArgs {
-  const uint8_t *bases;
-  const uint64_t *off;
-  const uint32_t *len;
-  uint32_t r0;                  // first read (0-based) of this launch
-  uint32_t nreads;
-  int32_t k, H;
-  const uint64_t *filter;       // sorted canonical codes, or null
-  uint32_t nfilter;
-  int32_t *minhash;             // [read][H]
-  unsigned long long *kmers;    // hashed k-mers (stats)
-};
-
-__device__ __forceinline__ bool filtered(const uint64_t *f, uint32_t n, uint64_t c) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (f[mid] < c) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo < n && f[lo] == c;
+__device__ __host__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
 }
 
-// One xorshift64 step (<<21, >>35, <<4) on the state's two 32-bit halves.  64-bit shifts
-// (v_lshlrev_b64) measured faster than a v_alignbit split of the same step (108 vs 129 ms
-// for the 50k-read sketch).
-__device__ __forceinline__ void xs64(uint32_t &lo, uint32_t &hi) {
-  uint64_t x = ((uint64_t)hi << 32) | lo;
-  x ^= x << 21;
-  x ^= x >> 35;
-  x ^= x << 4;
-  lo = (uint32_t)x;
-  hi = (uint32_t)(x >> 32);
+__device__ __host__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xFF51AFD7ED558CCDull;
+  k ^= k >> 33;
+  k *= 0xC4CEB9FE1A85EC53ull;
+  k ^= k >> 33;
+  return k;
 }
 
-// One xorshift64 step of N independent chains, each sub-step over all chains before the
-// next (shift results in their own registers): written chain by chain, the compiler emitted
-// every chain's 9 instructions back to back, each on the previous one's result.  On the
-// configs[3] sketch 845 -> 831 ms (profiles/r05h_mhap_xorshift_ab.txt, sketches equal); the
-// kernel is VALU-bound on the draws themselves (~9.5 VALU per draw, the PMC's count:
-// profiles/r05f_mhap_pmc.txt), so interleaving gains little
-template <int N>
-__device__ __forceinline__ void xs64_n(uint32_t (&lo)[N], uint32_t (&hi)[N]) {
-  uint64_t x[N];
-#pragma unroll
-  for (int i = 0; i < N; i++) x[i] = ((uint64_t)hi[i] << 32) | lo[i];
-  uint64_t t[N];
-#pragma unroll
-  for (int i = 0; i < N; i++) t[i] = x[i] << 21;
-#pragma unroll
-  for (int i = 0; i < N; i++) x[i] ^= t[i];
-#pragma unroll
-  for (int i = 0; i < N; i++) t[i] = x[i] >> 35;
-#pragma unroll
-  for (int i = 0; i < N; i++) x[i] ^= t[i];
-#pragma unroll
-  for (int i = 0; i < N; i++) t[i] = x[i] << 4;
-#pragma unroll
-  for (int i = 0; i < N; i++) x[i] ^= t[i];
-#pragma unroll
-  for (int i = 0; i < N; i++) { lo[i] = (uint32_t)x[i]; hi[i] = (uint32_t)(x[i] >> 32); }
+// Guava Hashing.murmur3_128(0).hashUnencodedChars(kmer).asLong(): MurmurHash3_x64_128 of
+// the chars as little-endian UTF-16, first 8 bytes (h1)  (HashUtils.computeSequenceHashesLong
+// @0-108; oracle mhap_jar.murmur3_128_h1)
+template <class CH>
+__device__ __host__ __forceinline__ uint64_t murmur128_h1(CH ch, int32_t k) {
+  const uint64_t c1 = 0x87C37B91114253D5ull, c2 = 0x4CF5AD432745937Full;
+  uint64_t h1 = 0, h2 = 0;
+  const int32_t nb = k >> 3;
+  int32_t q = 0;
+  for (int32_t b = 0; b < nb; b++, q += 8) {
+    uint64_t k1 = ch(q) | (ch(q + 1) << 16) | (ch(q + 2) << 32) | (ch(q + 3) << 48);
+    uint64_t k2 = ch(q + 4) | (ch(q + 5) << 16) | (ch(q + 6) << 32) | (ch(q + 7) << 48);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52DCE729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495AB5;
+  }
+  const int32_t t = k - 8 * nb;
+  if (t > 4) {
+    uint64_t k2 = 0;
+    for (int32_t j = 0; j < t - 4; j++) k2 |= ch(q + 4 + j) << (16 * j);
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  if (t > 0) {
+    uint64_t k1 = 0;
+    for (int32_t j = 0; j < (t < 4 ? t : 4); j++) k1 |= ch(q + j) << (16 * j);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(2 * k);
+  h2 ^= (uint64_t)(2 * k);
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  return h1 + h2;
 }
 
-// Stage 1 (oracle: mhap_oracle.sketch)
-__global__ void __launch_bounds__(256) k_mh_sketch(SketchArgs A) {
-  extern __shared__ int32_t s_min[];               // [4 waves][H]
-  const uint32_t r = A.r0 + blockIdx.x;
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int32_t H = A.H, k = A.k;
-  for (int32_t j = tid; j < 4 * H; j += 256) s_min[j] = I32MAX;
-  __syncthreads();
-  const uint8_t *s = A.bases + A.off[r];
-  const int32_t L = (int32_t)A.len[r];
-  const int32_t npos = L - k + 1;                  // k-mer start positions
-  unsigned long long nk = 0;
-  for (int32_t base = 0; base < npos; base += 256 * RK) {
-    const int32_t p0 = base + (int32_t)tid * RK;   // this thread: starts p0 .. p0+RK-1
-    uint64_t X[RK];
-    uint32_t vm = 0;
-    if (p0 < npos) {
-      Roller R(k);
-      for (int32_t i = 0; i < k - 1; i++) R.push(base_code(s[p0 + i]));
-#pragma unroll
-      for (int i = 0; i < RK; i++) {
-        X[i] = 0;
-        const int32_t p = p0 + i;
-        if (p < npos) {
-          bool ok = R.push(base_code(s[p + k - 1]));
-          uint64_t c = R.canon();
-          if (ok && A.filter && filtered(A.filter, A.nfilter, c)) ok = false;
-          if (ok) {
-            X[i] = splitmix64(c);
-            vm |= 1u << i;
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < RK; i++) X[i] = 0;
-    }
-    nk += __builtin_popcount(vm);
-    if (__builtin_amdgcn_ballot_w64(vm != 0) == 0) continue;   // wave has nothing here
-    // invalid slots take a copy of a valid k-mer's state (min is idempotent), so the
-    // per-function loop needs no per-slot masking; a thread with no valid k-mer at all
-    // contributes INT32_MAX
-    {
-      uint64_t x0 = 0;
-#pragma unroll
-      for (int i = RK - 1; i >= 0; i--) x0 = (vm >> i) & 1u ? X[i] : x0;
-#pragma unroll
-      for (int i = 0; i < RK; i++) X[i] = (vm >> i) & 1u ? X[i] : x0;
-    }
-    const bool live = vm != 0;
-    int32_t *wm = s_min + wave * H;
-    uint32_t XL[RK], XH[RK];
-#pragma unroll
-    for (int i = 0; i < RK; i++) { XL[i] = (uint32_t)X[i]; XH[i] = (uint32_t)(X[i] >> 32); }
-    for (int32_t j = 0; j < H; j++) {
-      int32_t v[RK];
-#pragma unroll
-      for (int i = 0; i < RK; i++) {
-        xs64(XL[i], XH[i]);
-        v[i] = (int32_t)XL[i];
-      }
-      // min over the slots as a min3 tree
-      int32_t m = v[0];
-#pragma unroll
-      for (int i = 1; i + 1 < RK; i += 2) {
-        const int32_t a = v[i] < v[i + 1] ? v[i] : v[i + 1];
-        m = m < a ? m : a;
-      }
-      if ((RK & 1) == 0) m = m < v[RK - 1] ? m : v[RK - 1];
-      m = live ? m : I32MAX;
-      m = wave_min(m);
-      if (lane == 0 && m < wm[j]) wm[j] = m;
-    }
-  }
-  __syncthreads();
-  for (int32_t j = tid; j < H; j += 256) {
-    int32_t m = s_min[j];
-    for (int w = 1; w < 4; w++) m = s_min[w * H + j] < m ? s_min[w * H + j] : m;
-    A.minhash[(size_t)r * H + j] = m;
-  }
-  if (A.kmers) {
-    for (int s2 = 32; s2 > 0; s2 >>= 1) nk += __shfl_xor(nk, s2);
-    if (lane == 0 && nk) atomicAdd(A.kmers, nk);
-  }
-}
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
-// ---- weighted MinHash (MHAP 2.x tf-idf repeat weighting, restated; canu_mhap.h) --------
-// Each distinct k-mer of a read counts once with weight w >= 1 (w draws of its xorshift64
-// chain per hash function), so the reads' k-mers are first made distinct and counted:
-//   k_mh_kmer_keys  one block per read: (read index << 2k | canonical code) per valid k-mer
-//                   (a sentinel for the rest), RKK consecutive positions per thread
-//   radix sort      of the batch's keys (hipcub): each read's k-mers contiguous, equal
-//                   k-mers adjacent -- tf is a run length
-//   k_mh_sketch_w   one block per read over its sorted run: run starts only, weight from
-//                   the run length and the -f table, then the sketch loop of k_mh_sketch
-//                   with w draws per slot and function
-constexpr int RKK = 16;           // positions per thread in k_mh_kmer_keys
-#ifndef MH_RKW
-#define MH_RKW 8
-#endif
-constexpr int RKW = MH_RKW;       // distinct k-mers per thread per round in k_mh_sketch_w
-
-struct KeyArgs {
-  const uint8_t *bases;
-  const uint64_t *off;
-  const uint32_t *len;
-  uint32_t r0, nreads;
-  int32_t k;
-  const uint64_t *koff;         // per read of the batch: its first key
-  uint64_t sentinel;            // key of an invalid position (sorts after every real key)
-  void *keys;                   // K[]
-  uint32_t *vcnt;               // 32-bit keys: valid k-mers per read
-  unsigned long long *kmers;
-};
-
-// K = uint32_t (2k <= 32): each read's keys are its codes, sorted per read (segmented
-// sort); K = uint64_t: read index << 2k | code, one sort over the batch.  4^k - 1 (all T)
-// is never a canonical code, so it can mark an invalid position in the 32-bit form.
-template <typename K>
-__global__ void __launch_bounds__(256) k_mh_kmer_keys(KeyArgs A) {
-  const uint32_t ri = blockIdx.x, r = A.r0 + ri;
-  const int32_t k = A.k;
-  const uint8_t *s = A.bases + A.off[r];
-  const int32_t L = (int32_t)A.len[r];
-  const int32_t npos = L - k + 1;
-  K *out = (K *)A.keys + A.koff[ri];
-  const uint64_t hi = sizeof(K) == 8 ? ((uint64_t)ri << (2 * k)) : 0;
-  unsigned long long nk = 0;
-  for (int32_t base = 0; base < npos; base += 256 * RKK) {
-    const int32_t p0 = base + (int32_t)threadIdx.x * RKK;
-    if (p0 >= npos) continue;
-    Roller R(k);
-    for (int32_t i = 0; i < k - 1; i++) R.push(base_code(s[p0 + i]));
-#pragma unroll
-    for (int i = 0; i < RKK; i++) {
-      const int32_t p = p0 + i;
-      if (p < npos) {
-        const bool ok = R.push(base_code(s[p + k - 1]));
-        out[p] = ok ? (K)(hi | R.canon()) : (K)A.sentinel;
-        nk += ok;
-      }
-    }
+// Guava Hashing.murmur3_32(0) of the chars as UTF-16 (HashUtils.computeSequenceHashes
+// @0-106; oracle mhap_jar.murmur3_32)
+__device__ __forceinline__ uint32_t murmur32(const Strand &S, int32_t p, int32_t k) {
+  const uint32_t c1 = 0xCC9E2D51u, c2 = 0x1B873593u;
+  uint32_t h = 0;
+  const int32_t nb = k >> 1;
+  for (int32_t b = 0; b < nb; b++) {
+    uint32_t kk = (uint32_t)S.ch(p + 2 * b) | ((uint32_t)S.ch(p + 2 * b + 1) << 16);
+    kk *= c1; kk = rotl32(kk, 15); kk *= c2;
+    h ^= kk;
+    h = rotl32(h, 13); h = h * 5 + 0xE6546B64u;
   }
-  for (int s2 = 32; s2 > 0; s2 >>= 1) nk += __shfl_xor(nk, s2);
-  if ((threadIdx.x & 63) == 0 && nk) {
-    if (A.kmers) atomicAdd(A.kmers, nk);
-    if (sizeof(K) == 4) atomicAdd(&A.vcnt[ri], (uint32_t)nk);
+  if (k & 1) {
+    uint32_t kk = (uint32_t)S.ch(p + k - 1);
+    kk *= c1; kk = rotl32(kk, 15); kk *= c2;
+    h ^= kk;
   }
-}
-
-// The -f multipliers as an open-addressing table (a binary search over the sorted codes
-// cost ~17 dependent loads per distinct k-mer): slot = splitmix64(code) & mask, linear
-// probing, empty slots hold FEMPTY (no 2k-bit code reaches it).
-constexpr uint64_t FEMPTY = ~0ull;
-struct FreqSlot {
-  uint64_t code;
-  double mult;
-};
-
-struct WSketchArgs {
-  const void *keys;             // K[], sorted (per read, or over the batch)
-  uint64_t nkeys;
-  const uint64_t *koff;         // 32-bit keys: per read its first key ...
-  const uint32_t *vcnt;         // ... and its valid ones
-  uint32_t r0, nreads;
-  int32_t k, H;
-  const FreqSlot *ftab;         // -f k-mers and their multipliers m(c), or null
-  uint64_t fmask;               // table slots - 1
-  double dmult;                 // m(c) of every other k-mer (< 0: it never enters a sketch)
-  int32_t no_tf;
-  int32_t *minhash;             // [read][H]
-};
-
-__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t n, uint64_t v) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// Stage 1, weighted (oracle: mhap_oracle.sketch_weighted)
-template <typename K>
-__global__ void __launch_bounds__(256) k_mh_sketch_w(WSketchArgs A) {
-  const K *keys = (const K *)A.keys;
-  extern __shared__ int32_t s_min[];               // [4 waves][H]
-  __shared__ uint64_t s_rng[2];
-  const uint32_t ri = blockIdx.x, r = A.r0 + ri;
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int32_t H = A.H, k = A.k;
-  const uint64_t cmask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1);
-  for (int32_t j = tid; j < 4 * H; j += 256) s_min[j] = I32MAX;
-  if (tid == 0) {
-    if (sizeof(K) == 4) {
-      s_rng[0] = A.koff[ri];
-      s_rng[1] = A.koff[ri] + A.vcnt[ri];
-    } else {
-      s_rng[0] = lower_bound_u64((const uint64_t *)keys, A.nkeys, (uint64_t)ri << (2 * k));
-      s_rng[1] = lower_bound_u64((const uint64_t *)keys, A.nkeys, (uint64_t)(ri + 1) << (2 * k));
-    }
-  }
-  __syncthreads();
-  const uint64_t s0 = s_rng[0], s1 = s_rng[1];
-  int32_t *wm = s_min + wave * H;
-  for (uint64_t base = s0; base < s1; base += 256 * RKW) {
-    const uint64_t p0 = base + (uint64_t)tid * RKW;
-    uint32_t XL[RKW], XH[RKW];
-    int32_t W[RKW];
-    uint32_t vm = 0;
-#pragma unroll
-    for (int i = 0; i < RKW; i++) {
-      XL[i] = XH[i] = 0;
-      W[i] = 0;
-      const uint64_t p = p0 + i;
-      if (p < s1) {
-        const K key = keys[p];
-        if (p == s0 || keys[p - 1] != key) {             // a run start: a distinct k-mer
-          uint64_t e = p + 1;
-          while (e < s1 && keys[e] == key) e++;
-          const uint64_t c = (uint64_t)key & cmask;
-          double m = A.dmult;
-          if (A.ftab) {
-            for (uint64_t h = splitmix64(c) & A.fmask;; h = (h + 1) & A.fmask) {
-              const FreqSlot fs = A.ftab[h];
-              if (fs.code == c) { m = fs.mult; break; }
-              if (fs.code == FEMPTY) break;
-            }
-          }
-          if (m >= 0.0) {                       // m < 0: removed (--supress-noise 1)
-            const double tf = A.no_tf ? 1.0 : (double)(e - p);
-            const double wf = floor(tf * m + 0.5);
-            W[i] = wf < 1.0 ? 1 : (int32_t)wf;
-            const uint64_t x = splitmix64(c);
-            XL[i] = (uint32_t)x;
-            XH[i] = (uint32_t)(x >> 32);
-            vm |= 1u << i;
-          }
-        }
-      }
-    }
-    if (__builtin_amdgcn_ballot_w64(vm != 0) == 0) continue;
-    // empty slots take a copy of a live slot's chain and weight (min is idempotent)
-    {
-      uint32_t l0 = 0, h0 = 0;
-      int32_t w0 = 0;
-#pragma unroll
-      for (int i = RKW - 1; i >= 0; i--)
-        if ((vm >> i) & 1u) { l0 = XL[i]; h0 = XH[i]; w0 = W[i]; }
-#pragma unroll
-      for (int i = 0; i < RKW; i++)
-        if (!((vm >> i) & 1u)) { XL[i] = l0; XH[i] = h0; W[i] = w0; }
-    }
-    const bool live = vm != 0;
-    // The draws per slot are a per-lane loop; when every live slot of the wave has the same
-    // small weight (w = 2: a distinct k-mer at the default multiplier r + (1 - r) X = 1.9,
-    // canu's case; or w = 1) the draws are straight-line code instead (no exec-mask loop
-    // per slot and function)
-    bool all1 = true, all2 = true;
-#pragma unroll
-    for (int i = 0; i < RKW; i++) { all1 &= W[i] == 1; all2 &= W[i] == 2; }
-    const int32_t wu = __builtin_amdgcn_ballot_w64(live && !all2) == 0 ? 2
-                     : __builtin_amdgcn_ballot_w64(live && !all1) == 0 ? 1 : 0;
-    auto run = [&](auto wc) {
-      constexpr int WC = decltype(wc)::value;
-      for (int32_t j = 0; j < H; j++) {
-        int32_t m = I32MAX;
-        if constexpr (WC > 0) {
-#pragma unroll
-          for (int t = 0; t < WC; t++) {
-            xs64_n<RKW>(XL, XH);
-#pragma unroll
-            for (int i = 0; i < RKW; i++) m = (int32_t)XL[i] < m ? (int32_t)XL[i] : m;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < RKW; i++) {
-            for (int32_t t = 0; t < W[i]; t++) {
-              xs64(XL[i], XH[i]);
-              const int32_t v = (int32_t)XL[i];
-              m = v < m ? v : m;
-            }
-          }
-        }
-        m = live ? m : I32MAX;
-        m = wave_min(m);
-        if (lane == 0 && m < wm[j]) wm[j] = m;
-      }
-    };
-    if (wu == 2)      run(std::integral_constant<int, 2>());
-    else if (wu == 1) run(std::integral_constant<int, 1>());
-    else              run(std::integral_constant<int, 0>());
-  }
-  __syncthreads();
-  for (int32_t j = tid; j < H; j += 256) {
-    int32_t m = s_min[j];
-    for (int w = 1; w < 4; w++) m = s_min[w * H + j] < m ? s_min[w * H + j] : m;
-    A.minhash[(size_t)r * H + j] = m;
-  }
-}
-
-struct OrderedArgs {
-  const uint8_t *bases;
-  const uint64_t *off;
-  const uint32_t *len;
-  uint32_t r0, nreads;
-  int32_t k, S;
-  uint64_t *ordered;            // [read][S]: hash << 32 | pos << 1 | strand
-  uint32_t *ocount;
-};
-
-// Stage 3 input (oracle: mhap_oracle.ordered_sketch)
-__global__ void __launch_bounds__(256) k_mh_ordered(OrderedArgs A) {
-  __shared__ uint32_t hist[NBIN];
-  __shared__ uint64_t list[OCAP];
-  __shared__ uint32_t part[256];
-  __shared__ int32_t sB;
-  __shared__ uint32_t sN, sCnt;
-  const uint32_t r = A.r0 + blockIdx.x;
-  const uint32_t tid = threadIdx.x;
-  const int32_t k = A.k, S = A.S;
-  for (int32_t i = tid; i < NBIN; i += 256) hist[i] = 0;
-  if (tid == 0) sCnt = 0;
-  __syncthreads();
-  const uint8_t *s = A.bases + A.off[r];
-  const int32_t L = (int32_t)A.len[r];
-  const int32_t npos = L - k + 1;
-  const int32_t seg = npos > 0 ? (npos + 255) / 256 : 0;
-  const int32_t p0 = (int32_t)tid * seg, p1 = min(p0 + seg, npos > 0 ? npos : 0);
-  // pass 1: histogram of hash >> 20
-  if (p0 < p1) {
-    Roller R(k);
-    for (int32_t i = 0; i < k - 1; i++) R.push(base_code(s[p0 + i]));
-    for (int32_t p = p0; p < p1; p++) {
-      if (R.push(base_code(s[p + k - 1]))) {
-        uint32_t h = (uint32_t)(splitmix64(R.canon()) >> 32);
-        atomicAdd(&hist[h >> 20], 1u);
-      }
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    // smallest bin B whose cumulative count reaches S (the last bin if none does), then
-    // drop whole bins from the top while the collected entries exceed the LDS capacity
-    uint32_t cs = 0;
-    int32_t B = NBIN - 1;
-    for (int32_t b = 0; b < NBIN; b++) {
-      cs += hist[b];
-      if (cs >= (uint32_t)S) { B = b; break; }
-    }
-    while (B >= 0 && cs > (uint32_t)OCAP) { cs -= hist[B]; B--; }
-    sB = B;
-    sN = cs;
-  }
-  __syncthreads();
-  const int32_t B = sB;
-  const uint32_t n = sN;
-  // pass 2: collect the entries of bins <= B
-  if (B >= 0 && p0 < p1) {
-    Roller R(k);
-    for (int32_t i = 0; i < k - 1; i++) R.push(base_code(s[p0 + i]));
-    for (int32_t p = p0; p < p1; p++) {
-      if (R.push(base_code(s[p + k - 1]))) {
-        uint32_t h = (uint32_t)(splitmix64(R.canon()) >> 32);
-        if ((int32_t)(h >> 20) <= B) {
-          uint32_t idx = atomicAdd(&sCnt, 1u);
-          if (idx < (uint32_t)OCAP)
-            list[idx] = ((uint64_t)h << 32) | ((uint64_t)(uint32_t)p << 1) | R.strand();
-        }
-      }
-    }
-  }
-  __syncthreads();
-  uint32_t P = 1;
-  while (P < n) P <<= 1;
-  for (uint32_t i = n + tid; i < P; i += 256) list[i] = ~0ull;
-  __syncthreads();
-  // bitonic sort list[0 .. P) ascending
-  for (uint32_t kk = 2; kk <= P; kk <<= 1) {
-    for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i = tid; i < P; i += 256) {
-        uint32_t ix = i ^ jj;
-        if (ix > i) {
-          uint64_t a = list[i], b = list[ix];
-          bool up = (i & kk) == 0;
-          if ((a > b) == up) { list[i] = b; list[ix] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // dedup by hash (first = smallest position), keep the first S
-  const uint32_t per = (n + 255) / 256;
-  const uint32_t i0 = tid * per, i1 = min(i0 + per, n);
-  uint32_t c = 0;
-  for (uint32_t i = i0; i < i1; i++)
-    if (i == 0 || (list[i] >> 32) != (list[i - 1] >> 32)) c++;
-  part[tid] = c;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int t = 0; t < 256; t++) { uint32_t v = part[t]; part[t] = acc; acc += v; }
-    A.ocount[r] = acc < (uint32_t)S ? acc : (uint32_t)S;
-  }
-  __syncthreads();
-  uint32_t rank = part[tid];
-  uint64_t *dst = A.ordered + (size_t)r * S;
-  for (uint32_t i = i0; i < i1; i++) {
-    if (i == 0 || (list[i] >> 32) != (list[i - 1] >> 32)) {
-      if (rank < (uint32_t)S) dst[rank] = list[i];
-      rank++;
-    }
-  }
-}
-
-// MinHash index keys: (j << 32 | value ^ 0x80000000), value = read; invalid -> table H.
-// rows r0 .. r0 + nreads - 1 of the sketch (the indexed reads)
-__global__ void k_mh_index_keys(const int32_t *mh, uint32_t r0, uint32_t nreads, int32_t H,
-                                uint64_t *keys, uint32_t *vals) {
-  size_t n = (size_t)nreads * H;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
-       e += (size_t)gridDim.x * blockDim.x) {
-    uint32_t r = r0 + (uint32_t)(e / H), j = (uint32_t)(e % H);
-    int32_t v = mh[(size_t)r0 * H + e];
-    keys[e] = (v == I32MAX) ? ((uint64_t)H << 32)
-                            : (((uint64_t)j << 32) | ((uint32_t)v ^ 0x80000000u));
-    vals[e] = r;
-  }
-}
-
-__global__ void k_mh_table_offsets(const uint64_t *keys, size_t n, int32_t H, uint64_t *off) {
-  int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j > H) return;
-  uint64_t key = (uint64_t)j << 32;
-  size_t lo = 0, hi = n;
-  while (lo < hi) {
-    size_t mid = (lo + hi) >> 1;
-    if (keys[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  off[j] = lo;
-}
-
-struct CandArgs {
-  const int32_t *mh;
-  const uint64_t *keys;
-  const uint32_t *vals;
-  const uint64_t *toff;
-  int32_t H;
-  uint32_t q0, q1;              // queries [q0, q1), 0-based
-  uint32_t all_targets;         // 0: targets t > q (all-vs-all, each pair once); 1: t != q
-  uint32_t min_matches;
-  Cand *out;
-  uint32_t *nout;
-  uint32_t cap;
-  uint32_t *overflow;
-};
-
-// Stage 2 (oracle: mhap_oracle.candidates)
-__global__ void __launch_bounds__(256) k_mh_candidates(CandArgs A) {
-  extern __shared__ uint32_t s_tab[];              // [4][TSLOTS] keys, then [4][TSLOTS] counts
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t q = A.q0 + blockIdx.x * 4 + wave;
-  if (q >= A.q1) return;                           // whole wave leaves together
-  uint32_t *tk = s_tab + wave * TSLOTS;
-  uint32_t *tc = s_tab + 4 * TSLOTS + wave * TSLOTS;
-  for (uint32_t i = lane; i < TSLOTS; i += 64) { tk[i] = 0; tc[i] = 0; }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  bool ovf = false;
-  for (int32_t j = lane; j < A.H; j += 64) {
-    const int32_t v = A.mh[(size_t)q * A.H + j];
-    if (v == I32MAX) continue;
-    const uint64_t key = ((uint64_t)j << 32) | ((uint32_t)v ^ 0x80000000u);
-    uint64_t lo = A.toff[j], hi = A.toff[j + 1];
-    while (lo < hi) {
-      uint64_t mid = (lo + hi) >> 1;
-      if (A.keys[mid] < key) lo = mid + 1;
-      else hi = mid;
-    }
-    const uint64_t end = A.toff[j + 1];
-    for (uint64_t i = lo; i < end && A.keys[i] == key; i++) {
-      const uint32_t t = A.vals[i];
-      if (A.all_targets ? t == q : t <= q) continue;
-      uint32_t sl = (t * 2654435761u) >> TSHIFT;
-      uint32_t probes = 0;
-      for (;;) {
-        uint32_t old = atomicCAS(&tk[sl], 0u, t + 1);
-        if (old == 0u || old == t + 1) { atomicAdd(&tc[sl], 1u); break; }
-        sl = (sl + 1) & (TSLOTS - 1);
-        if (++probes >= TSLOTS) { ovf = true; break; }
-      }
-      if (ovf) break;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (ovf) atomicOr(A.overflow, 1u);
-  for (uint32_t i = lane; i < TSLOTS; i += 64) {
-    const uint32_t key = tk[i], c = tc[i];
-    if (key && c >= A.min_matches) {
-      uint32_t idx = atomicAdd(A.nout, 1u);
-      if (idx < A.cap) A.out[idx] = Cand{q, key - 1, c, 0};
-      else atomicOr(A.overflow, 2u);
-    }
-  }
-}
-
-struct CmpArgs {
-  const Cand *cand;
-  uint32_t ncand;
-  const uint64_t *ordered;
-  const uint32_t *ocount;
-  const uint32_t *len;
-  uint32_t first_iid;
-  int32_t S, kk, min_olap;
-  double threshold;
-  RecDev *out;
-  uint32_t *nout;
-  uint32_t cap;
-  uint32_t *overflow;
-};
-
-__device__ __forceinline__ uint32_t lds_lower_bound_hash(const uint64_t *b, uint32_t n,
-                                                         uint32_t h) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if ((uint32_t)(b[mid] >> 32) < h) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
+  h ^= (uint32_t)(2 * k);
+  h ^= h >> 16; h *= 0x85EBCA6Bu;
+  h ^= h >> 13; h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -713,166 +164,825 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
 
-// Stage 3 (oracle: mhap_oracle.compare).  Two waves per block; per wave LDS:
-// B's sketch (S u64), the shared list (S x {pA, pB | same << 31}), a 256-bin histogram.
-__global__ void __launch_bounds__(128) k_mh_compare(CmpArgs A) {
-  extern __shared__ uint64_t s_cmp[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int32_t S = A.S, kk = A.kk;
-  const size_t wave_words = (size_t)S + S + 128;   // u64 words: B, shared (2 x u32), hist
-  uint64_t *bk = s_cmp + wave * wave_words;
-  uint32_t *shA = (uint32_t *)(bk + S);
-  uint32_t *shB = shA + S;
-  uint32_t *hist = (uint32_t *)(bk + 2 * S);
-  const uint64_t lane_lt = (1ull << lane) - 1;
-  for (uint32_t c = blockIdx.x * 2 + wave; c < A.ncand; c += gridDim.x * 2) {
-    wave_sync();                                   // the previous pair's LDS reads are done
-    const Cand cd = A.cand[c];
-    const uint32_t q = cd.q, t = cd.t;
-    const uint32_t na = A.ocount[q], nb = A.ocount[t];
-    const int32_t la = (int32_t)A.len[q], lb = (int32_t)A.len[t];
-    const uint64_t *ak = A.ordered + (size_t)q * S;
-    const uint64_t *bg = A.ordered + (size_t)t * S;
-    for (uint32_t i = lane; i < nb; i += 64) bk[i] = bg[i];
-    wave_sync();
-    // shared entries (each A entry with the first B entry of its hash; the median and the
-    // counts below only need them as a set): lane l merges its own run of A,
-    // A[l c .. l c + c), against B from one binary search for the run's first hash -- about
-    // c + nb / 64 LDS reads per lane instead of a binary search (log2 nb reads) per entry
-    uint32_t nsh = 0, nsame = 0;
-    const uint32_t crun = (na + 63) / 64;
-    const uint32_t a_lo = lane * crun, a_hi = a_lo + crun < na ? a_lo + crun : na;
-    uint32_t bp = a_lo < a_hi ? lds_lower_bound_hash(bk, nb, (uint32_t)(ak[a_lo] >> 32)) : nb;
-    for (uint32_t st = 0; st < crun; st++) {
-      const uint32_t i = a_lo + st;
-      bool found = false, same = false;
-      uint32_t pa = 0, pb = 0;
-      if (i < a_hi) {
-        const uint64_t ka = ak[i];
-        const uint32_t h = (uint32_t)(ka >> 32);
-        while (bp < nb && (uint32_t)(bk[bp] >> 32) < h) bp++;
-        if (bp < nb && (uint32_t)(bk[bp] >> 32) == h) {
-          const uint64_t kb = bk[bp];
-          found = true;
-          pa = (uint32_t)(ka >> 1) & 0x7FFFFFFFu;
-          pb = (uint32_t)(kb >> 1) & 0x7FFFFFFFu;
-          same = (ka & 1) == (kb & 1);
+__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {
+  for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+  return v;
+}
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+  for (int s = 32; s > 0; s >>= 1) { const int32_t t = __shfl_xor(v, s); v = t < v ? t : v; }
+  return v;
+}
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
+  for (int s = 32; s > 0; s >>= 1) { const int32_t t = __shfl_xor(v, s); v = t > v ? t : v; }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  for (int s = 32; s > 0; s >>= 1) { const uint32_t t = __shfl_xor(v, s); v = t < v ? t : v; }
+  return v;
+}
+
+// signed 64-bit minimum over the wave, result uniform: DPP row shifts within 16-lane rows,
+// then the row broadcasts (lanes whose source is outside the row read LMAX)
+template <int CTRL, int RM>
+__device__ __forceinline__ int64_t dpp_i64(int64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)(uint32_t)v, CTRL, RM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)0x7FFFFFFF, (int)(uint32_t)((uint64_t)v >> 32),
+                                             CTRL, RM, 0xf, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+  int64_t t;
+  t = dpp_i64<0x111, 0xf>(v); v = t < v ? t : v;
+  t = dpp_i64<0x112, 0xf>(v); v = t < v ? t : v;
+  t = dpp_i64<0x114, 0xf>(v); v = t < v ? t : v;
+  t = dpp_i64<0x118, 0xf>(v); v = t < v ? t : v;
+  t = dpp_i64<0x142, 0xa>(v); v = t < v ? t : v;
+  t = dpp_i64<0x143, 0xc>(v); v = t < v ? t : v;
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), 63);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// ---- ordered sketch -----------------------------------------------------------------------
+struct OrderedArgs {
+  const uint8_t *bases;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint32_t r0, nstrands;          // strands 2 r0 .. 2 r0 + nstrands - 1
+  int32_t kk, S, min_use;         // k', ordered sketch size, shortest used read
+  int32_t no_rc;
+  uint64_t *ordered;              // [strand][S]: (hash ^ 0x80000000) << 32 | position
+  uint32_t *ocount;
+};
+
+// key of the k'-mer at p: signed hash order, then position (stable radix sort of the jar)
+__device__ __forceinline__ uint64_t okey(const Strand &S, int32_t p, int32_t kk) {
+  return ((uint64_t)(murmur32(S, p, kk) ^ 0x80000000u) << 32) | (uint32_t)p;
+}
+
+// BottomOverlapSketch.<init>(s, k', S, false) @0-177 (oracle mhap_jar.ordered_sketch)
+__global__ void __launch_bounds__(256) k_mh_ordered(OrderedArgs A) {
+  __shared__ uint32_t hist[NBIN];
+  __shared__ uint64_t list[OCAP];
+  __shared__ uint32_t sD, sCnt, sBelow, sDone;
+  const uint32_t sid = 2 * A.r0 + blockIdx.x;
+  const uint32_t r = sid >> 1, tid = threadIdx.x;
+  const int32_t L = (int32_t)A.len[r];
+  const int32_t kk = A.kk;
+  const int32_t npos = L - kk + 1;
+  // a read shorter than --min-olap-length, or without a k'-mer, is not used; --no-rc: the
+  // reverse strand is not stored
+  if (L < A.min_use || npos <= 0 || ((sid & 1) && A.no_rc)) {
+    if (tid == 0) A.ocount[sid] = 0;
+    return;
+  }
+  const Strand St{A.bases + A.off[r], L, (int32_t)(sid & 1)};
+  const uint32_t want = (uint32_t)min(A.S, npos);
+  // radix select of the `want` smallest keys: digits of 12 bits from the top; prefix =
+  // the digits fixed so far, below = keys known to be smaller than the prefix's range
+  uint64_t prefix = 0;
+  int32_t fixed = 0;
+  uint32_t below = 0;
+  uint64_t bound = 0;             // collect keys whose top (fixed + 12) bits <= bound
+  int32_t bshift = 0;
+  for (;;) {
+    for (int32_t i = tid; i < NBIN; i += 256) hist[i] = 0;
+    __syncthreads();
+    const int32_t width = fixed + 12 <= 64 ? 12 : 64 - fixed;
+    const int32_t sh = 64 - fixed - width;
+    for (int32_t p = tid; p < npos; p += 256) {
+      const uint64_t key = okey(St, p, kk);
+      if (fixed == 0 || (key >> (64 - fixed)) == prefix)
+        atomicAdd(&hist[(uint32_t)((key >> sh) & ((1ull << width) - 1))], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t need = want - below;
+      uint32_t cs = 0, D = (1u << width) - 1;
+      for (uint32_t b = 0; b < (1u << width); b++) {
+        if (cs + hist[b] >= need) { D = b; break; }
+        cs += hist[b];
+      }
+      sD = D;
+      sBelow = below + cs;                        // keys below digit D (all selected)
+      sDone = (below + cs + hist[D] <= (uint32_t)OCAP) ? 1u : 0u;
+    }
+    __syncthreads();
+    const uint32_t D = sD;
+    if (sDone) {
+      bound = (fixed == 0 ? 0 : prefix << width) | D;
+      bshift = sh;
+      break;
+    }
+    below = sBelow;
+    prefix = (fixed == 0 ? 0 : prefix << width) | D;
+    fixed += width;
+    __syncthreads();
+  }
+  // collect every key whose top bits are <= (prefix, D): exactly the selected ones below
+  // plus all of bin D (>= want in total, <= OCAP)
+  if (tid == 0) sCnt = 0;
+  __syncthreads();
+  for (int32_t p = tid; p < npos; p += 256) {
+    const uint64_t key = okey(St, p, kk);
+    if ((key >> bshift) <= bound) {
+      const uint32_t idx = atomicAdd(&sCnt, 1u);
+      if (idx < (uint32_t)OCAP) list[idx] = key;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = min(sCnt, (uint32_t)OCAP);
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + tid; i < P; i += 256) list[i] = ~0ull;
+  __syncthreads();
+  for (uint32_t kb = 2; kb <= P; kb <<= 1) {
+    for (uint32_t jb = kb >> 1; jb > 0; jb >>= 1) {
+      for (uint32_t i = tid; i < P; i += 256) {
+        const uint32_t ix = i ^ jb;
+        if (ix > i) {
+          const uint64_t a = list[i], b = list[ix];
+          const bool up = (i & kb) == 0;
+          if ((a > b) == up) { list[i] = b; list[ix] = a; }
         }
       }
-      const uint64_t fm = __builtin_amdgcn_ballot_w64(found);
-      const uint64_t smm = __builtin_amdgcn_ballot_w64(found && same);
-      if (found) {
-        const uint32_t slot = nsh + popc64(fm & lane_lt);
-        shA[slot] = pa;
-        shB[slot] = pb | (same ? 0x80000000u : 0u);
+      __syncthreads();
+    }
+  }
+  uint64_t *dst = A.ordered + (size_t)sid * A.S;
+  for (uint32_t i = tid; i < want; i += 256) dst[i] = list[i];
+  if (tid == 0) A.ocount[sid] = want;
+}
+
+// ---- MinHash keys ---------------------------------------------------------------------------
+struct KeyArgs {
+  const uint8_t *bases;
+  const uint64_t *off;
+  const uint32_t *len;
+  const uint32_t *sids;           // the batch's strands
+  const uint64_t *koff;           // per batch strand: its first key
+  int32_t k;
+  uint64_t *keys;
+  uint32_t *pos;
+};
+
+// HashUtils.computeSequenceHashesLong(s, k, 0, false) of one strand per block
+__global__ void __launch_bounds__(256) k_mh_keys(KeyArgs A) {
+  const uint32_t bi = blockIdx.x, sid = A.sids[bi], r = sid >> 1;
+  const int32_t L = (int32_t)A.len[r], k = A.k;
+  const int32_t npos = L - k + 1;
+  const Strand St{A.bases + A.off[r], L, (int32_t)(sid & 1)};
+  uint64_t *out = A.keys + A.koff[bi];
+  uint32_t *po = A.pos + A.koff[bi];
+  for (int32_t p = threadIdx.x; p < npos; p += 256) {
+    out[p] = murmur128_h1([&](int32_t q) { return St.ch(p + q); }, k);
+    po[p] = (uint32_t)p;
+  }
+}
+
+// ---- MinHash sketch -------------------------------------------------------------------------
+// The -f table (FrequencyCounts.fractionCounts): open addressing on the 64-bit key.
+struct FreqSlot {
+  uint64_t key;
+  double sidf;                    // scaledIdf of the k-mer (weighting mode 1)
+  uint32_t used, pad;
+};
+
+enum { W_ONE = 0, W_TFIDF = 1, W_COUNT = 2 };
+
+struct SketchArgs {
+  const uint64_t *keys;           // sorted per strand
+  const uint32_t *pos;            // first positions ride along (stable sort)
+  const uint64_t *koff;           // per batch strand: segment start, [nb + 1]
+  const uint32_t *sids;
+  int32_t H;
+  int32_t mode;                   // W_ONE (repeat_weight < 0), W_TFIDF, W_COUNT
+  const FreqSlot *ftab;           // null: no -f table
+  uint64_t fmask;
+  double range;                   // scaledIdf of a k-mer not in the table
+  int32_t no_tf;
+  int32_t *minhash;               // [strand][H]
+  uint32_t *ocount;               // zeroed for a strand with no k-mer of weight > 0
+  unsigned long long *stat;       // [0] distinct k-mers, [1] draws
+};
+
+__device__ __forceinline__ uint64_t slot_hash(uint64_t key) {
+  return fmix64(key ^ 0x9E3779B97F4A7C15ull);
+}
+
+__device__ __forceinline__ const FreqSlot *table_find(const FreqSlot *t, uint64_t mask,
+                                                      uint64_t key) {
+  for (uint64_t h = slot_hash(key) & mask;; h = (h + 1) & mask) {
+    const FreqSlot *s = t + h;
+    if (!s->used) return nullptr;
+    if (s->key == key) return s;
+  }
+}
+
+// Math.round(double): the closest long, ties toward positive infinity
+__device__ __forceinline__ int64_t java_round(double x) {
+  const double f = floor(x);
+  return (int64_t)f + (__dsub_rn(x, f) >= 0.5 ? 1 : 0);
+}
+
+// one xorshift64 step (<<21, >>>35, <<4)
+__device__ __forceinline__ uint64_t xs64(uint64_t x) {
+  x ^= x << 21;
+  x ^= x >> 35;
+  x ^= x << 4;
+  return x;
+}
+
+// MinHashSketch.computeNgramMinHashesWeighted @0-476 (oracle mhap_jar.minhash); one block
+// per strand.  LDS: per wave and hash function the best (draw, first position, value).
+__global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
+  extern __shared__ uint8_t s_raw[];
+  const int32_t H = A.H;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int64_t *bx_all = (int64_t *)s_raw;                       // [4][H]
+  uint32_t *bp_all = (uint32_t *)(bx_all + 4 * H);          // [4][H]
+  uint32_t *bv_all = bp_all + 4 * H;                        // [4][H]
+  __shared__ uint32_t s_live;
+  for (int32_t j = tid; j < 4 * H; j += 256) {
+    bx_all[j] = LMAX;
+    bp_all[j] = 0xFFFFFFFFu;
+    bv_all[j] = 0;
+  }
+  if (tid == 0) s_live = 0;
+  __syncthreads();
+  const uint32_t bi = blockIdx.x, sid = A.sids[bi];
+  const uint64_t s0 = A.koff[bi], s1 = A.koff[bi + 1];
+  int64_t *bx = bx_all + wave * H;
+  uint32_t *bp = bp_all + wave * H;
+  uint32_t *bv = bv_all + wave * H;
+  unsigned long long nkm = 0, ndraw = 0;
+  for (uint64_t base = s0; base < s1; base += 256 * RKW) {
+    const uint64_t p0 = base + (uint64_t)tid * RKW;
+    uint64_t X[RKW];
+    uint32_t KL[RKW], KH[RKW], FP[RKW];
+    int32_t W[RKW];
+#pragma unroll
+    for (int i = 0; i < RKW; i++) {
+      X[i] = 0; KL[i] = KH[i] = 0; FP[i] = 0xFFFFFFFFu; W[i] = 0;
+      const uint64_t p = p0 + i;
+      if (p < s1) {
+        const uint64_t key = A.keys[p];
+        if (p == s0 || A.keys[p - 1] != key) {             // a run start: a distinct k-mer
+          uint64_t e = p + 1;
+          while (e < s1 && A.keys[e] == key) e++;
+          const uint32_t cnt = (uint32_t)(e - p);
+          int64_t w = cnt;
+          if (A.mode == W_ONE) {
+            w = (A.ftab && table_find(A.ftab, A.fmask, key)) ? 0 : 1;
+          } else if (A.mode == W_TFIDF) {
+            const FreqSlot *f = A.ftab ? table_find(A.ftab, A.fmask, key) : nullptr;
+            const double sidf = f ? f->sidf : A.range;
+            const double tf = A.no_tf ? 1.0 : (double)cnt;
+            w = java_round(__dmul_rn(tf, sidf));
+            if (w < 1) w = 1;
+          }
+          if (w > 0) {
+            W[i] = (int32_t)(w > 0x7FFFFFFF ? 0x7FFFFFFF : w);
+            X[i] = key;
+            KL[i] = (uint32_t)key;
+            KH[i] = (uint32_t)(key >> 32);
+            FP[i] = A.pos[p];
+            nkm++;
+            ndraw += (unsigned long long)W[i] * (unsigned long long)H;
+          }
+        }
       }
-      nsh += popc64(fm);
-      nsame += popc64(smm);
+    }
+    int32_t wl = 0;
+#pragma unroll
+    for (int i = 0; i < RKW; i++) wl = W[i] > wl ? W[i] : wl;
+    if (__builtin_amdgcn_ballot_w64(wl > 0) == 0) continue;   // nothing in this wave
+    for (int32_t j = 0; j < H; j++) {
+      int64_t mx = LMAX;
+      uint32_t mp = 0xFFFFFFFFu, mv = 0;
+#pragma unroll
+      for (int i = 0; i < RKW; i++) {
+        int64_t mi = LMAX;
+        for (int32_t t = 0; t < W[i]; t++) {
+          X[i] = xs64(X[i]);
+          mi = (int64_t)X[i] < mi ? (int64_t)X[i] : mi;
+        }
+        // the jar's strict '<' in key order: equal draws keep the earlier first occurrence
+        if (mi < mx || (mi == mx && FP[i] < mp)) {
+          mx = mi;
+          mp = FP[i];
+          mv = (j & 1) ? KH[i] : KL[i];
+        }
+      }
+      const int64_t wx = wave_min_i64(mx);
+      if (wx == LMAX) continue;                     // no draw below the initial value
+      const uint64_t hold = __builtin_amdgcn_ballot_w64(mx == wx);
+      uint32_t wp, wv;
+      if (popc64(hold) == 1) {
+        const uint32_t ln = (uint32_t)__builtin_ctzll(hold);
+        wp = __builtin_amdgcn_readlane(mp, ln);
+        wv = __builtin_amdgcn_readlane(mv, ln);
+      } else {
+        wp = wave_min_u32(mx == wx ? mp : 0xFFFFFFFFu);
+        const uint64_t who = __builtin_amdgcn_ballot_w64(mx == wx && mp == wp);
+        wv = __builtin_amdgcn_readlane(mv, (uint32_t)__builtin_ctzll(who));
+      }
+      if (lane == 0 && (wx < bx[j] || (wx == bx[j] && wp < bp[j]))) {
+        bx[j] = wx;
+        bp[j] = wp;
+        bv[j] = wv;
+      }
+    }
+  }
+  for (int s = 32; s > 0; s >>= 1) {
+    nkm += __shfl_xor(nkm, s);
+    ndraw += __shfl_xor(ndraw, s);
+  }
+  if (lane == 0 && nkm) {
+    atomicAdd(&s_live, 1u);
+    if (A.stat) {
+      atomicAdd(&A.stat[0], nkm);
+      atomicAdd(&A.stat[1], ndraw);
+    }
+  }
+  __syncthreads();
+  for (int32_t j = tid; j < H; j += 256) {
+    int64_t x = bx_all[j];
+    uint32_t p = bp_all[j], v = bv_all[j];
+    for (int w = 1; w < 4; w++) {
+      const int64_t y = bx_all[w * H + j];
+      const uint32_t q = bp_all[w * H + j];
+      if (y < x || (y == x && q < p)) { x = y; p = q; v = bv_all[w * H + j]; }
+    }
+    A.minhash[(size_t)sid * H + j] = x == LMAX ? 0 : (int32_t)v;
+  }
+  // no k-mer of positive weight: the jar's sketch constructor fails and the read (or this
+  // strand) is skipped
+  if (tid == 0 && s_live == 0) A.ocount[sid] = 0;
+}
+
+// a read whose forward strand was skipped is skipped whole (SequenceSketchStreamer
+// .enqueue @67-95: the reverse strand is made only after the forward one)
+__global__ void k_mh_strand_fixup(uint32_t *ocount, uint32_t r0, uint32_t nr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nr && ocount[2 * (r0 + i)] == 0) ocount[2 * (r0 + i) + 1] = 0;
+}
+
+// ---- index ----------------------------------------------------------------------------------
+// (j << 32 | value ^ 0x80000000) -> stored strand; strands not stored -> table H
+__global__ void k_mh_index_keys(const int32_t *mh, const uint32_t *ocount, uint32_t s0,
+                                uint32_t ns, int32_t H, uint64_t *keys, uint32_t *vals) {
+  const size_t n = (size_t)ns * H;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t sid = s0 + (uint32_t)(e / H), j = (uint32_t)(e % H);
+    const int32_t v = mh[(size_t)s0 * H + e];
+    keys[e] = ocount[sid] == 0 ? ((uint64_t)H << 32)
+                               : (((uint64_t)j << 32) | ((uint32_t)v ^ 0x80000000u));
+    vals[e] = sid;
+  }
+}
+
+__global__ void k_mh_table_offsets(const uint64_t *keys, size_t n, int32_t H, uint64_t *off) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > H) return;
+  const uint64_t key = (uint64_t)j << 32;
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) >> 1;
+    if (keys[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  off[j] = lo;
+}
+
+// ---- first stage ----------------------------------------------------------------------------
+struct CandArgs {
+  const int32_t *mh;
+  const uint32_t *ocount;
+  const uint32_t *len;
+  const uint64_t *keys;
+  const uint32_t *vals;
+  const uint64_t *toff;
+  int32_t H;
+  uint32_t q0, q1;                // query reads [q0, q1)
+  uint32_t self;                  // 1: toSelf (stored reads of smaller ID), 0: all but q
+  int32_t min_store;
+  uint32_t min_matches;
+  Cand *out;
+  uint32_t *nout;
+  uint32_t cap;
+  uint32_t *overflow;
+};
+
+// MinHashSearch.findMatches(query, toSelf) @0-492 (oracle mhap_jar.find_matches)
+__global__ void __launch_bounds__(256) k_mh_candidates(CandArgs A) {
+  extern __shared__ uint32_t s_tab[];              // [4][TSLOTS] keys, then [4][TSLOTS] counts
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t q = A.q0 + blockIdx.x * 4 + wave;
+  if (q >= A.q1) return;                           // whole wave leaves together
+  if (A.ocount[2 * q] == 0) return;                // query not used
+  uint32_t *tk = s_tab + wave * TSLOTS;
+  uint32_t *tc = s_tab + 4 * TSLOTS + wave * TSLOTS;
+  for (uint32_t i = lane; i < TSLOTS; i += 64) { tk[i] = 0; tc[i] = 0; }
+  wave_sync();
+  const int32_t qlen = (int32_t)A.len[q], ms = A.min_store;
+  bool ovf = false;
+  for (int32_t j = lane; j < A.H; j += 64) {
+    const int32_t v = A.mh[(size_t)(2 * q) * A.H + j];
+    const uint64_t key = ((uint64_t)j << 32) | ((uint32_t)v ^ 0x80000000u);
+    uint64_t lo = A.toff[j], hi = A.toff[j + 1];
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (A.keys[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint64_t end = A.toff[j + 1];
+    for (uint64_t i = lo; i < end && A.keys[i] == key; i++) {
+      const uint32_t t = A.vals[i], tr = t >> 1;
+      if (tr == q) continue;
+      const int32_t tlen = (int32_t)A.len[tr];
+      if (tlen < ms && qlen < ms) continue;                                 // @393-416
+      if (A.self && tr > q && tlen >= ms && qlen >= ms) continue;           // @419-462
+      if (A.self && tlen < ms && qlen >= ms) continue;                      // @465-492
+      uint32_t sl = ((t + 1) * 2654435761u) >> TSHIFT;
+      uint32_t probes = 0;
+      for (;;) {
+        const uint32_t old = atomicCAS(&tk[sl], 0u, t + 1);
+        if (old == 0u || old == t + 1) { atomicAdd(&tc[sl], 1u); break; }
+        sl = (sl + 1) & (TSLOTS - 1);
+        if (++probes >= TSLOTS) { ovf = true; break; }
+      }
+      if (ovf) break;
+    }
+  }
+  wave_sync();
+  if (ovf) atomicOr(A.overflow, 1u);
+  for (uint32_t i = lane; i < TSLOTS; i += 64) {
+    const uint32_t key = tk[i], c = tc[i];
+    if (key && c >= A.min_matches) {
+      const uint32_t idx = atomicAdd(A.nout, 1u);
+      if (idx < A.cap) A.out[idx] = Cand{q, key - 1, c, 0};
+      else atomicOr(A.overflow, 2u);
+    }
+  }
+}
+
+// ---- second stage ---------------------------------------------------------------------------
+struct CmpArgs {
+  const Cand *cand;
+  uint32_t ncand;
+  const uint64_t *ordered;
+  const uint32_t *ocount;
+  const uint32_t *len;
+  int32_t S, kk;
+  double max_shift;
+  const uint32_t *pass;           // bit n (S + 1) + inter: identity(inter / n) >= threshold
+  uint32_t pass_empty;            // identity 0 (n = 0) >= threshold
+  RecDev *out;
+  uint32_t *nout;
+  uint32_t cap;
+  uint32_t *overflow;
+};
+
+__device__ __forceinline__ uint32_t hash_of(uint64_t e) { return (uint32_t)(e >> 32); }
+__device__ __forceinline__ int32_t pos_of(uint64_t e) { return (int32_t)(uint32_t)e; }
+
+// A group: the entries of one hash present in both sketches, A[a0, a1) and B[b0, b1)
+struct Group {
+  uint32_t a0, a1, b0, b1;
+};
+__device__ __forceinline__ uint64_t pack_group(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
+  return (uint64_t)a0 | ((uint64_t)a1 << 16) | ((uint64_t)b0 << 32) | ((uint64_t)b1 << 48);
+}
+__device__ __forceinline__ Group unpack_group(uint64_t g) {
+  return Group{(uint32_t)(g & 0xFFFF), (uint32_t)((g >> 16) & 0xFFFF),
+               (uint32_t)((g >> 32) & 0xFFFF), (uint32_t)(g >> 48)};
+}
+
+// MatchData's state for one recordMatchingKmers pass: median shift, its absMax and the
+// valid position windows (performUpdate @0-134, valid1/2Lower/Upper)
+struct Window {
+  int32_t m, amax, v1lo, v1hi, v2lo, v2hi;
+};
+
+__device__ __forceinline__ Window make_window(int32_t m, int32_t amax, int32_t sl1, int32_t sl2) {
+  Window w;
+  w.m = m;
+  w.amax = amax;
+  w.v1lo = max(0, -m - amax);
+  w.v2lo = max(0, m - amax);
+  w.v1hi = min(sl1, sl2 - m + amax);
+  w.v2hi = min(sl2, sl1 + m + amax);
+  return w;
+}
+
+// performUpdate with records whose median shift is m
+__device__ __forceinline__ int32_t abs_max(int32_t m, int32_t sl1, int32_t sl2, double msp) {
+  const int32_t lo = max(0, -m);
+  const int32_t hi = min(sl1, sl2 - m);
+  const int32_t olap = max(10, hi - lo);
+  return min(max(sl1, sl2), (int32_t)__dmul_rn((double)olap, msp));
+}
+
+// recordMatchingKmers @0-450 restricted to one group (the jar's merge only ever compares
+// entries of equal hash when it records, and enters each group at its first entries on both
+// sides, so groups are independent): emit(p1, p2) per recorded match, in the jar's order
+template <class Emit>
+__device__ __forceinline__ void group_records(const uint64_t *A, const uint64_t *B, Group g,
+                                              const Window &w, Emit emit) {
+  uint32_t i1 = g.a0, i2 = g.b0;
+  while (i1 < g.a1 && i2 < g.b1) {
+    const int32_t p1 = pos_of(A[i1]);
+    if (p1 < w.v1lo || p1 >= w.v1hi) { i1++; continue; }
+    const int32_t p2 = pos_of(B[i2]);
+    if (p2 < w.v2lo || p2 >= w.v2hi) { i2++; continue; }
+    const int32_t d = (p2 - p1) - w.m;
+    if (d > w.amax) { i1++; continue; }
+    if (d < -w.amax) { i2++; continue; }
+    emit(p1, p2);
+    uint32_t l1 = i1, l2 = i2;
+    for (uint32_t j = i1 + 1; j < g.a1; j++) {
+      const int32_t p = pos_of(A[j]);
+      if (p < w.v1lo || p >= w.v1hi) break;
+      l1 = j;
+    }
+    for (uint32_t j = i2 + 1; j < g.b1; j++) {
+      const int32_t p = pos_of(B[j]);
+      if (p < w.v2lo || p >= w.v2hi) break;
+      l2 = j;
+    }
+    if (l1 == i1 && l2 == i2) {
+      i1++;
+      i2++;
+    } else {
+      emit(pos_of(A[l1]), pos_of(B[l2]));
+      i1 = l1 + 1;
+      i2 = l2 + 1;
+    }
+  }
+}
+
+// the same records after optimizeShifts @0-165 (consecutive records of one p1 keep the one
+// whose shift is nearest the median m; equal p1 only ever occur inside a group)
+template <class Emit>
+__device__ __forceinline__ void group_records_opt(const uint64_t *A, const uint64_t *B, Group g,
+                                                  const Window &w, int32_t m, Emit emit) {
+  bool has = false;
+  int32_t q1 = 0, q2 = 0;
+  group_records(A, B, g, w, [&](int32_t p1, int32_t p2) {
+    if (has && q1 == p1) {
+      if (abs(q2 - q1 - m) > abs(p2 - p1 - m)) q2 = p2;
+    } else {
+      if (has) emit(q1, q2);
+      has = true;
+      q1 = p1;
+      q2 = p2;
+    }
+  });
+  if (has) emit(q1, q2);
+}
+
+// The (count / 2)-th smallest shift p2 - p1 over the records gen() emits (Utils.quickSelect
+// of performUpdate): a radix select over u = shift + off (off = sl1, so u > 0) in 8-bit
+// digits; count = the number of records (0: none)
+template <class Gen>
+__device__ int32_t wave_median(Gen gen, int32_t off, uint32_t bits, uint32_t *hist,
+                               uint32_t lane, uint32_t &count) {
+  const int npass = (int)((bits + 7) / 8);
+  uint32_t prefix = 0, pmask = 0, kth = 0;
+  count = 0;
+  for (int pass = npass - 1; pass >= 0; pass--) {
+    for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
+    wave_sync();
+    gen([&](int32_t p1, int32_t p2) {
+      const uint32_t u = (uint32_t)(p2 - p1 + off);
+      if ((u & pmask) == prefix) atomicAdd(&hist[(u >> (8 * pass)) & 255u], 1u);
+    });
+    wave_sync();
+    const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                   h3 = hist[4 * lane + 3];
+    const uint32_t tot = h0 + h1 + h2 + h3;
+    uint32_t incl = tot;
+    for (int sft = 1; sft < 64; sft <<= 1) {
+      const uint32_t v = __shfl_up(incl, sft);
+      if ((int)lane >= sft) incl += v;
+    }
+    if (pass == npass - 1) {
+      count = __shfl(incl, 63);
+      if (count == 0) return 0;
+      kth = count / 2;
+    }
+    const uint32_t excl = incl - tot;
+    const bool mine = excl <= kth && kth < incl;
+    const uint64_t who = __builtin_amdgcn_ballot_w64(mine);
+    const uint32_t owner = (uint32_t)__builtin_ctzll(who);
+    uint32_t bin = 0, before = excl;
+    if (mine) {
+      const uint32_t rem = kth - excl;
+      if (rem < h0) bin = 0;
+      else if (rem < h0 + h1) { bin = 1; before += h0; }
+      else if (rem < h0 + h1 + h2) { bin = 2; before += h0 + h1; }
+      else { bin = 3; before += h0 + h1 + h2; }
+      bin += 4 * lane;
+    }
+    bin = __shfl(bin, owner);
+    before = __shfl(before, owner);
+    kth -= before;
+    prefix |= bin << (8 * pass);
+    pmask |= 255u << (8 * pass);
+    wave_sync();
+  }
+  return (int32_t)prefix - off;
+}
+
+// BottomOverlapSketch.getOverlapInfo(other, maxShift) @0-211 (oracle mhap_jar.overlap_info);
+// one wave per candidate; LDS per wave: A [S], B [S], groups [S] (u64) and a 256-bin histogram
+__global__ void __launch_bounds__(64) k_mh_compare(CmpArgs A) {
+  extern __shared__ uint64_t s_cmp[];
+  const uint32_t lane = threadIdx.x;
+  const int32_t S = A.S;
+  uint64_t *la = s_cmp;
+  uint64_t *lb = la + S;
+  uint64_t *lg = lb + S;
+  uint32_t *hist = (uint32_t *)(lg + S);
+  const uint64_t lane_lt = (1ull << lane) - 1;
+  for (uint32_t c = blockIdx.x; c < A.ncand; c += gridDim.x) {
+    wave_sync();                                   // the previous pair's LDS reads are done
+    const Cand cd = A.cand[c];
+    const uint32_t sa = 2 * cd.q, sb = cd.t;
+    const uint32_t na = A.ocount[sa], nb = A.ocount[sb];
+    const int32_t la_len = (int32_t)A.len[cd.q], lb_len = (int32_t)A.len[sb >> 1];
+    const int32_t sl1 = la_len - A.kk + 1, sl2 = lb_len - A.kk + 1;   // seqLength
+    {
+      const uint64_t *ga = A.ordered + (size_t)sa * S;
+      const uint64_t *gb = A.ordered + (size_t)sb * S;
+      for (uint32_t i = lane; i < na; i += 64) la[i] = ga[i];
+      for (uint32_t i = lane; i < nb; i += 64) lb[i] = gb[i];
     }
     wave_sync();
-    if (nsh == 0) continue;
-    const uint32_t o = (nsame >= nsh - nsame) ? 0u : 1u;
-    const uint32_t ncons = o == 0 ? nsame : nsh - nsame;
-    if (ncons == 0) continue;
-    // lower median of d = pA - pB' over the consistent entries: 4-pass radix select
-    uint32_t kth = (ncons - 1) / 2, prefix = 0, pmask = 0;
-    for (int pass = 3; pass >= 0; pass--) {
-      for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
-      wave_sync();
-      for (uint32_t i = lane; i < nsh; i += 64) {
-        const uint32_t pb_raw = shB[i];
-        const bool sm = (pb_raw >> 31) != 0;
-        if (sm != (o == 0)) continue;
-        const int32_t pb = (int32_t)(pb_raw & 0x7FFFFFFFu);
-        const int32_t pbp = o == 0 ? pb : lb - kk - pb;
-        const uint32_t u = (uint32_t)((int32_t)shA[i] - pbp) ^ 0x80000000u;
-        if ((u & pmask) == prefix) atomicAdd(&hist[(u >> (8 * pass)) & 255u], 1u);
+    // groups, in hash order: lane l owns A[l c, l c + c) and the groups starting there
+    const uint32_t crun = (na + 63) / 64;
+    const uint32_t a_lo = lane * crun, a_hi = min(a_lo + crun, na);
+    auto discover = [&](auto found) {
+      uint32_t bp = 0;
+      if (a_lo < a_hi) {                           // lower bound of A[a_lo]'s hash in B
+        const uint32_t h = hash_of(la[a_lo]);
+        uint32_t lo = 0, hi = nb;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (hash_of(lb[mid]) < h) lo = mid + 1;
+          else hi = mid;
+        }
+        bp = lo;
       }
-      wave_sync();
-      // bin holding the kth element: lane l owns bins 4l .. 4l+3
-      uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
-               h3 = hist[4 * lane + 3];
-      uint32_t tot = h0 + h1 + h2 + h3;
-      uint32_t incl = tot;                          // inclusive scan over lanes
-      for (int sft = 1; sft < 64; sft <<= 1) {
-        uint32_t v = __shfl_up(incl, sft);
-        if ((int)lane >= sft) incl += v;
+      for (uint32_t i = a_lo; i < a_hi; i++) {
+        const uint32_t h = hash_of(la[i]);
+        if (i > 0 && hash_of(la[i - 1]) == h) continue;   // not a group start
+        while (bp < nb && hash_of(lb[bp]) < h) bp++;
+        if (bp < nb && hash_of(lb[bp]) == h) {
+          uint32_t ae = i + 1, be = bp + 1;
+          while (ae < na && hash_of(la[ae]) == h) ae++;
+          while (be < nb && hash_of(lb[be]) == h) be++;
+          found(i, ae, bp, be);
+        }
       }
-      const uint32_t excl = incl - tot;
-      const bool mine = excl <= kth && kth < incl;
-      const uint64_t who = __builtin_amdgcn_ballot_w64(mine);
-      const uint32_t owner = (uint32_t)__builtin_ctzll(who);
-      uint32_t bin = 0, before = excl;
-      if (mine) {
-        uint32_t rem = kth - excl;
-        if (rem < h0) bin = 0;
-        else if (rem < h0 + h1) { bin = 1; before += h0; }
-        else if (rem < h0 + h1 + h2) { bin = 2; before += h0 + h1; }
-        else { bin = 3; before += h0 + h1 + h2; }
-        bin += 4 * lane;
-      }
-      bin = __shfl(bin, owner);
-      before = __shfl(before, owner);
-      kth -= before;
-      prefix |= bin << (8 * pass);
-      pmask |= 255u << (8 * pass);
-      wave_sync();
+    };
+    uint32_t mine = 0;
+    discover([&](uint32_t, uint32_t, uint32_t, uint32_t) { mine++; });
+    uint32_t goff = mine;                          // exclusive scan over lanes
+    for (int sft = 1; sft < 64; sft <<= 1) {
+      const uint32_t v = __shfl_up(goff, sft);
+      if ((int)lane >= sft) goff += v;
     }
-    const int32_t dm = (int32_t)(prefix ^ 0x80000000u);
-    const int32_t a_bgn = dm > 0 ? dm : 0;
-    const int32_t a_end = la < lb + dm ? la : lb + dm;
-    if (a_end - a_bgn < A.min_olap) continue;
-    const int32_t b_bgn = a_bgn - dm, b_end = a_end - dm;
-    uint32_t cA = 0, cB = 0, m = 0;
+    const uint32_t ngroups = __shfl(goff, 63);
+    goff -= mine;
+    if (ngroups == 0) continue;                    // no shared k'-mer: EMPTY
+    discover([&](uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
+      lg[goff++] = pack_group(a0, a1, b0, b1);
+    });
+    wave_sync();
+    const uint32_t bits = 32u - (uint32_t)__builtin_clz((uint32_t)(sl1 + sl2));
+    // pass 0: no records yet -> median 0, absMax = max(seqLength) + 1, everything valid
+    const Window w0 = make_window(0, max(sl1, sl2) + 1, sl1, sl2);
+    uint32_t n0 = 0;
+    const int32_t m0 = wave_median([&](auto emit) {
+      for (uint32_t g = lane; g < ngroups; g += 64) group_records(la, lb, unpack_group(lg[g]), w0, emit);
+    }, sl1, bits, hist, lane, n0);
+    if (n0 == 0) continue;
+    // pass 1 in the windows of pass 0's median
+    const Window w1 = make_window(m0, abs_max(m0, sl1, sl2, A.max_shift), sl1, sl2);
+    uint32_t n1 = 0;
+    const int32_t m1 = wave_median([&](auto emit) {
+      for (uint32_t g = lane; g < ngroups; g += 64) group_records(la, lb, unpack_group(lg[g]), w1, emit);
+    }, sl1, bits, hist, lane, n1);
+    if (n1 == 0) continue;
+    // optimizeShifts with pass 1's median, then computeEdges with the new median
+    uint32_t n2 = 0;
+    const int32_t m2 = wave_median([&](auto emit) {
+      for (uint32_t g = lane; g < ngroups; g += 64)
+        group_records_opt(la, lb, unpack_group(lg[g]), w1, m1, emit);
+    }, sl1, bits, hist, lane, n2);
+    const int32_t a2m = abs_max(m2, sl1, sl2, A.max_shift);
+    int32_t cnt = 0, l1 = 0x7FFFFFFF, l2 = 0x7FFFFFFF, r1 = (int32_t)0x80000000,
+            r2 = (int32_t)0x80000000;
+    for (uint32_t g = lane; g < ngroups; g += 64) {
+      group_records_opt(la, lb, unpack_group(lg[g]), w1, m1, [&](int32_t p1, int32_t p2) {
+        if (abs(p2 - p1 - m2) > a2m) return;
+        l1 = min(l1, p1); l2 = min(l2, p2);
+        r1 = max(r1, p1); r2 = max(r2, p2);
+        cnt++;
+      });
+    }
+    cnt = wave_sum_i32(cnt);
+    if (cnt < 3) continue;
+    l1 = wave_min_i32(l1); l2 = wave_min_i32(l2);
+    r1 = wave_max_i32(r1); r2 = wave_max_i32(r2);
+    // computeEdges @118-236: int imul / isub (wrapping), i2d, ddiv, Math.round, l2i
+    auto edge = [&](int32_t x, int32_t y) {
+      const int32_t num = (int32_t)((uint32_t)((uint32_t)cnt * (uint32_t)x) - (uint32_t)y);
+      return (int32_t)java_round((double)num / (double)(cnt - 1));
+    };
+    const int32_t e_a1 = max(0, edge(l1, r1));
+    const int32_t e_a2 = min(sl1, edge(r1, l1));
+    const int32_t e_b1 = max(0, edge(l2, r2));
+    const int32_t e_b2 = min(sl2, edge(r2, l2));
+    // computeKBottomSketchJaccard @0-227: the entries of each sketch whose position lies in
+    // its edge range (in hash order), n = min of the two counts, a merge of n steps counting
+    // equal hashes.  Closed form: a value v present in both with rx / ry entries in range
+    // takes max(rx, ry) steps, min(rx, ry) of them equal, after xr + yr - E(< v) steps (xr,
+    // yr: entries in range below v; E: equal steps of smaller values); a value in one
+    // sketch only adds steps, no equality.  The hash halves of la / lb are replaced by the
+    // exclusive prefix counts of in-range entries (group discovery is done).
+    uint32_t nx = 0, ny = 0;
     for (uint32_t i0 = 0; i0 < na; i0 += 64) {
       const uint32_t i = i0 + lane;
       bool in = false;
-      if (i < na) {
-        const int32_t p = (int32_t)((uint32_t)(ak[i] >> 1) & 0x7FFFFFFFu);
-        in = p >= a_bgn && p <= a_end - kk;
-      }
-      cA += popc64(__builtin_amdgcn_ballot_w64(in));
+      int32_t p = 0;
+      if (i < na) { p = pos_of(la[i]); in = p >= e_a1 && p <= e_a2; }
+      const uint64_t m = __builtin_amdgcn_ballot_w64(in);
+      if (i < na) la[i] = ((uint64_t)(nx + popc64(m & lane_lt)) << 32) | (uint32_t)p;
+      nx += popc64(m);
     }
     for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
       const uint32_t i = i0 + lane;
       bool in = false;
-      if (i < nb) {
-        const int32_t pb = (int32_t)((uint32_t)(bk[i] >> 1) & 0x7FFFFFFFu);
-        const int32_t p = o == 0 ? pb : lb - kk - pb;
-        in = p >= b_bgn && p <= b_end - kk;
-      }
-      cB += popc64(__builtin_amdgcn_ballot_w64(in));
+      int32_t p = 0;
+      if (i < nb) { p = pos_of(lb[i]); in = p >= e_b1 && p <= e_b2; }
+      const uint64_t m = __builtin_amdgcn_ballot_w64(in);
+      if (i < nb) lb[i] = ((uint64_t)(ny + popc64(m & lane_lt)) << 32) | (uint32_t)p;
+      ny += popc64(m);
     }
-    for (uint32_t i0 = 0; i0 < nsh; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      bool in = false;
-      if (i < nsh) {
-        const uint32_t pb_raw = shB[i];
-        const bool sm = (pb_raw >> 31) != 0;
-        if (sm == (o == 0)) {
-          const int32_t pa = (int32_t)shA[i];
-          const int32_t pb = (int32_t)(pb_raw & 0x7FFFFFFFu);
-          const int32_t pbp = o == 0 ? pb : lb - kk - pb;
-          in = pa >= a_bgn && pa <= a_end - kk && pbp >= b_bgn && pbp <= b_end - kk;
+    wave_sync();
+    const uint32_t n = min(nx, ny);
+    uint32_t inter = 0;
+    if (n > 0) {
+      uint32_t carry = 0;                         // E over the groups before this chunk
+      for (uint32_t g0 = 0; g0 < ngroups; g0 += 64) {
+        const uint32_t g = g0 + lane;
+        uint32_t eq = 0, xr = 0, yr = 0;
+        if (g < ngroups) {
+          const Group G = unpack_group(lg[g]);
+          xr = hash_of(la[G.a0]);
+          yr = hash_of(lb[G.b0]);
+          const uint32_t xe = G.a1 < na ? hash_of(la[G.a1]) : nx;
+          const uint32_t ye = G.b1 < nb ? hash_of(lb[G.b1]) : ny;
+          eq = min(xe - xr, ye - yr);
         }
+        uint32_t incl = eq;
+        for (int sft = 1; sft < 64; sft <<= 1) {
+          const uint32_t v = __shfl_up(incl, sft);
+          if ((int)lane >= sft) incl += v;
+        }
+        const int64_t steps = (int64_t)xr + yr - (int64_t)(carry + incl - eq);
+        const int64_t left = (int64_t)n - steps;
+        uint32_t got = 0;
+        if (eq && left > 0) got = (uint32_t)min<int64_t>(eq, left);
+        inter += got;
+        carry += __shfl(incl, 63);
       }
-      m += popc64(__builtin_amdgcn_ballot_w64(in));
+      inter = (uint32_t)wave_sum_i32((int32_t)inter);
     }
-    if (m == 0) continue;
-    const double J = (double)m / (double)(cA + cB - m);
-    const double D = -log(2.0 * J / (1.0 + J)) / (double)kk;
-    if (1.0 - D < A.threshold) continue;
+    const bool ok = n == 0 ? A.pass_empty != 0
+                           : ((A.pass[((size_t)n * (S + 1) + inter) >> 5] >> (((size_t)n * (S + 1) + inter) & 31)) & 1u) != 0;
+    if (!ok) continue;
     if (lane == 0) {
-      uint32_t idx = atomicAdd(A.nout, 1u);
+      const uint32_t idx = atomicAdd(A.nout, 1u);
       if (idx < A.cap) {
         RecDev rr;
-        rr.a = A.first_iid + q;
-        rr.b = A.first_iid + t;
-        rr.erate = D < 1.0 ? D : 1.0;
-        rr.count = cd.cnt;
-        rr.a_bgn = a_bgn; rr.a_end = a_end; rr.a_len = la;
-        rr.o = o;
-        rr.b_bgn = b_bgn; rr.b_end = b_end; rr.b_len = lb;
+        rr.a = cd.q;
+        rr.b = sb >> 1;
+        rr.o = sb & 1;
+        rr.cnt = cd.cnt;
+        rr.inter = inter;
+        rr.n = n;
+        rr.raw = (uint32_t)cnt;
+        rr.pad = 0;
+        rr.a1 = e_a1; rr.a2 = e_a2; rr.a_len = la_len;
+        // MatchResult.<init> @86-143: reverse-strand coordinates mirrored on the read
+        rr.b1 = rr.o ? lb_len - e_b2 - 1 : e_b1;
+        rr.b2 = rr.o ? lb_len - e_b1 - 1 : e_b2;
+        rr.b_len = lb_len;
         A.out[idx] = rr;
       } else {
         atomicOr(A.overflow, 1u);
@@ -939,20 +1049,23 @@ struct mhap_ctx {
   MBuf<uint64_t> off_own;
   const uint64_t *d_off = nullptr;
   MBuf<uint32_t> d_len;
-  MBuf<uint64_t> filter;
-  uint32_t nfilter = 0;
-  // repeat weighting (mhap_set_kmer_frequencies): weighted sketch when repeat_weight >= 0
-  mhap_weighting W{-1.0, 10.0, 1e-5, 0};
-  bool weighted = false;
-  MBuf<uint64_t> wkeys, wkeys2;
+  // weighting (MhapMain options + FrequencyCounts)
+  mhap_weighting W{0.9, 3.0, 1e-5, 0, 0};
+  bool has_table = false;
   MBuf<FreqSlot> ftab;
   uint64_t fmask = 0;
-  uint32_t nf = 0;
-  double dmult = 1.0;
-  MBuf<uint8_t> wsort_tmp;
+  // second-stage acceptance: identity(inter / n) >= threshold, per (n, inter)
+  MBuf<uint32_t> pass;
+  uint32_t pass_empty = 0;
+  // sketches
   MBuf<int32_t> minhash;
   MBuf<uint64_t> ordered;
   MBuf<uint32_t> ocount;
+  MBuf<uint64_t> mkeys, mkeys2;
+  MBuf<uint32_t> mpos, mpos2, msids;
+  MBuf<uint64_t> mkoff;
+  MBuf<uint8_t> msort_tmp;
+  // index
   MBuf<uint64_t> keys, keys2, toff;
   MBuf<uint32_t> vals, vals2;
   MBuf<uint8_t> sort_tmp;
@@ -972,6 +1085,18 @@ static float elapsed(mhap_ctx *c) {
   return t;
 }
 
+// the jar's score of a Jaccard value (BottomOverlapSketch.jaccardToIdentity @0-25)
+static double jaccard_identity(double J, int kk) {
+  if (!(J > 0.0)) return 0.0;
+  const double d = (-1.0 / (double)kk) * log(2.0 * J / (1.0 + J));
+  return exp(-d);
+}
+
+// computeKBottomSketchJaccard's J = inter / n (0 when n = 0)
+static double jaccard_of(uint32_t inter, uint32_t n) {
+  return n == 0 ? 0.0 : (double)inter / (double)n;
+}
+
 extern "C" {
 
 int mhap_abi_version(void) { return MHAP_ABI_VERSION; }
@@ -985,6 +1110,17 @@ void mhap_params_init(mhap_params *p) {
   p->ordered_k = 12;
   p->min_olap = 500;
   p->threshold = 0.78;
+  p->max_shift = 0.2;
+  p->min_store = 0;
+  p->no_rc = 0;
+}
+
+void mhap_weighting_init(mhap_weighting *w) {
+  w->repeat_weight = 0.9;
+  w->repeat_idf_scale = 3.0;
+  w->filter_threshold = 1e-5;
+  w->no_tf = 0;
+  w->supress_noise = 0;
 }
 
 int mhap_ctx_create(const mhap_params *p, int device, mhap_ctx **out) {
@@ -994,9 +1130,11 @@ int mhap_ctx_create(const mhap_params *p, int device, mhap_ctx **out) {
     return mfail(M_BAD_PARAM, "k-mer sizes must be 1..32");
   if (p->num_hashes < 1 || p->num_hashes > 1024)
     return mfail(M_BAD_PARAM, "num_hashes must be 1..1024");
-  if (p->ordered_sketch < 1 || p->ordered_sketch > 1984)   // k_mh_compare LDS: 2 waves x 8(2S+128) B
-    return mfail(M_BAD_PARAM, "ordered_sketch must be 1..1984");
+  if (p->ordered_sketch < 1 || p->ordered_sketch > 2048)   // k_mh_compare LDS: 3 x 8 S + 1 KB
+    return mfail(M_BAD_PARAM, "ordered_sketch must be 1..2048");
   if (p->min_matches < 1) return mfail(M_BAD_PARAM, "min_matches must be >= 1");
+  if (!(p->max_shift >= -1.0)) return mfail(M_BAD_PARAM, "--max-shift must be >= -1");
+  if (p->min_store < 0) return mfail(M_BAD_PARAM, "--min-store-length must be >= 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
     return mfail(M_NO_DEVICE, "no HIP device %d", device);
@@ -1014,9 +1152,33 @@ int mhap_ctx_create(const mhap_params *p, int device, mhap_ctx **out) {
     delete c;
     return mfail(M_HIP, "stream/event creation failed");
   }
-  if (c->ctr.alloc(16) != hipSuccess || c->kctr.alloc(1) != hipSuccess) {
+  if (c->ctr.alloc(16) != hipSuccess || c->kctr.alloc(2) != hipSuccess) {
     delete c;
     return mfail(M_OOM, "counters");
+  }
+  // the complement table (Utils$Translate)
+  uint8_t comp[256] = {0};
+  const char *from = "ABCDGHKMNRSTVWY", *to = "TVGHCDMKNYSABWR";
+  for (int i = 0; from[i]; i++) comp[(uint8_t)from[i]] = (uint8_t)to[i];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(c_comp), comp, 256) != hipSuccess) {
+    delete c;
+    return mfail(M_HIP, "complement table");
+  }
+  // acceptance bits: the identity is computed here, on the host, exactly as the oracle does
+  const uint32_t S = p->ordered_sketch;
+  const size_t nbits = (size_t)(S + 1) * (S + 1);
+  std::vector<uint32_t> bits((nbits + 31) / 32, 0);
+  for (uint32_t n = 1; n <= S; n++)
+    for (uint32_t i = 0; i <= n; i++)
+      if (jaccard_identity(jaccard_of(i, n), (int)p->ordered_k) >= p->threshold) {
+        const size_t b = (size_t)n * (S + 1) + i;
+        bits[b >> 5] |= 1u << (b & 31);
+      }
+  c->pass_empty = jaccard_identity(0.0, (int)p->ordered_k) >= p->threshold ? 1u : 0u;
+  if (c->pass.alloc(bits.size()) != hipSuccess ||
+      hipMemcpy(c->pass.p, bits.data(), 4 * bits.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    delete c;
+    return mfail(M_OOM, "acceptance table");
   }
   *out = c;
   return M_OK;
@@ -1032,19 +1194,11 @@ void mhap_ctx_destroy(mhap_ctx *c) {
   delete c;
 }
 
-// the MinHash kernel's launch just completed (events ev[2] .. ev[3]): its time, summed
-static void sketch_kernel_time(mhap_ctx *c) {
-  float t = 0;
-  (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
-  c->stats.ms_sketch_kernel += t;
-  c->stats.sketch_launches++;
-}
-
 static int alloc_sketches(mhap_ctx *c) {
-  const size_t n = c->nreads;
+  const size_t n = 2ull * c->nreads;
   if (c->minhash.alloc(n * c->P.num_hashes) || c->ordered.alloc(n * c->P.ordered_sketch) ||
       c->ocount.alloc(n))
-    return mfail(M_OOM, "sketch arrays for %zu reads", n);
+    return mfail(M_OOM, "sketch arrays for %u reads", c->nreads);
   MHC(hipMemsetAsync(c->ocount.p, 0, 4 * n, c->stream));
   c->indexed = false;
   return M_OK;
@@ -1052,6 +1206,7 @@ static int alloc_sketches(mhap_ctx *c) {
 
 static int set_lengths(mhap_ctx *c, uint32_t first_iid, uint32_t nreads, const uint32_t *lens) {
   if (first_iid == 0) return mfail(M_BAD_PARAM, "gkStore IDs start at 1");
+  if (nreads >= 0x7FFFFFF0u) return mfail(M_BAD_PARAM, "too many reads");
   for (uint32_t i = 0; i < nreads; i++)
     if (lens[i] >= 0x7FFFFFFFu) return mfail(M_BAD_INPUT, "read %u too long", first_iid + i);
   c->first_iid = first_iid;
@@ -1094,214 +1249,137 @@ int mhap_load_reads_device(mhap_ctx *c, uint32_t first_iid, uint32_t nreads,
   return M_OK;
 }
 
-int mhap_set_filter_kmers(mhap_ctx *c, const char *kmers, uint64_t n) {
-  if (!c) return mfail(M_STATE, "null context");
-  const uint32_t k = c->P.k;
-  std::vector<uint64_t> codes;
-  for (uint64_t i = 0; i < n; i++) {
-    uint64_t f = 0, r = 0;
-    bool ok = true;
-    for (uint32_t t = 0; t < k; t++) {
-      char ch = kmers[i * k + t] | 0x20;
-      uint64_t b = ch == 'a' ? 0 : ch == 'c' ? 1 : ch == 'g' ? 2 : ch == 't' ? 3 : 9;
-      if (b > 3) { ok = false; break; }
-      f = (f << 2) | b;
-      r |= (3 - b) << (2 * t);
-    }
-    if (ok) codes.push_back(f < r ? f : r);
-  }
-  std::sort(codes.begin(), codes.end());
-  codes.erase(std::unique(codes.begin(), codes.end()), codes.end());
-  MHC(hipSetDevice(c->device));
-  if (c->filter.alloc(codes.size())) return mfail(M_OOM, "filter");
-  if (!codes.empty())
-    MHC(hipMemcpy(c->filter.p, codes.data(), 8 * codes.size(), hipMemcpyHostToDevice));
-  c->nfilter = (uint32_t)codes.size();
+static int check_weighting(const mhap_weighting *w) {
+  if (!w) return mfail(M_BAD_PARAM, "null weighting");
+  if (!(w->repeat_idf_scale >= 1.0))
+    return mfail(M_BAD_PARAM, "The minimum repeat idf scale must be >=1.0.");
+  if (w->supress_noise < 0 || w->supress_noise > 2)
+    return mfail(M_BAD_PARAM, "--supress-noise %d (0, 1 or 2)", w->supress_noise);
+  if (w->supress_noise != 0)
+    return mfail(M_BAD_PARAM, "--supress-noise %d: the jar's Bloom-filter noise suppression "
+                              "is not implemented (canu passes it only with mhapFilterUnique)",
+                 w->supress_noise);
   return M_OK;
 }
 
-void mhap_weighting_init(mhap_weighting *w) {
-  w->repeat_weight = -1.0;
-  w->repeat_idf_scale = 10.0;
-  w->filter_threshold = 1e-5;
-  w->no_tf = 0;
-  w->supress_noise = 0;
+int mhap_set_weighting(mhap_ctx *c, const mhap_weighting *w) {
+  if (!c) return mfail(M_STATE, "null context");
+  const int rc = check_weighting(w);
+  if (rc) return rc;
+  c->W = *w;
+  c->has_table = false;
+  return M_OK;
 }
 
-static bool kmer_code(const char *km, uint32_t k, uint64_t *canon) {
-  uint64_t f = 0, r = 0;
-  for (uint32_t t = 0; t < k; t++) {
-    const char ch = km[t] | 0x20;
-    const uint64_t b = ch == 'a' ? 0 : ch == 'c' ? 1 : ch == 'g' ? 2 : ch == 't' ? 3 : 9;
-    if (b > 3) return false;
-    f = (f << 2) | b;
-    r |= (3 - b) << (2 * t);
-  }
-  *canon = f < r ? f : r;
-  return true;
-}
-
+// FrequencyCounts.<init> @0-429 and its lambda$1 (oracle mhap_jar.FrequencyCounts)
 int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *fractions,
                               uint64_t n, const mhap_weighting *w) {
-  if (!c || !w) return mfail(M_STATE, "null argument");
+  if (!c) return mfail(M_STATE, "null context");
+  int rc = check_weighting(w);
+  if (rc) return rc;
   if (n && (!kmers || !fractions)) return mfail(M_BAD_PARAM, "null k-mers / fractions");
-  if (!(w->filter_threshold > 0.0) || !(w->repeat_idf_scale >= 1.0))
-    return mfail(M_BAD_PARAM, "filter_threshold must be > 0 and repeat_idf_scale >= 1");
   const uint32_t k = c->P.k;
-  if (w->repeat_weight >= 0.0 && 2 * k > 56)
-    return mfail(M_BAD_PARAM, "weighted sketches need k <= 28 (read index beside the code)");
-  if (w->supress_noise < 0 || w->supress_noise > 2)
-    return mfail(M_BAD_PARAM, "--supress-noise %d (0, 1 or 2)", w->supress_noise);
-  if (w->supress_noise && w->repeat_weight < 0.0)
-    return mfail(M_BAD_PARAM, "--supress-noise needs the weighted sketch (--repeat-weight >= 0)");
-  // --supress-noise: every -f k-mer is in the table (those below the threshold at the top
-  // multiplier), so that a k-mer NOT in the file can be told apart
-  const bool noise = w->supress_noise != 0 && n != 0;
-  c->W = *w;
-  c->weighted = w->repeat_weight >= 0.0;
-  // the -f k-mers at or above the threshold, canonical (both strands are listed), the
-  // largest fraction per k-mer
-  std::vector<std::pair<uint64_t, double>> F;
+  const bool do_rc = !c->P.no_rc;
+  const double offset = (w->repeat_weight >= 0.0 && w->repeat_weight < 1.0) ? w->repeat_weight : 0.0;
+  const double cutoff = w->filter_threshold, range = w->repeat_idf_scale;
+  // key -> fraction, file order, a later line of the same key replacing an earlier one
+  std::vector<std::pair<uint64_t, double>> kv;
+  double max_value = -INFINITY;
+  std::vector<uint8_t> km(k), rk(k);
   for (uint64_t i = 0; i < n; i++) {
-    uint64_t cc;
-    if (!kmer_code(kmers + i * k, k, &cc)) continue;
-    if (!(fractions[i] >= w->filter_threshold) && !noise) continue;
-    F.emplace_back(cc, fractions[i]);
-  }
-  std::sort(F.begin(), F.end());
-  std::vector<uint64_t> codes;
-  std::vector<double> fr;
-  for (size_t i = 0; i < F.size(); i++) {
-    if (!codes.empty() && codes.back() == F[i].first) {
-      fr.back() = std::max(fr.back(), F[i].second);
-      continue;
+    const double f = fractions[i];
+    if (!(f >= cutoff)) continue;
+    for (uint32_t t = 0; t < k; t++) km[t] = (uint8_t)kmers[i * k + t];
+    const uint8_t *use = km.data();
+    if (do_rc) {                                  // Utils.rc: reverse, upper case, complement
+      static const char *from = "ABCDGHKMNRSTVWY", *to = "TVGHCDMKNYSABWR";
+      for (uint32_t t = 0; t < k; t++) {
+        const uint8_t b = (uint8_t)upper_byte(km[k - 1 - t]);
+        uint8_t o = 0;
+        for (int q = 0; from[q]; q++)
+          if ((uint8_t)from[q] == b) o = (uint8_t)to[q];
+        rk[t] = o;
+      }
+      if (memcmp(rk.data(), km.data(), k) < 0) use = rk.data();   // String.compareTo
     }
-    codes.push_back(F[i].first);
-    fr.push_back(F[i].second);
+    const uint64_t key = murmur128_h1([&](int32_t q) { return (uint64_t)use[q]; }, (int32_t)k);
+    max_value = std::max(max_value, f);
+    kv.emplace_back(key, f);
+  }
+  const auto idf = [&](double x) { return log(max_value / x - offset); };
+  const double min_idf = idf(max_value), max_idf = idf(cutoff);
+  const double scale = (max_idf - min_idf) / (range - 1.0);
+  // open addressing at load <= 1/2; later lines overwrite
+  uint64_t slots = 16;
+  while (slots < 2 * kv.size() + 1) slots <<= 1;
+  std::vector<FreqSlot> tab(slots, FreqSlot{0, 0.0, 0, 0});
+  for (const auto &e : kv) {
+    uint64_t h = fmix64(e.first ^ 0x9E3779B97F4A7C15ull) & (slots - 1);
+    while (tab[h].used && tab[h].key != e.first) h = (h + 1) & (slots - 1);
+    tab[h].key = e.first;
+    tab[h].used = 1;
+    tab[h].sidf = 1.0 + (idf(e.second) - min_idf) / scale;     // scaledIdf @31-94
   }
   MHC(hipSetDevice(c->device));
-  if (!c->weighted) {                 // MHAP 1.x: the repeats are dropped
-    if (c->filter.alloc(codes.size())) return mfail(M_OOM, "filter");
-    if (!codes.empty())
-      MHC(hipMemcpy(c->filter.p, codes.data(), 8 * codes.size(), hipMemcpyHostToDevice));
-    c->nfilter = (uint32_t)codes.size();
-    c->nf = 0;
-    return M_OK;
-  }
-  c->nfilter = 0;
-  // multipliers m(c) = r + (1 - r) * (1 + (X - 1) * (idf - idf_min) / (idf_max - idf_min))
-  const double r = w->repeat_weight, X = w->repeat_idf_scale;
-  const double idf_max = log(1.0 / w->filter_threshold);
-  double idf_min = idf_max;
-  std::vector<double> idf(codes.size());
-  for (size_t i = 0; i < codes.size(); i++) {
-    // below the threshold (only listed with --supress-noise): the top idf
-    idf[i] = fr[i] >= w->filter_threshold ? log(1.0 / fr[i]) : idf_max;
-    idf_min = std::min(idf_min, idf[i]);
-  }
-  auto mult = [&](double v) {
-    if (r >= 1.0 || codes.empty()) return 1.0;
-    const double sc = idf_max > idf_min ? 1.0 + (X - 1.0) * (v - idf_min) / (idf_max - idf_min) : X;
-    return r + (1.0 - r) * sc;
-  };
-  std::vector<double> m(codes.size());
-  for (size_t i = 0; i < codes.size(); i++) m[i] = mult(idf[i]);
-  // a k-mer not in the table: the top multiplier; with --supress-noise 2 the most frequent
-  // k-mer's (suppressed like a repeat), with 1 none (-1: it never enters a sketch)
-  c->dmult = !noise ? mult(idf_max) : w->supress_noise == 2 ? mult(idf_min) : -1.0;
-  // open addressing at load <= 1/2
-  uint64_t slots = 16;
-  while (slots < 2 * codes.size() + 1) slots <<= 1;
-  std::vector<FreqSlot> tab(slots, FreqSlot{FEMPTY, 0.0});
-  for (size_t i = 0; i < codes.size(); i++) {
-    uint64_t h = splitmix64(codes[i]) & (slots - 1);
-    while (tab[h].code != FEMPTY) h = (h + 1) & (slots - 1);
-    tab[h] = FreqSlot{codes[i], m[i]};
-  }
   if (c->ftab.alloc(slots)) return mfail(M_OOM, "k-mer frequency table");
   MHC(hipMemcpy(c->ftab.p, tab.data(), sizeof(FreqSlot) * slots, hipMemcpyHostToDevice));
   c->fmask = slots - 1;
-  c->nf = (uint32_t)codes.size();
+  c->W = *w;
+  c->has_table = true;
   return M_OK;
 }
 
-// The weighted MinHash of reads r0 .. r0+nr-1 in batches of <= WKEY_BUDGET positions: keys,
-// radix sort, sketch (the ordered sketch is the caller's, unweighted as in the jar).
-static int sketch_weighted(mhap_ctx *c, uint32_t r0, uint32_t nr) {
+// The MinHash sketches of strands (sids) in batches of <= KEY_BUDGET k-mers: keys, segmented
+// radix sort of (key, position), draws.
+static int sketch_minhash(mhap_ctx *c, const std::vector<uint32_t> &sids) {
   hipStream_t s = c->stream;
-  const uint32_t k = c->P.k;
-  // k <= 16: 32-bit codes sorted per read (a segmented sort, 4 B per key); longer k-mers:
-  // 64-bit (read index, code) keys in one sort over the batch
-  const bool k32 = 2 * k <= 32;
-  const uint64_t WKEY_BUDGET = 1ull << 30;                  // keys per batch
-  const uint32_t idx_bits = 64 - 2 * k;
-  const uint64_t max_reads = k32 ? (1u << 20)
-                                 : (idx_bits >= 32 ? 0xFFFFFFF0ull : (1ull << idx_bits) - 2);
-  for (uint32_t a = 0; a < nr;) {
+  const int32_t k = (int32_t)c->P.k;
+  const uint64_t KEY_BUDGET = 1ull << 29;
+  const int mode = c->W.repeat_weight < 0.0 ? W_ONE
+                 : (c->has_table && c->W.repeat_weight < 1.0) ? W_TFIDF : W_COUNT;
+  for (size_t a = 0; a < sids.size();) {
     std::vector<uint64_t> koff;
     uint64_t tot = 0;
-    uint32_t b = a;
-    while (b < nr && b - a < max_reads && b - a < (1u << 20)) {
-      const int64_t np = (int64_t)c->h_len[r0 + b] - (int64_t)k + 1;
+    size_t b = a;
+    while (b < sids.size() && b - a < (1u << 20)) {
+      const int64_t np = (int64_t)c->h_len[sids[b] >> 1] - k + 1;
       const uint64_t add = np > 0 ? (uint64_t)np : 0;
-      if (tot + add > WKEY_BUDGET && b > a) break;
+      if (tot + add > KEY_BUDGET && b > a) break;
       koff.push_back(tot);
       tot += add;
       b++;
     }
-    koff.push_back(tot);                                    // the segments' end offsets
-    const uint32_t nb = b - a;
-    uint32_t end_bit;
-    uint64_t sentinel;
-    if (k32) {
-      end_bit = 2 * k;
-      sentinel = (1ull << (2 * k)) - 1;                     // never a canonical code
-    } else {
-      end_bit = 2 * k + (uint32_t)std::max<int>(1, 64 - __builtin_clzll((uint64_t)nb + 1));
-      sentinel = end_bit >= 64 ? ~0ull : ((1ull << end_bit) - 1);
-    }
-    const size_t ksz = k32 ? 4 : 8;
-    MBuf<uint64_t> d_koff;
-    MBuf<uint32_t> d_vcnt;
-    const uint64_t kwords = (std::max<uint64_t>(tot, 1) * ksz + 7) / 8;
-    if (d_koff.alloc(nb + 1) || d_vcnt.alloc(nb) || c->wkeys.alloc(kwords) ||
-        c->wkeys2.alloc(kwords))
-      return mfail(M_OOM, "weighted-sketch keys (%llu)", (unsigned long long)tot);
-    MHC(hipMemcpyAsync(d_koff.p, koff.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
-    MHC(hipMemsetAsync(d_vcnt.p, 0, 4ull * nb, s));
-    KeyArgs KA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)k, d_koff.p, sentinel,
-               c->wkeys.p, d_vcnt.p, c->kctr.p};
-    if (k32) hipLaunchKernelGGL(k_mh_kmer_keys<uint32_t>, dim3(nb), dim3(256), 0, s, KA);
-    else     hipLaunchKernelGGL(k_mh_kmer_keys<uint64_t>, dim3(nb), dim3(256), 0, s, KA);
+    koff.push_back(tot);
+    const uint32_t nb = (uint32_t)(b - a);
+    if (c->mkoff.alloc(nb + 1) || c->msids.alloc(nb) || c->mkeys.alloc(tot) ||
+        c->mkeys2.alloc(tot) || c->mpos.alloc(tot) || c->mpos2.alloc(tot))
+      return mfail(M_OOM, "MinHash keys (%llu)", (unsigned long long)tot);
+    MHC(hipMemcpyAsync(c->mkoff.p, koff.data(), 8ull * (nb + 1), hipMemcpyHostToDevice, s));
+    MHC(hipMemcpyAsync(c->msids.p, sids.data() + a, 4ull * nb, hipMemcpyHostToDevice, s));
+    KeyArgs KA{c->d_bases, c->d_off, c->d_len.p, c->msids.p, c->mkoff.p, k, c->mkeys.p, c->mpos.p};
+    hipLaunchKernelGGL(k_mh_keys, dim3(nb), dim3(256), 0, s, KA);
     MHC(hipGetLastError());
     size_t tb = 0;
-    if (k32) {
-      uint32_t *ki = (uint32_t *)c->wkeys.p, *ko = (uint32_t *)c->wkeys2.p;
-      MHC(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, ki, ko, (int)tot, (int)nb,
-                                                     d_koff.p, d_koff.p + 1, 0, (int)end_bit, s));
-      if (c->wsort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
-      MHC(hipcub::DeviceSegmentedRadixSort::SortKeys(c->wsort_tmp.p, tb, ki, ko, (int)tot, (int)nb,
-                                                     d_koff.p, d_koff.p + 1, 0, (int)end_bit, s));
-    } else {
-      // key counts can pass 2^31: the 64-bit-count form of the sort
-      MHC(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
-                                            (int)end_bit, s));
-      if (c->wsort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
-      MHC(hipcub::DeviceRadixSort::SortKeys(c->wsort_tmp.p, tb, c->wkeys.p, c->wkeys2.p, tot, 0,
-                                            (int)end_bit, s));
-    }
-    WSketchArgs WA{c->wkeys2.p, tot, d_koff.p, d_vcnt.p, r0 + a, nb, (int32_t)k,
-                   (int32_t)c->P.num_hashes, c->nf ? c->ftab.p : nullptr, c->fmask, c->dmult,
-                   c->W.no_tf, c->minhash.p};
+    MHC(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, c->mkeys.p, c->mkeys2.p,
+                                                    c->mpos.p, c->mpos2.p, (int)tot, (int)nb,
+                                                    c->mkoff.p, c->mkoff.p + 1, 0, 64, s));
+    if (c->msort_tmp.alloc(std::max<size_t>(tb, 1))) return mfail(M_OOM, "sort scratch");
+    MHC(hipcub::DeviceSegmentedRadixSort::SortPairs(c->msort_tmp.p, tb, c->mkeys.p, c->mkeys2.p,
+                                                    c->mpos.p, c->mpos2.p, (int)tot, (int)nb,
+                                                    c->mkoff.p, c->mkoff.p + 1, 0, 64, s));
+    SketchArgs SA{c->mkeys2.p, c->mpos2.p, c->mkoff.p, c->msids.p, (int32_t)c->P.num_hashes,
+                  mode, c->has_table ? c->ftab.p : nullptr, c->fmask, c->W.repeat_idf_scale,
+                  c->W.no_tf, c->minhash.p, c->ocount.p, c->kctr.p};
+    const size_t lds = 16ull * 4 * c->P.num_hashes;
     MHC(hipEventRecord(c->ev[2], s));
-    if (k32)
-      hipLaunchKernelGGL(k_mh_sketch_w<uint32_t>, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
-    else
-      hipLaunchKernelGGL(k_mh_sketch_w<uint64_t>, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, WA);
+    hipLaunchKernelGGL(k_mh_minhash, dim3(nb), dim3(256), lds, s, SA);
     MHC(hipGetLastError());
     MHC(hipEventRecord(c->ev[3], s));
-    MHC(hipStreamSynchronize(s));                           // d_koff / d_vcnt are freed here
-    sketch_kernel_time(c);
+    MHC(hipStreamSynchronize(s));                 // koff / sids are rewritten next batch
+    float t = 0;
+    (void)hipEventElapsedTime(&t, c->ev[2], c->ev[3]);
+    c->stats.ms_sketch_kernel += t;
+    c->stats.sketch_launches++;
     a = b;
   }
   return M_OK;
@@ -1316,40 +1394,43 @@ int mhap_sketch(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   MHC(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const uint32_t r0 = bgn - c->first_iid, nr = end - bgn + 1;
-  MHC(hipMemsetAsync(c->kctr.p, 0, 8, s));
+  MHC(hipMemsetAsync(c->kctr.p, 0, 16, s));
   c->stats.ms_sketch_kernel = 0;
   c->stats.sketch_launches = 0;
   MHC(hipEventRecord(c->ev[0], s));
-  // one block per read; launches of <= 65535 * 16 reads keep grids modest
-  if (c->weighted) {
-    const int rc = sketch_weighted(c, r0, nr);
-    if (rc) return rc;
-  }
-  for (uint32_t a = 0; a < nr; a += 1u << 20) {
-    const uint32_t nb = std::min<uint32_t>(nr - a, 1u << 20);
-    if (!c->weighted) {
-      SketchArgs SA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.k,
-                    (int32_t)c->P.num_hashes, c->nfilter ? c->filter.p : nullptr, c->nfilter,
-                    c->minhash.p, c->kctr.p};
-      MHC(hipEventRecord(c->ev[2], s));
-      hipLaunchKernelGGL(k_mh_sketch, dim3(nb), dim3(256), 4 * 4 * c->P.num_hashes, s, SA);
-      MHC(hipGetLastError());
-      MHC(hipEventRecord(c->ev[3], s));
-      MHC(hipEventSynchronize(c->ev[3]));
-      sketch_kernel_time(c);
-    }
-    OrderedArgs OA{c->d_bases, c->d_off, c->d_len.p, r0 + a, nb, (int32_t)c->P.ordered_k,
-                   (int32_t)c->P.ordered_sketch, c->ordered.p, c->ocount.p};
-    hipLaunchKernelGGL(k_mh_ordered, dim3(nb), dim3(256), 0, s, OA);
+  // ordered sketches first: they decide which strands are used (ocount > 0)
+  const int32_t min_use = std::max<int32_t>(c->P.min_olap, (int32_t)c->P.k);
+  for (uint32_t a = 0; a < nr; a += 1u << 19) {
+    const uint32_t n = std::min<uint32_t>(nr - a, 1u << 19);
+    OrderedArgs OA{c->d_bases, c->d_off, c->d_len.p, r0 + a, 2 * n, (int32_t)c->P.ordered_k,
+                   (int32_t)c->P.ordered_sketch, min_use, c->P.no_rc, c->ordered.p, c->ocount.p};
+    hipLaunchKernelGGL(k_mh_ordered, dim3(2 * n), dim3(256), 0, s, OA);
     MHC(hipGetLastError());
   }
+  // the MinHash sketches of the strands in use (host lengths decide the same way)
+  std::vector<uint32_t> sids;
+  uint64_t used = 0;
+  for (uint32_t i = 0; i < nr; i++) {
+    const uint32_t r = r0 + i;
+    const int64_t L = c->h_len[r];
+    if (L < min_use || L < (int64_t)c->P.ordered_k) continue;
+    used++;
+    sids.push_back(2 * r);
+    if (!c->P.no_rc) sids.push_back(2 * r + 1);
+  }
+  int rc = sketch_minhash(c, sids);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_mh_strand_fixup, dim3((nr + 255) / 256), dim3(256), 0, s, c->ocount.p,
+                     r0, nr);
+  MHC(hipGetLastError());
   MHC(hipEventRecord(c->ev[1], s));
-  unsigned long long nk = 0;
-  MHC(hipMemcpyAsync(&nk, c->kctr.p, 8, hipMemcpyDeviceToHost, s));
+  unsigned long long st[2] = {0, 0};
+  MHC(hipMemcpyAsync(st, c->kctr.p, 16, hipMemcpyDeviceToHost, s));
   MHC(hipStreamSynchronize(s));
   c->stats.ms_sketch = elapsed(c);
-  c->stats.sketched_reads = nr;
-  c->stats.sketch_kmers = nk;
+  c->stats.sketched_reads = used;
+  c->stats.sketch_kmers = st[0];
+  c->stats.sketch_draws = st[1];
   c->indexed = false;
   return M_OK;
 }
@@ -1362,50 +1443,39 @@ int mhap_sketch_buffers(mhap_ctx *c, void **d_minhash, void **d_ordered, void **
   return M_OK;
 }
 
-int mhap_copy_sketches(mhap_ctx *c, uint32_t first, uint32_t n, void *d_minhash,
-                       void *d_ordered, void *d_ocount, int to_ctx) {
+static int copy_rows(mhap_ctx *c, uint32_t first, uint32_t n, void *mh, void *od, void *oc,
+                     int to_ctx, bool host) {
   if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
   if (n == 0) return M_OK;
   if (first < c->first_iid || (uint64_t)first + n > (uint64_t)c->first_iid + c->nreads)
     return mfail(M_BAD_PARAM, "rows %u..%u outside the loaded reads", first, first + n - 1);
+  if (!mh || !od || !oc) return mfail(M_BAD_PARAM, "null buffer");
   MHC(hipSetDevice(c->device));
-  const size_t r0 = first - c->first_iid;
+  const size_t s0 = 2ull * (first - c->first_iid), ns = 2ull * n;
   const size_t H = c->P.num_hashes, S = c->P.ordered_sketch;
   struct { void *ctx; void *user; size_t bytes; } parts[3] = {
-      {c->minhash.p + r0 * H, d_minhash, 4 * H * n},
-      {c->ordered.p + r0 * S, d_ordered, 8 * S * n},
-      {c->ocount.p + r0, d_ocount, 4ull * n}};
+      {c->minhash.p + s0 * H, mh, 4 * H * ns},
+      {c->ordered.p + s0 * S, od, 8 * S * ns},
+      {c->ocount.p + s0, oc, 4 * ns}};
+  const hipMemcpyKind in = host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  const hipMemcpyKind outk = host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
   for (auto &pt : parts) {
-    if (!pt.user) return mfail(M_BAD_PARAM, "null buffer");
-    if (to_ctx) MHC(hipMemcpyAsync(pt.ctx, pt.user, pt.bytes, hipMemcpyDeviceToDevice, c->stream));
-    else        MHC(hipMemcpyAsync(pt.user, pt.ctx, pt.bytes, hipMemcpyDeviceToDevice, c->stream));
+    if (to_ctx) MHC(hipMemcpyAsync(pt.ctx, pt.user, pt.bytes, in, c->stream));
+    else        MHC(hipMemcpyAsync(pt.user, pt.ctx, pt.bytes, outk, c->stream));
   }
   MHC(hipStreamSynchronize(c->stream));
   if (to_ctx) c->indexed = false;
   return M_OK;
 }
 
+int mhap_copy_sketches(mhap_ctx *c, uint32_t first, uint32_t n, void *d_minhash,
+                       void *d_ordered, void *d_ocount, int to_ctx) {
+  return copy_rows(c, first, n, d_minhash, d_ordered, d_ocount, to_ctx, false);
+}
+
 int mhap_copy_sketches_host(mhap_ctx *c, uint32_t first, uint32_t n, void *h_minhash,
                             void *h_ordered, void *h_ocount, int to_ctx) {
-  if (!c || !c->nreads) return mfail(M_STATE, "no reads loaded");
-  if (n == 0) return M_OK;
-  if (first < c->first_iid || (uint64_t)first + n > (uint64_t)c->first_iid + c->nreads)
-    return mfail(M_BAD_PARAM, "rows %u..%u outside the loaded reads", first, first + n - 1);
-  if (!h_minhash || !h_ordered || !h_ocount) return mfail(M_BAD_PARAM, "null buffer");
-  MHC(hipSetDevice(c->device));
-  const size_t r0 = first - c->first_iid;
-  const size_t H = c->P.num_hashes, S = c->P.ordered_sketch;
-  struct { void *ctx; void *user; size_t bytes; } parts[3] = {
-      {c->minhash.p + r0 * H, h_minhash, 4 * H * n},
-      {c->ordered.p + r0 * S, h_ordered, 8 * S * n},
-      {c->ocount.p + r0, h_ocount, 4ull * n}};
-  for (auto &pt : parts) {
-    if (to_ctx) MHC(hipMemcpyAsync(pt.ctx, pt.user, pt.bytes, hipMemcpyHostToDevice, c->stream));
-    else        MHC(hipMemcpyAsync(pt.user, pt.ctx, pt.bytes, hipMemcpyDeviceToHost, c->stream));
-  }
-  MHC(hipStreamSynchronize(c->stream));
-  if (to_ctx) c->indexed = false;
-  return M_OK;
+  return copy_rows(c, first, n, h_minhash, h_ordered, h_ocount, to_ctx, true);
 }
 
 int mhap_build_index(mhap_ctx *c) {
@@ -1420,14 +1490,15 @@ int mhap_build_index_range(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   MHC(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const int32_t H = (int32_t)c->P.num_hashes;
-  const uint32_t r0 = bgn - c->first_iid, nr = end - bgn + 1;
-  const size_t n = (size_t)nr * H;
+  const uint32_t s0 = 2 * (bgn - c->first_iid), ns = 2 * (end - bgn + 1);
+  const size_t n = (size_t)ns * H;
+  if (n >= 0x7FFFFFFFull) return mfail(M_BAD_PARAM, "index of %zu entries too large", n);
   if (c->keys.alloc(n) || c->vals.alloc(n) || c->keys2.alloc(n) || c->vals2.alloc(n) ||
       c->toff.alloc(H + 1))
     return mfail(M_OOM, "index (%zu entries)", n);
   MHC(hipEventRecord(c->ev[0], s));
-  hipLaunchKernelGGL(k_mh_index_keys, dim3(4096), dim3(256), 0, s, c->minhash.p, r0, nr, H,
-                     c->keys.p, c->vals.p);
+  hipLaunchKernelGGL(k_mh_index_keys, dim3(4096), dim3(256), 0, s, c->minhash.p, c->ocount.p,
+                     s0, ns, H, c->keys.p, c->vals.p);
   MHC(hipGetLastError());
   int end_bit = 32;
   while ((1ll << (end_bit - 32)) <= H) end_bit++;
@@ -1448,18 +1519,7 @@ int mhap_build_index_range(mhap_ctx *c, uint32_t bgn, uint32_t end) {
   return M_OK;
 }
 
-static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_targets,
-                        uint64_t *n_out);
-
-int mhap_compare(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
-  return compare_impl(c, bgn, end, 0, n_out);
-}
-
-int mhap_compare_all(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
-  return compare_impl(c, bgn, end, 1, n_out);
-}
-
-static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_targets,
+static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t self,
                         uint64_t *n_out) {
   if (!c || !c->indexed) return mfail(M_STATE, "mhap_build_index() first");
   if (bgn < c->first_iid || end >= c->first_iid + c->nreads || bgn > end)
@@ -1468,7 +1528,7 @@ static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_ta
   hipStream_t s = c->stream;
   const uint32_t q0 = bgn - c->first_iid, q1 = end - c->first_iid + 1;
   const uint32_t nq = q1 - q0;
-  // stage 2 (grow the candidate buffer and redo on overflow)
+  // first stage (grow the candidate buffer and redo on overflow)
   size_t cap = std::max<size_t>((size_t)nq * 64, 1u << 16);
   uint32_t h[4];
   float ms_cand = 0;
@@ -1476,9 +1536,9 @@ static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_ta
     if (cap > 0xFFFFFFF0ull) return mfail(M_OOM, "candidate list too large");
     if (c->cand.alloc(cap)) return mfail(M_OOM, "candidates");
     MHC(hipMemsetAsync(c->ctr.p, 0, 64, s));
-    CandArgs CA{c->minhash.p, c->keys2.p, c->vals2.p, c->toff.p, (int32_t)c->P.num_hashes,
-                q0, q1, all_targets, c->P.min_matches, c->cand.p, c->ctr.p, (uint32_t)cap,
-                c->ctr.p + 1};
+    CandArgs CA{c->minhash.p, c->ocount.p, c->d_len.p, c->keys2.p, c->vals2.p, c->toff.p,
+                (int32_t)c->P.num_hashes, q0, q1, self, c->P.min_store, c->P.min_matches,
+                c->cand.p, c->ctr.p, (uint32_t)cap, c->ctr.p + 1};
     MHC(hipEventRecord(c->ev[0], s));
     hipLaunchKernelGGL(k_mh_candidates, dim3((nq + 3) / 4), dim3(256),
                        2 * 4 * TSLOTS * sizeof(uint32_t), s, CA);
@@ -1487,24 +1547,24 @@ static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_ta
     MHC(hipMemcpyAsync(h, c->ctr.p, 16, hipMemcpyDeviceToHost, s));
     MHC(hipStreamSynchronize(s));
     ms_cand += elapsed(c);
-    if (h[1] & 1u) return mfail(M_BAD_INPUT, "a query has more than %d candidate targets", TSLOTS);
+    if (h[1] & 1u) return mfail(M_BAD_INPUT, "a query has more than %d candidate strands", TSLOTS);
     if (h[1] & 2u) { cap = (size_t)h[0] + (h[0] >> 2) + 1024; continue; }
     break;
   }
   const uint32_t ncand = h[0];
-  // stage 3
-  size_t rcap = std::max<size_t>(ncand, 1024);
+  // second stage
+  const size_t rcap = std::max<size_t>(ncand, 1024);
   if (c->rec.alloc(rcap)) return mfail(M_OOM, "records");
   MHC(hipMemsetAsync(c->ctr.p + 4, 0, 16, s));
   const int32_t S = (int32_t)c->P.ordered_sketch;
-  CmpArgs MA{c->cand.p, ncand, c->ordered.p, c->ocount.p, c->d_len.p, c->first_iid, S,
-             (int32_t)c->P.ordered_k, c->P.min_olap, c->P.threshold, c->rec.p, c->ctr.p + 4,
-             (uint32_t)rcap, c->ctr.p + 5};
-  const size_t lds = 2 * 8 * ((size_t)S + S + 128);
+  CmpArgs MA{c->cand.p, ncand, c->ordered.p, c->ocount.p, c->d_len.p, S,
+             (int32_t)c->P.ordered_k, c->P.max_shift, c->pass.p, c->pass_empty, c->rec.p,
+             c->ctr.p + 4, (uint32_t)rcap, c->ctr.p + 5};
+  const size_t lds = 3 * 8 * (size_t)S + 1024;
   MHC(hipEventRecord(c->ev[0], s));
   if (ncand) {
-    uint32_t blocks = std::min<uint32_t>((ncand + 1) / 2, 256u * 64u);
-    hipLaunchKernelGGL(k_mh_compare, dim3(blocks), dim3(128), lds, s, MA);
+    const uint32_t blocks = std::min<uint32_t>(ncand, 256u * 64u);
+    hipLaunchKernelGGL(k_mh_compare, dim3(blocks), dim3(64), lds, s, MA);
     MHC(hipGetLastError());
   }
   MHC(hipEventRecord(c->ev[1], s));
@@ -1520,21 +1580,83 @@ static int compare_impl(mhap_ctx *c, uint32_t bgn, uint32_t end, uint32_t all_ta
   return M_OK;
 }
 
+int mhap_compare(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+  return compare_impl(c, bgn, end, 1, n_out);
+}
+
+int mhap_compare_all(mhap_ctx *c, uint32_t bgn, uint32_t end, uint64_t *n_out) {
+  return compare_impl(c, bgn, end, 0, n_out);
+}
+
 int mhap_fetch(mhap_ctx *c, mhap_record *out, uint64_t max_records, uint64_t *n_copied) {
   if (!c) return mfail(M_STATE, "null context");
   MHC(hipSetDevice(c->device));
   std::vector<RecDev> h(c->nrec);
   if (c->nrec) MHC(hipMemcpy(h.data(), c->rec.p, sizeof(RecDev) * c->nrec, hipMemcpyDeviceToHost));
   std::sort(h.begin(), h.end(), [](const RecDev &x, const RecDev &y) {
-    return x.a != y.a ? x.a < y.a : x.b < y.b;
+    return x.a != y.a ? x.a < y.a : x.b != y.b ? x.b < y.b : x.o < y.o;
   });
-  uint64_t n = std::min<uint64_t>(max_records, h.size());
+  const uint64_t n = std::min<uint64_t>(max_records, h.size());
   for (uint64_t i = 0; i < n; i++) {
     const RecDev &r = h[i];
-    out[i] = mhap_record{r.a, r.b, r.erate, r.count, r.a_bgn, r.a_end, r.a_len, r.o,
-                         r.b_bgn, r.b_end, r.b_len};
+    const double score = jaccard_identity(jaccard_of(r.inter, r.n), (int)c->P.ordered_k);
+    out[i] = mhap_record{c->first_iid + r.a, c->first_iid + r.b, 1.0 - std::min(score, 1.0),
+                         (double)r.raw, r.a1, r.a2, r.a_len, r.o, r.b1, r.b2, r.b_len, r.cnt};
   }
   *n_copied = n;
+  return M_OK;
+}
+
+// Java's String.format("%.6f", x): the shortest decimal that reads back as x
+// (FloatingDecimal), rounded half-up to 6 places (FormattedFloatingDecimal.applyPrecision)
+static std::string java_fixed6(double x) {
+  char buf[64];
+  auto res = std::to_chars(buf, buf + sizeof buf, x, std::chars_format::scientific);
+  *res.ptr = 0;
+  // d.ddddde[+-]xx -> digits, exponent
+  std::string mant(buf, strchr(buf, 'e'));
+  const int ex = atoi(strchr(buf, 'e') + 1);
+  bool neg = false;
+  if (!mant.empty() && mant[0] == '-') { neg = true; mant.erase(0, 1); }
+  std::string dig;
+  for (char ch : mant)
+    if (ch != '.') dig += ch;
+  // value = 0.dig * 10^(ex + 1); keep integer part + 6 decimals
+  const int ip = ex + 1;                         // digits before the point
+  std::string intpart, frac;
+  if (ip <= 0) {
+    intpart = "0";
+    frac = std::string(-ip, '0') + dig;
+  } else {
+    if ((int)dig.size() < ip) dig += std::string(ip - dig.size(), '0');
+    intpart = dig.substr(0, ip);
+    frac = dig.substr(ip);
+  }
+  if (frac.size() < 7) frac += std::string(7 - frac.size(), '0');
+  const bool up = frac[6] >= '5';
+  std::string num = intpart + frac.substr(0, 6);
+  if (up) {
+    int i = (int)num.size() - 1;
+    while (i >= 0 && num[i] == '9') num[i--] = '0';
+    if (i >= 0) num[i]++;
+    else num.insert(num.begin(), '1');
+  }
+  std::string s = num.substr(0, num.size() - 6) + "." + num.substr(num.size() - 6);
+  return neg ? "-" + s : s;
+}
+
+int mhap_format_line(const mhap_record *x, uint32_t hash_base, uint32_t num_hash,
+                     uint32_t query_base, char *buf, size_t cap) {
+  if (!x || !buf) return mfail(M_BAD_PARAM, "null argument");
+  if (hash_base == 0 || query_base == 0) return mfail(M_BAD_PARAM, "bases are 1-based IDs");
+  // mhapConvert.C:122-123: a_iid = W0 + (query_base - 1) - num_hash, b_iid = W1 + hash_base - 1
+  const uint64_t w0 = (uint64_t)x->a_iid - (query_base - 1) + num_hash;
+  const uint64_t w1 = (uint64_t)x->b_iid - (hash_base - 1);
+  const int n = snprintf(buf, cap, "%llu %llu %s %s 0 %d %d %d %u %d %d %d",
+                         (unsigned long long)w0, (unsigned long long)w1,
+                         java_fixed6(x->erate).c_str(), java_fixed6(x->raw).c_str(), x->a_bgn,
+                         x->a_end, x->a_len, x->b_rc, x->b_bgn, x->b_end, x->b_len);
+  if (n < 0 || (size_t)n >= cap) return mfail(M_BAD_PARAM, "line buffer too small");
   return M_OK;
 }
 
@@ -1548,14 +1670,12 @@ int mhap_write_text(mhap_ctx *c, const char *path, uint32_t hash_base, uint32_t 
   if (rc) return rc;
   FILE *F = fopen(path, "w");
   if (!F) return mfail(M_BAD_INPUT, "open '%s': %s", path, strerror(errno));
+  char line[256];
   for (uint64_t i = 0; i < n; i++) {
-    const mhap_record &x = r[i];
-    // mhapConvert.C:122-123: a_iid = W0 + (query_base - 1) - num_hash, b_iid = W1 + hash_base - 1
-    const uint64_t w0 = (uint64_t)x.a_iid - (query_base - 1) + num_hash;
-    const uint64_t w1 = (uint64_t)x.b_iid - (hash_base - 1);
-    fprintf(F, "%llu %llu %.6f %u 0 %d %d %d %u %d %d %d\n", (unsigned long long)w0,
-            (unsigned long long)w1, x.erate, x.count, x.a_bgn, x.a_end, x.a_len, x.b_rc,
-            x.b_bgn, x.b_end, x.b_len);
+    rc = mhap_format_line(&r[i], hash_base, num_hash, query_base, line, sizeof line);
+    if (rc) { fclose(F); return rc; }
+    fputs(line, F);
+    fputc('\n', F);
   }
   if (fclose(F) != 0) return mfail(M_BAD_INPUT, "write '%s': %s", path, strerror(errno));
   return M_OK;

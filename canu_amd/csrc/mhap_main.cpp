@@ -10,19 +10,17 @@
 //
 // Read numbering follows the jar's (OverlapMhap.pm:227-232, mhapConvert.C:119-120): the
 // hash block's reads are 1..N, the query files' reads (in file-name order) N+1..N+M.  The
-// compute step reports the hash block against itself (each pair once) unless --no-self,
-// then every query read against every hash read, one line per overlap:
-//   query-id hash-id erate shared-min-mers 0 a-bgn a-end a-len b-rc b-bgn b-end b-len
+// compute step reports the hash block against itself (MinHashSearch's self search: each
+// read against the stored reads of smaller ID) unless --no-self, then every query read
+// against every hash read, one MatchResult line per overlap:
+//   query-id hash-id erate raw-score 0 a-bgn a-end a-len b-rc b-bgn b-end b-len
 // The .dat format is this executable's own (the jar's is internal to it): a header, the
 // read lengths and the three sketch arrays of include/canu_mhap.h.
 //
-// The jar's tf-idf repeat weighting (--repeat-weight, --repeat-idf-scale,
-// --filter-threshold, --no-tf, -f with its fractions) is restated from the published MHAP
-// 2.x algorithm in include/canu_mhap.h (mhap_weighting); parity with the jar itself is
-// unpinned.  Without --repeat-weight (or with a negative one) the sketch is
-// MHAP 1.x's unweighted one and -f k-mers at or above --filter-threshold are left out.
-// --supress-noise (canu: with mhapFilterUnique) is restated from the jar's option text in
-// include/canu_mhap.h (mhap_weighting.supress_noise); unpinned like the rest.
+// The sketch, the weighting (--repeat-weight, --repeat-idf-scale, --filter-threshold,
+// --no-tf, -f with its fractions) and both filter stages are the jar's, read from its
+// bytecode (include/canu_mhap.h, oracle/mhap_jar.py).  --supress-noise 1/2 (the jar's Guava
+// Bloom filter; canu: only with mhapFilterUnique) is refused.
 #include <zlib.h>
 
 #include <algorithm>
@@ -41,7 +39,7 @@
 
 namespace {
 
-const char kMagic[8] = {'C', 'A', 'M', 'H', 'A', 'P', '0', '1'};
+const char kMagic[8] = {'C', 'A', 'M', 'H', 'A', 'P', '0', '2'};
 
 struct Block {
   uint32_t k = 0, H = 0, S = 0, ok = 0, n = 0;
@@ -60,8 +58,7 @@ int usage(const char *prog) {
           "  --ordered-sketch-size n  --ordered-kmer-size n  --min-olap-length n\n"
           "  --num-threads n (ignored: one GPU)   CANU_MHAP_DEVICE picks the GPU\n"
           "  --repeat-weight x  --repeat-idf-scale x  --filter-threshold x  --no-tf\n"
-          "  --supress-noise 0|1|2\n"
-          "                                      (tf-idf repeat weighting, canu_mhap.h)\n",
+          "  --max-shift x  --min-store-length n  --no-rc  --supress-noise 0\n",
           prog, prog);
   return 1;
 }
@@ -85,8 +82,7 @@ bool read_fasta(const char *path, std::vector<uint8_t> &bases, std::vector<uint6
     for (ssize_t i = 0; i < got; i++) {
       char ch = line[i];
       if (ch == '\n' || ch == '\r' || ch == ' ' || ch == '\t') continue;
-      ch = (char)(ch & ~0x20);
-      if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T') ch = 'N';
+      if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);     // the jar reads upper case
       bases.push_back((uint8_t)ch);
       len.back()++;
     }
@@ -130,7 +126,7 @@ bool write_dat(const std::string &path, const Block &b) {
             fwrite(b.len.data(), 4, b.n, F) == b.n &&
             fwrite(b.minhash.data(), 4, b.minhash.size(), F) == b.minhash.size() &&
             fwrite(b.ordered.data(), 8, b.ordered.size(), F) == b.ordered.size() &&
-            fwrite(b.ocount.data(), 4, b.n, F) == b.n;
+            fwrite(b.ocount.data(), 4, b.ocount.size(), F) == b.ocount.size();
   return fclose(F) == 0 && ok;
 }
 
@@ -144,13 +140,13 @@ bool read_dat(const std::string &path, Block &b, std::string &err) {
   if (ok) {
     b.k = hdr[0]; b.H = hdr[1]; b.S = hdr[2]; b.ok = hdr[3]; b.n = hdr[4];
     b.len.resize(b.n);
-    b.minhash.resize((size_t)b.n * b.H);
-    b.ordered.resize((size_t)b.n * b.S);
-    b.ocount.resize(b.n);
+    b.minhash.resize(2ull * b.n * b.H);
+    b.ordered.resize(2ull * b.n * b.S);
+    b.ocount.resize(2ull * b.n);
     ok = fread(b.len.data(), 4, b.n, F) == b.n &&
          fread(b.minhash.data(), 4, b.minhash.size(), F) == b.minhash.size() &&
          fread(b.ordered.data(), 8, b.ordered.size(), F) == b.ordered.size() &&
-         fread(b.ocount.data(), 4, b.n, F) == b.n;
+         fread(b.ocount.data(), 4, b.ocount.size(), F) == b.ocount.size();
   }
   fclose(F);
   if (!ok) err = "'" + path + "' is not a sketch file of this mhap";
@@ -180,15 +176,16 @@ int fail_lib(const char *what) {
   return 1;
 }
 
-void print_records(mhap_ctx *ctx, uint64_t n) {
+int print_records(mhap_ctx *ctx, uint64_t n) {
   std::vector<mhap_record> r(n);
   uint64_t got = 0;
-  if (n && mhap_fetch(ctx, r.data(), n, &got) != 0) return;
+  if (n && mhap_fetch(ctx, r.data(), n, &got) != 0) return fail_lib("fetch");
+  char line[256];
   for (uint64_t i = 0; i < got; i++) {
-    const mhap_record &x = r[i];
-    printf("%u %u %.6f %u 0 %d %d %d %u %d %d %d\n", x.a_iid, x.b_iid, x.erate, x.count,
-           x.a_bgn, x.a_end, x.a_len, x.b_rc, x.b_bgn, x.b_end, x.b_len);
+    if (mhap_format_line(&r[i], 1, 0, 1, line, sizeof line) != 0) return fail_lib("format");
+    puts(line);
   }
+  return 0;
 }
 
 }  // namespace
@@ -217,6 +214,9 @@ int main(int argc, char **argv) {
     else if (a == "--ordered-sketch-size") P.ordered_sketch = (uint32_t)atoi(num("--ordered-sketch-size"));
     else if (a == "--ordered-kmer-size") P.ordered_k = (uint32_t)atoi(num("--ordered-kmer-size"));
     else if (a == "--min-olap-length") P.min_olap = atoi(num("--min-olap-length"));
+    else if (a == "--max-shift") P.max_shift = atof(num("--max-shift"));
+    else if (a == "--min-store-length") P.min_store = atoi(num("--min-store-length"));
+    else if (a == "--no-rc") P.no_rc = 1;
     else if (a == "--num-threads") num("--num-threads");
     else if (a == "--filter-threshold") W.filter_threshold = atof(num("--filter-threshold"));
     else if (a == "--repeat-weight") W.repeat_weight = atof(num("--repeat-weight"));
@@ -233,6 +233,11 @@ int main(int argc, char **argv) {
       fprintf(stderr, "mhap: unknown option '%s'\n", a.c_str());
       return usage(argv[0]);
     }
+  }
+  if (W.supress_noise != 0) {
+    fprintf(stderr, "mhap: --supress-noise %d: the jar's Bloom-filter noise suppression is not "
+                    "implemented\n", W.supress_noise);
+    return 1;
   }
   if ((fasta != nullptr) == (spath != nullptr)) {
     fprintf(stderr, "mhap: give either -p (precompute) or -s (compute)\n");
@@ -261,9 +266,9 @@ int main(int argc, char **argv) {
     b.k = P.k; b.H = P.num_hashes; b.S = P.ordered_sketch; b.ok = P.ordered_k;
     b.n = (uint32_t)len.size();
     b.len = len;
-    b.minhash.resize((size_t)b.n * b.H);
-    b.ordered.resize((size_t)b.n * b.S);
-    b.ocount.resize(b.n);
+    b.minhash.resize(2ull * b.n * b.H);
+    b.ordered.resize(2ull * b.n * b.S);
+    b.ocount.resize(2ull * b.n);
     if (b.n) {
       if (mhap_load_reads(ctx, 1, b.n, bases.data(), off.data(), len.data()) != 0) {
         rc = fail_lib("load");
@@ -273,9 +278,9 @@ int main(int argc, char **argv) {
         if (fpath && !read_filter(fpath, P.k, kmers, fr)) {
           fprintf(stderr, "mhap: cannot read filter '%s'\n", fpath);
           rc = 1;
-        } else if ((fpath || W.repeat_weight >= 0.0) &&
-                   mhap_set_kmer_frequencies(ctx, kmers.data(), fr.data(), fr.size(), &W) != 0) {
-          rc = fail_lib("k-mer frequencies");
+        } else if (fpath ? mhap_set_kmer_frequencies(ctx, kmers.data(), fr.data(), fr.size(), &W)
+                         : mhap_set_weighting(ctx, &W)) {
+          rc = fail_lib("weighting");
         }
       }
       if (!rc && mhap_sketch(ctx, 1, b.n) != 0) rc = fail_lib("sketch");
@@ -350,11 +355,11 @@ int main(int argc, char **argv) {
       uint64_t n = 0;
       if (!rc && !no_self) {
         if (mhap_compare(ctx, 1, hb.n, &n) != 0) rc = fail_lib("compare (self)");
-        else print_records(ctx, n);
+        else rc = print_records(ctx, n);
       }
       if (!rc && nq) {
         if (mhap_compare_all(ctx, hb.n + 1, (uint32_t)ntot, &n) != 0) rc = fail_lib("compare");
-        else print_records(ctx, n);
+        else rc = print_records(ctx, n);
       }
     }
     if (fflush(stdout) != 0) rc = 1;

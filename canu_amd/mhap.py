@@ -15,18 +15,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libcanu_mhap.so")
 
 # the C struct mhap_record
-MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("count", "<u4"),
+MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("raw", "<f8"),
                        ("a_bgn", "<i4"), ("a_end", "<i4"), ("a_len", "<i4"), ("o", "<u4"),
-                       ("b_bgn", "<i4"), ("b_end", "<i4"), ("b_len", "<i4")], align=True)
+                       ("b_bgn", "<i4"), ("b_end", "<i4"), ("b_len", "<i4"),
+                       ("count", "<u4")], align=True)
 
 EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last_error",
            "mhap_abi_version", "mhap_load_reads", "mhap_load_reads_device",
-           "mhap_set_filter_kmers", "mhap_sketch", "mhap_sketch_buffers", "mhap_copy_sketches",
+           "mhap_set_weighting", "mhap_sketch", "mhap_sketch_buffers", "mhap_copy_sketches",
            "mhap_build_index", "mhap_build_index_range", "mhap_compare_all",
            "mhap_copy_sketches_host", "mhap_weighting_init", "mhap_set_kmer_frequencies",
-           "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_get_stats"]
+           "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_format_line",
+           "mhap_get_stats"]
 
-ABI_VERSION = 5          # MHAP_ABI_VERSION of include/canu_mhap.h
+ABI_VERSION = 6          # MHAP_ABI_VERSION of include/canu_mhap.h
 
 
 class MhapError(RuntimeError):
@@ -39,7 +41,8 @@ class _Params(ctypes.Structure):
     _fields_ = [("k", ctypes.c_uint32), ("num_hashes", ctypes.c_uint32),
                 ("min_matches", ctypes.c_uint32), ("ordered_sketch", ctypes.c_uint32),
                 ("ordered_k", ctypes.c_uint32), ("min_olap", ctypes.c_int32),
-                ("threshold", ctypes.c_double)]
+                ("threshold", ctypes.c_double), ("max_shift", ctypes.c_double),
+                ("min_store", ctypes.c_int32), ("no_rc", ctypes.c_int32)]
 
 
 class _Weighting(ctypes.Structure):
@@ -53,7 +56,8 @@ class _Stats(ctypes.Structure):
                 ("overlaps", ctypes.c_uint64), ("ms_sketch", ctypes.c_double),
                 ("ms_index", ctypes.c_double), ("ms_candidates", ctypes.c_double),
                 ("ms_compare", ctypes.c_double), ("sketch_kmers", ctypes.c_uint64),
-                ("ms_sketch_kernel", ctypes.c_double), ("sketch_launches", ctypes.c_uint64)]
+                ("ms_sketch_kernel", ctypes.c_double), ("sketch_launches", ctypes.c_uint64),
+                ("sketch_draws", ctypes.c_uint64)]
 
 
 _lib = None
@@ -78,7 +82,7 @@ def load_library(path: str | None = None):
     lib.mhap_last_error.restype = ctypes.c_char_p
     lib.mhap_load_reads.argtypes = [V, U32, U32, V, V, V]
     lib.mhap_load_reads_device.argtypes = [V, U32, U32, V, V, V]
-    lib.mhap_set_filter_kmers.argtypes = [V, ctypes.c_char_p, U64]
+    lib.mhap_set_weighting.argtypes = [V, P(_Weighting)]
     lib.mhap_sketch.argtypes = [V, U32, U32]
     lib.mhap_sketch_buffers.argtypes = [V, P(V), P(V), P(V)]
     lib.mhap_copy_sketches.argtypes = [V, U32, U32, V, V, V, ctypes.c_int]
@@ -89,6 +93,7 @@ def load_library(path: str | None = None):
     lib.mhap_compare.argtypes = [V, U32, U32, P(U64)]
     lib.mhap_fetch.argtypes = [V, V, U64, P(U64)]
     lib.mhap_write_text.argtypes = [V, ctypes.c_char_p, U32, U32, U32]
+    lib.mhap_format_line.argtypes = [V, U32, U32, U32, ctypes.c_char_p, ctypes.c_size_t]
     lib.mhap_get_stats.argtypes = [V, P(_Stats)]
     lib.mhap_weighting_init.argtypes = [P(_Weighting)]
     lib.mhap_set_kmer_frequencies.argtypes = [V, ctypes.c_char_p, V, U64, P(_Weighting)]
@@ -98,7 +103,8 @@ def load_library(path: str | None = None):
 
 @dataclasses.dataclass
 class MhapParameters:
-    """MHAP options canu sets (OverlapMhap.pm:109-150; Defaults.pm:698-706)."""
+    """MHAP options canu sets (OverlapMhap.pm:109-150, :380-392; Defaults.pm:698-706) and
+    the jar's own defaults for the rest (MhapMain.<init> option table)."""
     k: int = 16
     num_hashes: int = 512
     num_min_matches: int = 3
@@ -106,14 +112,18 @@ class MhapParameters:
     ordered_sketch_size: int = 1536
     ordered_kmer_size: int = 12
     min_olap_length: int = 500
-    # repeat weighting (canu_mhap.h mhap_weighting; canu passes --repeat-weight 0.9
-    # --repeat-idf-scale 10 --filter-threshold, OverlapMhap.pm:382, :390); < 0: unweighted
-    repeat_weight: float = -1.0
-    repeat_idf_scale: float = 10.0
+    max_shift: float = 0.2
+    min_store_length: int = 0
+    no_rc: bool = False
+    # repeat weighting (canu_mhap.h mhap_weighting; the jar's defaults 0.9 / 3 / 1e-5, canu
+    # passes --repeat-weight 0.9 --repeat-idf-scale 10 --filter-threshold, OverlapMhap.pm:382,
+    # :390); without -f frequencies a k-mer weighs its count (repeat_weight >= 0) or 1
+    repeat_weight: float = 0.9
+    repeat_idf_scale: float = 3.0
     filter_threshold: float = 1e-5
     no_tf: bool = False
-    # --supress-noise (canu passes 2 with mhapFilterUnique, OverlapMhap.pm:383): k-mers not
-    # in the -f file removed (1) or weighted like the most frequent one (2); canu_mhap.h
+    # --supress-noise 1 / 2 (canu: with mhapFilterUnique, OverlapMhap.pm:483) build a Guava
+    # Bloom filter in the jar; not implemented: the library refuses them
     supress_noise: int = 0
 
     @classmethod
@@ -142,7 +152,8 @@ class MhapParameters:
 
     def to_c(self) -> _Params:
         return _Params(self.k, self.num_hashes, self.num_min_matches, self.ordered_sketch_size,
-                       self.ordered_kmer_size, self.min_olap_length, self.threshold)
+                       self.ordered_kmer_size, self.min_olap_length, self.threshold,
+                       self.max_shift, self.min_store_length, 1 if self.no_rc else 0)
 
     def weighting_c(self) -> _Weighting:
         return _Weighting(self.repeat_weight, self.repeat_idf_scale, self.filter_threshold,
@@ -161,7 +172,8 @@ class MhapParameters:
                     ordered_k=self.ordered_kmer_size, min_olap=self.min_olap_length,
                     repeat_weight=self.repeat_weight, repeat_idf_scale=self.repeat_idf_scale,
                     filter_threshold=self.filter_threshold, no_tf=bool(self.no_tf),
-                    supress_noise=int(self.supress_noise))
+                    supress_noise=int(self.supress_noise), max_shift=self.max_shift,
+                    min_store=self.min_store_length, no_rc=bool(self.no_rc))
 
 
 def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
@@ -188,6 +200,12 @@ def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
             p.ordered_kmer_size = int(val); i += 1
         elif a == "--min-olap-length":
             p.min_olap_length = int(val); i += 1
+        elif a == "--max-shift":
+            p.max_shift = float(val); i += 1
+        elif a == "--min-store-length":
+            p.min_store_length = int(val); i += 1
+        elif a == "--no-rc":
+            p.no_rc = True
         elif a in ("-f", "-p", "-q", "-s", "--num-threads"):
             io[a] = val; i += 1
         elif a == "--repeat-weight":
@@ -273,13 +291,13 @@ class Mhap:
                                                     d_bases, d_offsets, lens.ctypes.data))
         self.first_iid, self.nreads = first_iid, int(lens.shape[0])
 
-    def set_filter_kmers(self, kmers: list[str]) -> None:
-        blob = "".join(kmers).encode()
-        self._check(self.lib.mhap_set_filter_kmers(self.ctx, blob, len(kmers)))
+    def set_weighting(self) -> None:
+        """This job's weighting options (params.repeat_weight ...) without a -f table."""
+        w = self.params.weighting_c()
+        self._check(self.lib.mhap_set_weighting(self.ctx, ctypes.byref(w)))
 
     def set_kmer_frequencies(self, kmers: list[str], fractions) -> None:
-        """-f with fractions, under this job's weighting options (params.repeat_weight ...):
-        weighted sketches when repeat_weight >= 0 (no k-mers: tf weighting alone)."""
+        """-f with fractions (file order), under this job's weighting options."""
         blob = "".join(kmers).encode()
         fr = np.ascontiguousarray(fractions, dtype=np.float64)
         w = self.params.weighting_c()
@@ -316,8 +334,9 @@ class Mhap:
 
     def compare(self, bgn: int | None = None, end: int | None = None,
                 all_targets: bool = False) -> int:
-        """Queries bgn..end against the indexed reads with larger IDs, or (all_targets)
-        against every indexed read but themselves."""
+        """The jar's self search: queries bgn..end (forward strands) against the indexed
+        strands of reads with smaller IDs; or (all_targets, the -q search) against every
+        indexed read but themselves."""
         bgn = self.first_iid if bgn is None else bgn
         end = self.first_iid + self.nreads - 1 if end is None else end
         n = ctypes.c_uint64()
@@ -342,26 +361,33 @@ class Mhap:
         self._check(self.lib.mhap_get_stats(self.ctx, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in _Stats._fields_}
 
-    def run(self, rs, filter_kmers=None, frequencies=None) -> np.ndarray:
-        """One all-vs-all job over rs: every pair (a < b) once, records sorted by (a, b).
-        frequencies = (k-mers, fractions) of a -f file; with params.repeat_weight >= 0 the
-        sketches are weighted (tf weighting alone when no frequencies are given)."""
+    def run(self, rs, frequencies=None) -> np.ndarray:
+        """The jar's self job over rs (-s block without --no-self): records sorted by
+        (a, b, o), a the query (larger ID).  frequencies = (k-mers, fractions) of a -f
+        file."""
         self.load_reads(rs)
-        if filter_kmers:
-            self.set_filter_kmers(filter_kmers)
-        if frequencies is not None or self.params.repeat_weight >= 0:
-            km, fr = frequencies if frequencies is not None else ([], np.zeros(0))
+        if frequencies is not None:
+            km, fr = frequencies
             self.set_kmer_frequencies(list(km), fr)
+        else:
+            self.set_weighting()
         self.sketch()
         self.build_index()
         self.compare()
         return self.fetch()
 
 
+def java_fixed6(x: float) -> str:
+    """String.format("%.6f", x) as Java does it: the shortest decimal that reads back as x
+    (FloatingDecimal), rounded half-up to 6 places (FormattedFloatingDecimal)."""
+    from decimal import Decimal, ROUND_HALF_UP
+    return str(Decimal(repr(float(x))).quantize(Decimal("0.000001"), rounding=ROUND_HALF_UP))
+
+
 def format_line(r, hash_base: int = 1, num_hash: int = 0, query_base: int = 1) -> str:
-    """One record as MHAP's text line (the layout mhap_write_text writes)."""
+    """One record as MatchResult.toString's line (the layout mhap_write_text writes)."""
     w0 = int(r["a"]) - (query_base - 1) + num_hash
     w1 = int(r["b"]) - (hash_base - 1)
-    return (f"{w0} {w1} {float(r['erate']):.6f} {int(r['count'])} 0 {int(r['a_bgn'])} "
-            f"{int(r['a_end'])} {int(r['a_len'])} {int(r['o'])} {int(r['b_bgn'])} "
-            f"{int(r['b_end'])} {int(r['b_len'])}")
+    return (f"{w0} {w1} {java_fixed6(r['erate'])} {java_fixed6(r['raw'])} 0 "
+            f"{int(r['a_bgn'])} {int(r['a_end'])} {int(r['a_len'])} {int(r['o'])} "
+            f"{int(r['b_bgn'])} {int(r['b_end'])} {int(r['b_len'])}")

@@ -180,6 +180,105 @@ def seq_hashes_int(s: bytes, k: int) -> np.ndarray:
                     dtype=np.int32)
 
 
+# ---- the same two hashes over every window of a sequence at once (numpy) ----------------
+# Equal, element for element, to seq_hashes_long(s, k, False) / seq_hashes_int(s, k) above
+# (tests/test_mhap.py checks both against each other); used by the sketches below for speed.
+def _windows(s: bytes, k: int) -> np.ndarray:
+    a = np.frombuffer(s, dtype=np.uint8).astype(np.uint64)
+    return np.lib.stride_tricks.sliding_window_view(a, k)
+
+
+def _u64(v: int) -> np.uint64:
+    return np.uint64(v & M64)
+
+
+def _rotl64_np(x, r):
+    return (x << np.uint64(r)) | (x >> np.uint64(64 - r))
+
+
+def _fmix64_np(k):
+    k = k ^ (k >> np.uint64(33))
+    k = k * _u64(0xFF51AFD7ED558CCD)
+    k = k ^ (k >> np.uint64(33))
+    k = k * _u64(0xC4CEB9FE1A85EC53)
+    return k ^ (k >> np.uint64(33))
+
+
+def _lanes64(w: np.ndarray, c0: int, n: int) -> np.ndarray:
+    """Chars c0 .. c0+n-1 (n <= 4) of every window as little-endian UTF-16 in one u64."""
+    v = np.zeros(w.shape[0], dtype=np.uint64)
+    for j in range(n):
+        v |= w[:, c0 + j] << np.uint64(16 * j)
+    return v
+
+
+def murmur128_h1_windows(s: bytes, k: int) -> np.ndarray:
+    """murmur3_128_h1(_chars(window)) of every k-window of s, int64."""
+    n = len(s) - k + 1
+    if n <= 0:
+        return np.zeros(0, dtype=np.int64)
+    w = _windows(s, k)
+    c1, c2 = _u64(0x87C37B91114253D5), _u64(0x4CF5AD432745937F)
+    h1 = np.zeros(n, dtype=np.uint64)
+    h2 = np.zeros(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        nb = k // 8                                   # 16-byte blocks = 8 chars
+        for b in range(nb):
+            k1 = _lanes64(w, 8 * b, 4)
+            k2 = _lanes64(w, 8 * b + 4, 4)
+            k1 = _rotl64_np(k1 * c1, 31) * c2
+            h1 ^= k1
+            h1 = _rotl64_np(h1, 27) + h2
+            h1 = h1 * np.uint64(5) + np.uint64(0x52DCE729)
+            k2 = _rotl64_np(k2 * c2, 33) * c1
+            h2 ^= k2
+            h2 = _rotl64_np(h2, 31) + h1
+            h2 = h2 * np.uint64(5) + np.uint64(0x38495AB5)
+        t = k - 8 * nb                                # tail chars
+        if t > 4:
+            k2 = _lanes64(w, 8 * nb + 4, t - 4)
+            h2 ^= _rotl64_np(k2 * c2, 33) * c1
+        if t > 0:
+            k1 = _lanes64(w, 8 * nb, min(t, 4))
+            h1 ^= _rotl64_np(k1 * c1, 31) * c2
+        h1 ^= np.uint64(2 * k)
+        h2 ^= np.uint64(2 * k)
+        h1 = h1 + h2
+        h2 = h2 + h1
+        h1 = _fmix64_np(h1)
+        h2 = _fmix64_np(h2)
+        h1 = h1 + h2
+    return h1.view(np.int64)
+
+
+def murmur32_windows(s: bytes, k: int) -> np.ndarray:
+    """murmur3_32(_chars(window)) of every k-window of s, int32."""
+    n = len(s) - k + 1
+    if n <= 0:
+        return np.zeros(0, dtype=np.int32)
+    w = _windows(s, k).astype(np.uint32)
+    c1, c2 = np.uint32(0xCC9E2D51), np.uint32(0x1B873593)
+    h = np.zeros(n, dtype=np.uint32)
+
+    def rotl(x, r):
+        return (x << np.uint32(r)) | (x >> np.uint32(32 - r))
+
+    with np.errstate(over="ignore"):
+        for b in range(k // 2):                       # 4-byte blocks = 2 chars
+            kk = w[:, 2 * b] | (w[:, 2 * b + 1] << np.uint32(16))
+            h ^= rotl(kk * c1, 15) * c2
+            h = rotl(h, 13) * np.uint32(5) + np.uint32(0xE6546B64)
+        if k % 2:
+            h ^= rotl(w[:, k - 1] * c1, 15) * c2
+        h ^= np.uint32(2 * k)
+        h ^= h >> np.uint32(16)
+        h = h * np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h = h * np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+    return h.view(np.int32)
+
+
 # ---- FrequencyCounts (-f) ----------------------------------------------------------------
 class FrequencyCounts:
     """FrequencyCounts.<init>(reader, filterCutoff, offset, removeUnique, noTf, threads,
@@ -231,6 +330,12 @@ class FrequencyCounts:
         return 1.0 + (idf - self.min_idf) / scale
 
 
+def i32(x: int) -> int:
+    """Java int arithmetic: wrap to a signed 32-bit value."""
+    x &= M32
+    return x - (1 << 32) if x >> 31 else x
+
+
 def java_round(x: float) -> int:
     """Math.round(double): the closest long, ties toward positive infinity."""
     r = math.floor(x)
@@ -238,15 +343,6 @@ def java_round(x: float) -> int:
 
 
 # ---- MinHashSketch.computeNgramMinHashesWeighted -----------------------------------------
-def _xorshift_steps(x: np.ndarray, n: int) -> np.ndarray:
-    with np.errstate(over="ignore"):
-        for _ in range(n):
-            x ^= x << np.uint64(21)
-            x ^= x >> np.uint64(35)
-            x ^= x << np.uint64(4)
-    return x
-
-
 def minhash(s: bytes, p: dict, fc: FrequencyCounts | None):
     """MinHashSketch.computeNgramMinHashesWeighted(s, k, H, filter, false, repeatWeight)
     @0-476: None when the sequence has no k-mer (@10-26 / @142-160 / @458-473: the read is
@@ -263,10 +359,10 @@ def minhash(s: bytes, p: dict, fc: FrequencyCounts | None):
     k, H = p["k"], p["num_hashes"]
     if len(s) - k + 1 < 1:
         return None
-    keys = seq_hashes_long(s, k, False)
-    counts = {}
-    for key in keys:                                 # dict keeps insertion order
-        counts[key] = counts.get(key, 0) + 1
+    keys = murmur128_h1_windows(s, k)                # = seq_hashes_long(s, k, False)
+    uk, first, cnt = np.unique(keys, return_index=True, return_counts=True)
+    order = np.argsort(first, kind="stable")          # LinkedOpenHashMap: insertion order
+    counts = dict(zip(uk[order].tolist(), cnt[order].tolist()))
     if not counts:
         return None
     rw = float(p["repeat_weight"])
@@ -289,24 +385,30 @@ def minhash(s: bytes, p: dict, fc: FrequencyCounts | None):
         return None
     key_u = np.array([kk & M64 for kk in ks], dtype=np.uint64)
     w = np.array(ws, dtype=np.int64)
-    x = key_u.copy()
     out = np.zeros(max(1, H), dtype=np.int32)
     lo = (key_u & np.uint64(M32)).astype(np.uint32).view(np.int32)
     hi = (key_u >> np.uint64(32)).astype(np.uint32).view(np.int32)
-    wmax = int(w.max())
-    for j in range(H):
-        best = np.full(x.shape[0], LONG_MAX, dtype=np.int64)
-        for t in range(wmax):
-            act = t < w
-            xa = _xorshift_steps(x[act], 1)
-            x[act] = xa
-            v = xa.view(np.int64)
-            cur = best[act]
-            best[act] = np.where(v < cur, v, cur)
-        # strictly smaller wins: the first key (insertion order) among equal minima
-        i = int(np.argmin(best))
-        if best[i] < LONG_MAX:
-            out[j] = lo[i] if j % 2 == 0 else hi[i]
+    # the keys' chains advance independently, so keys of equal weight are stepped together
+    # (a class), each class's minimum scattered back into insertion order per word
+    classes = [(int(c), np.flatnonzero(w == c)) for c in np.unique(w)]
+    xs = [key_u[idx].copy() for _, idx in classes]
+    best = np.empty(key_u.shape[0], dtype=np.int64)
+    with np.errstate(over="ignore"):
+        for j in range(H):
+            for ci, (wc, idx) in enumerate(classes):
+                x = xs[ci]
+                b = None
+                for _ in range(wc):
+                    x ^= x << np.uint64(21)
+                    x ^= x >> np.uint64(35)
+                    x ^= x << np.uint64(4)
+                    v = x.view(np.int64)
+                    b = v.copy() if b is None else np.minimum(b, v)
+                best[idx] = b
+            # strictly smaller wins: the first key (insertion order) among equal minima
+            i = int(np.argmin(best))
+            if best[i] < LONG_MAX:
+                out[j] = lo[i] if j % 2 == 0 else hi[i]
     return out
 
 
@@ -320,7 +422,7 @@ def ordered_sketch(s: bytes, p: dict):
     n = len(s) - kk + 1
     if n <= 0:
         return None
-    h = seq_hashes_int(s, kk)
+    h = murmur32_windows(s, kk)                      # = seq_hashes_int(s, kk)
     perm = np.argsort(h, kind="stable")[:min(S, n)]
     return h[perm].astype(np.int32), perm.astype(np.int32), n
 
@@ -397,10 +499,13 @@ class _MatchData:
             c += 1
         if c < 3:
             return None
-        a1 = max(0, java_round((c * l1 - r1) / float(c - 1)))
-        a2 = min(self.sl1, java_round((c * r1 - l1) / float(c - 1)))
-        b1 = max(0, java_round((c * l2 - r2) / float(c - 1)))
-        b2 = min(self.sl2, java_round((c * r2 - l2) / float(c - 1)))
+        # imul / isub (wrapping), i2d, ddiv, Math.round, l2i
+        def edge(x, y):
+            return i32(java_round(i32(i32(c * x) - y) / float(c - 1)))
+        a1 = max(0, edge(l1, r1))
+        a2 = min(self.sl1, edge(r1, l1))
+        b1 = max(0, edge(l2, r2))
+        b2 = min(self.sl2, edge(r2, l2))
         return a1, a2, b1, b2, c
 
 
@@ -452,14 +557,76 @@ def _record_matching(md: _MatchData, s1, s2):
             i1, i2 = l1 + 1, l2 + 1
 
 
-def overlap_info(A, B, max_shift: float, kk: int):
+def _groups(h1s, h2s):
+    """The hashes present in both sorted sketches: [(a0, a1, b0, b1)] index ranges, in
+    hash order."""
+    u1, i1, c1 = np.unique(h1s, return_index=True, return_counts=True)
+    u2, i2, c2 = np.unique(h2s, return_index=True, return_counts=True)
+    _, x1, x2 = np.intersect1d(u1, u2, assume_unique=True, return_indices=True)
+    return [(int(i1[a]), int(i1[a] + c1[a]), int(i2[b]), int(i2[b] + c2[b]))
+            for a, b in zip(x1, x2)]
+
+
+def _record_matching_groups(md: _MatchData, groups, p1s, p2s):
+    """_record_matching, one group of equal hashes at a time: the merge records only
+    entries of equal hash and enters every group at the group's first entries on both sides
+    (a smaller hash on either side is stepped over, whatever the windows), so the groups are
+    independent and their records come out in hash order (tests/test_mhap.py checks this
+    form against the merge itself)."""
+    v1lo, v2lo, v1hi, v2hi = md.valid()
+    m, amax = md.median, md.absmax
+    md.reset()
+    for a0, a1, b0, b1 in groups:
+        i1, i2 = a0, b0
+        while i1 < a1 and i2 < b1:
+            p1 = p1s[i1]
+            if p1 < v1lo or p1 >= v1hi:
+                i1 += 1
+                continue
+            p2 = p2s[i2]
+            if p2 < v2lo or p2 >= v2hi:
+                i2 += 1
+                continue
+            d = p2 - p1 - m
+            if d > amax:
+                i1 += 1
+                continue
+            if d < -amax:
+                i2 += 1
+                continue
+            md.record(p1, p2, p2 - p1)
+            l1 = i1
+            while l1 + 1 < a1 and v1lo <= p1s[l1 + 1] < v1hi:
+                l1 += 1
+            l2 = i2
+            while l2 + 1 < b1 and v2lo <= p2s[l2 + 1] < v2hi:
+                l2 += 1
+            if i1 == l1 and i2 == l2:
+                i1 += 1
+                i2 += 1
+            else:
+                md.record(p1s[l1], p2s[l2], p2s[l2] - p1s[l1])
+                i1, i2 = l1 + 1, l2 + 1
+
+
+def overlap_info(A, B, max_shift: float, kk: int, literal: bool = False):
     """BottomOverlapSketch.getOverlapInfo(other, maxShift) @0-211: None (EMPTY) or
-    (score, raw, a1, a2, b1, b2).  A, B = (hashes, positions, seqLength)."""
+    (score, raw, a1, a2, b1, b2).  A, B = (hashes, positions, seqLength).  literal: run the
+    jar's merge itself instead of its group form (same records)."""
     md = _MatchData(A[2], B[2], max_shift)
-    _record_matching(md, A[:2], B[:2])
+    if literal:
+        def rec():
+            _record_matching(md, A[:2], B[:2])
+    else:
+        groups = _groups(A[0], B[0])
+        p1s, p2s = A[1].tolist(), B[1].tolist()
+
+        def rec():
+            _record_matching_groups(md, groups, p1s, p2s)
+    rec()
     if not md.sh:
         return None
-    _record_matching(md, A[:2], B[:2])
+    rec()
     if not md.sh:
         return None
     md.optimize()
@@ -469,18 +636,19 @@ def overlap_info(A, B, max_shift: float, kk: int):
     if e is None:
         return None
     a1, a2, b1, b2, c = e
-    # computeKBottomSketchJaccard @0-227 (entries of each sketch inside its edge range)
-    sel1 = [(int(h), int(q)) for h, q in zip(A[0], A[1]) if a1 <= q <= a2]
-    sel2 = [(int(h), int(q)) for h, q in zip(B[0], B[1]) if b1 <= q <= b2]
+    # computeKBottomSketchJaccard @0-227 (entries of each sketch inside its edge range, in
+    # sketch order)
+    sel1 = A[0][(A[1] >= a1) & (A[1] <= a2)].tolist()
+    sel2 = B[0][(B[1] >= b1) & (B[1] <= b2)].tolist()
     n = min(len(sel1), len(sel2))
     if n == 0:
         J = 0.0
     else:
         i = j = inter = 0
         for _ in range(n):
-            if sel1[i][0] < sel2[j][0]:
+            if sel1[i] < sel2[j]:
                 i += 1
-            elif sel1[i][0] > sel2[j][0]:
+            elif sel1[i] > sel2[j]:
                 j += 1
             else:
                 inter += 1
@@ -498,7 +666,8 @@ def overlap_info(A, B, max_shift: float, kk: int):
 
 MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("raw", "<f8"),
                        ("a_bgn", "<i4"), ("a_end", "<i4"), ("a_len", "<i4"), ("o", "<u4"),
-                       ("b_bgn", "<i4"), ("b_end", "<i4"), ("b_len", "<i4")])
+                       ("b_bgn", "<i4"), ("b_end", "<i4"), ("b_len", "<i4"),
+                       ("count", "<u4")])
 
 
 def sketch_read(s: bytes, p: dict, fc):
@@ -537,16 +706,33 @@ def sketches(rs, p: dict, fc=None, reads=None):
     return out
 
 
+def sketch_rows(rs, p: dict, freq=None, reads=None):
+    """The sketches in the library's layout (canu_mhap.h mhap_sketch_buffers): minhash
+    int32 [n][2][H], ordered uint64 [n][2][S] ((hash ^ 0x80000000) << 32 | position),
+    ocount uint32 [n][2] (0: strand not stored); rows of reads not sketched stay zero."""
+    fc = FrequencyCounts(freq[0], freq[1], p) if freq is not None else None
+    n, H, S = rs.nreads, p["num_hashes"], p["ordered_sketch"]
+    mh = np.zeros((n, 2, H), dtype=np.int32)
+    od = np.zeros((n, 2, S), dtype=np.uint64)
+    oc = np.zeros((n, 2), dtype=np.uint32)
+    for (i, st), (m, (h, pos, _), _) in sketches(rs, p, fc, reads).items():
+        mh[i, st] = m
+        oc[i, st] = h.shape[0]
+        od[i, st, :h.shape[0]] = ((h.view(np.uint32) ^ np.uint32(0x80000000)).astype(np.uint64)
+                                  << np.uint64(32)) | pos.astype(np.uint64)
+    return mh, od, oc
+
+
 def find_matches(q_id, q, store: dict, p: dict, to_self: bool):
     """MinHashSearch.findMatches(query, toSelf) @0-610: the stored sketches sharing at
     least --num-min-matches min-mers with the query (per hash function j: query[j] equal
     to the stored sketch's [j]), then the length / self rules and the second stage.
-    Returns [(target id, overlap info)] for accepted targets."""
+    Returns [(target id, shared count, overlap info)] for accepted targets."""
     out = []
     qmh, qosk, qlen = q
-    ms = p["min_store"]
+    ms = p.get("min_store", 0)
     for t_id, (tmh, tosk, tlen) in store.items():
-        if to_self and t_id[0] == q_id[0]:
+        if t_id[0] == q_id[0]:
             continue
         cnt = int((qmh == tmh).sum())
         if cnt < p["min_matches"]:
@@ -557,17 +743,17 @@ def find_matches(q_id, q, store: dict, p: dict, to_self: bool):
             continue
         if to_self and tlen < ms and qlen >= ms:             # @465-492
             continue
-        oi = overlap_info(qosk, tosk, p["max_shift"], p["ordered_k"])
+        oi = overlap_info(qosk, tosk, p.get("max_shift", 0.2), p["ordered_k"])
         if oi is None:
             continue
         if oi[0] >= p["threshold"]:
-            out.append((t_id, oi))
+            out.append((t_id, cnt, oi))
     return out
 
 
-def match_record(q_id, t_id, oi, qlen: int, tlen: int, first_iid: int):
+def match_record(q_id, t_id, cnt, oi, qlen: int, tlen: int, first_iid: int):
     """MatchResult.<init> @0-179: reverse-strand coordinates mirrored as len - x - 1, the
-    score capped at 1; the row of MatchResult.toString."""
+    score capped at 1; the row of MatchResult.toString (+ the first-stage count)."""
     score, raw, a1, a2, b1, b2 = oi
     if q_id[1]:
         a1, a2 = qlen - a2 - 1, qlen - a1 - 1
@@ -575,19 +761,31 @@ def match_record(q_id, t_id, oi, qlen: int, tlen: int, first_iid: int):
         b1, b2 = tlen - b2 - 1, tlen - b1 - 1
     score = min(score, 1.0)
     return (first_iid + q_id[0], first_iid + t_id[0], 1.0 - score, raw, a1, a2, qlen,
-            t_id[1], b1, b2, tlen)
+            t_id[1], b1, b2, tlen, cnt)
 
 
-def run_self(rs, p: dict, freq=None) -> np.ndarray:
-    """The jar's -s block against itself: every stored forward sketch as a query
-    (AbstractMatchSearch.findMatches() over getStoredForwardSequenceIds), toSelf = true.
-    Rows sorted by (a, b, o)."""
+def run(rs, p: dict, freq=None, q_range=None, t_range=None, to_self: bool = True) -> np.ndarray:
+    """The jar's compute step over rs: the stored reads t_range (0-based [lo, hi), default
+    all; both strands, AbstractMatchSearch's store) searched by the forward sketches of the
+    query reads q_range (default: the stored reads, the -s self search).  to_self: the self
+    search (MinHashSearch.findMatches toSelf: only stored reads of smaller ID); False: the -q
+    search.  Rows sorted by (a, b, o)."""
     fc = FrequencyCounts(freq[0], freq[1], p) if freq is not None else None
-    store = sketches(rs, p, fc)
+    t_lo, t_hi = t_range if t_range is not None else (0, rs.nreads)
+    q_lo, q_hi = q_range if q_range is not None else (t_lo, t_hi)
+    store = sketches(rs, p, fc, range(t_lo, t_hi))
+    qs = [i for i in range(q_lo, q_hi) if not t_lo <= i < t_hi]
+    queries = {k: v for k, v in store.items() if k[1] == 0 and q_lo <= k[0] < q_hi}
+    queries.update(sketches(rs, dict(p, no_rc=True), fc, qs))
     rows = []
-    for q_id in sorted(k for k in store if k[1] == 0):
-        for t_id, oi in find_matches(q_id, store[q_id], store, p, True):
-            rows.append(match_record(q_id, t_id, oi, store[q_id][2], store[t_id][2],
+    for q_id in sorted(queries):
+        for t_id, cnt, oi in find_matches(q_id, queries[q_id], store, p, to_self):
+            rows.append(match_record(q_id, t_id, cnt, oi, queries[q_id][2], store[t_id][2],
                                      rs.first_iid))
     a = np.array(rows, dtype=MHAP_DTYPE)
     return a[np.lexsort((a["o"], a["b"], a["a"]))] if a.size else a
+
+
+def run_self(rs, p: dict, freq=None) -> np.ndarray:
+    """The jar's -s block against itself."""
+    return run(rs, p, freq=freq)

@@ -79,7 +79,7 @@ def _mhap_worker(rank, world, port, q):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     sys.path.insert(0, os.path.join(root, "oracle"))
-    import mhap_oracle as M
+    import mhap_jar as M
     from canu_amd.dist import all_gather_rows, query_shards, read_slices
     from canu_amd.synth import ReadSet, synth_reads
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -87,11 +87,13 @@ def _mhap_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n, L = 41, 3000
     rs = synth_reads(n, L, n * L // 12, 0.04, seed=9)
-    p = M.default_params(num_hashes=128, ordered_sketch=600, min_olap=300)
+    p = M.default_params(num_hashes=64, ordered_sketch=600, min_olap=300)
     lo, hi = read_slices(n, world)[rank]
     part = ReadSet(bases=rs.bases, offsets=rs.offsets[lo:hi], lengths=rs.lengths[lo:hi])
-    mine = torch.from_numpy(M.sketch(part, p))
-    full = all_gather_rows(mine, n, dist).numpy()
+    # the library's row layout: [read][strand][H] / [read][strand][S] / [read][strand]
+    rows = M.sketch_rows(part, p)
+    full = [all_gather_rows(torch.from_numpy(r.reshape(hi - lo, -1).view(np.int32)), n,
+                            dist).numpy() for r in rows]
     q_lo, q_hi = query_shards(n, world)[rank]
     recs = M.run(rs, p, q_range=(q_lo - 1, q_hi))
     got = [None] * world
@@ -99,8 +101,10 @@ def _mhap_worker(rank, world, port, q):
     if rank == 0:
         whole = M.run(rs, p)
         union = np.concatenate([np.frombuffer(b, dtype=M.MHAP_DTYPE) for b in got])
-        union = union[np.lexsort((union["b"], union["a"]))]
-        q.put((np.array_equal(full, M.sketch(rs, p)), np.array_equal(union, whole), len(whole)))
+        union = union[np.lexsort((union["o"], union["b"], union["a"]))]
+        want = [r.reshape(n, -1).view(np.int32) for r in M.sketch_rows(rs, p)]
+        q.put((all(np.array_equal(a, b) for a, b in zip(full, want)),
+               np.array_equal(union, whole), len(whole)))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -124,7 +124,9 @@ def test_c4_full_plan_covers_the_reads(monkeypatch):
     for j in js:
         assert j["r"] == (1, j["h"][1])
     est = [j["est_s"] for j in js]
-    assert max(est) / min(est) < 1.03
+    # DRIVER6 replays the driver's discrete packing: one more hash batch (or super-batch) in
+    # a block costs ~2-3 s at once, so the blocks balance to within a step, not a percent
+    assert max(est) / min(est) < 1.10
     import bench
     monkeypatch.delenv("CANU_C4_PLAN", raising=False)
     monkeypatch.delenv("CANU_C4_HBLOCK", raising=False)

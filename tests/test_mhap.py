@@ -1,13 +1,18 @@
-"""The MHAP stage (include/canu_mhap.h, canu_amd/csrc/mhap.hip).
+"""The MHAP stage (include/canu_mhap.h, canu_amd/csrc/mhap.hip) against the jar's semantics.
 
-PARITY UNPINNED against the MHAP jar (src/mhap/mhap-2.1.2.tar: a prebuilt third-party
-archive, never run here).  What IS pinned:
-  * the output format, by the reference's own consumer: every line must go through
+The reference ships MHAP 2.1.2 only as a jar (src/mhap/mhap-2.1.2.tar): class files, no
+sources, no fixtures, and no JVM here.  Its bytecode was read as data (tools/classfile.py)
+and restated method by method in oracle/mhap_jar.py.  What pins what:
+  * the two library hashes the jar calls (Guava Murmur3_x64_128 / Murmur3_x86_32), by the
+    published test vectors of MurmurHash3;
+  * the restatement's faster forms (numpy window hashes, the group form of the ordered-
+    sketch merge), against the literal restatement of the bytecode;
+  * the output format, by the reference's own consumer: every line goes through
     mhapConvert (src/mhap/mhapConvert.C, compiled from the reference source into
-    oracle/_ref/) and come out as the ovOverlap records the line describes;
-  * the GPU path, against the CPU restatement oracle/mhap_oracle.py: integers bit-exact,
-    erate within 1e-6 (written with 6 decimals);
-  * sanity of the restated algorithm against the synthetic reads' known genome layout.
+    oracle/_ref/) and comes out as the ovOverlap records the line describes;
+  * the GPU path, against the restatement: integers bit-exact, erate bit-exact (the
+    identity is computed on the host with the same libm calls as the oracle).
+PARITY PINNED TO THE BYTECODE'S MEANING, NOT TO JAR OUTPUTS (none exist in the reference).
 CPU tests run here; @gpu tests on the MI355X box."""
 import os
 import re
@@ -15,17 +20,18 @@ import re
 import numpy as np
 import pytest
 
-import mhap_oracle as M
+import mhap_jar as M
 import oracle
 from canu_amd import mhap
-from canu_amd.synth import synth_reads
+from canu_amd.synth import ReadSet, synth_reads
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "canu_mhap.h")
-FIELDS = ("a", "b", "count", "a_bgn", "a_end", "a_len", "o", "b_bgn", "b_end", "b_len")
+FIELDS = ("a", "b", "erate", "raw", "a_bgn", "a_end", "a_len", "o", "b_bgn", "b_end",
+          "b_len", "count")
 
 
-def _reads(n=90, L=4000, cov=15, err=0.04, seed=3, **kw):
+def _reads(n=60, L=3000, cov=12, err=0.04, seed=3, **kw):
     return synth_reads(n_reads=n, read_len=L, genome_len=int(n * L / cov), error_rate=err,
                        seed=seed, **kw)
 
@@ -40,6 +46,8 @@ def small_oracle(small):
     return M.run(small, M.default_params())
 
 
+# ------------------------------------------------------------------------------- CPU ----
+
 def test_header_declares_the_python_exports():
     src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
     assert sorted(set(re.findall(r"\b(mhap_[a-z_]+)\s*\(", src))) == sorted(mhap.EXPORTS)
@@ -48,10 +56,18 @@ def test_header_declares_the_python_exports():
 def test_library_exports_every_declared_symbol(built):
     lib = mhap.load_library()
     assert [f for f in mhap.EXPORTS if not hasattr(lib, f)] == []
-    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 5
+    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 6
 
 
-def test_params_init_is_canu_normal(built):
+def test_record_layout_matches_the_header(built):
+    """mhap_record: 56 bytes, the fields at the C offsets."""
+    dt = mhap.MHAP_DTYPE
+    assert dt.itemsize == 56
+    assert [dt.fields[f][1] for f in ("a", "b", "erate", "raw", "a_bgn", "o", "b_len", "count")] \
+        == [0, 4, 8, 16, 24, 36, 48, 52]
+
+
+def test_params_init_is_canu_normal_and_jar_defaults(built):
     lib = mhap.load_library()
     p = mhap._Params()
     lib.mhap_params_init(p)
@@ -60,6 +76,14 @@ def test_params_init_is_canu_normal(built):
         (d.k, d.num_hashes, d.num_min_matches, d.ordered_sketch_size, d.ordered_kmer_size,
          d.min_olap_length) == (16, 512, 3, 1536, 12, 500)
     assert abs(p.threshold - 0.78) < 1e-12
+    assert (p.max_shift, p.min_store, p.no_rc) == (d.max_shift, d.min_store_length, 0) == \
+        (0.2, 0, 0)
+    w = mhap._Weighting()
+    lib.mhap_weighting_init(w)
+    # MhapMain's option table: --repeat-weight 0.9, --repeat-idf-scale 3, --filter-threshold 1e-5
+    assert (w.repeat_weight, w.repeat_idf_scale, w.filter_threshold, w.no_tf, w.supress_noise) \
+        == (0.9, 3.0, 1e-5, 0, 0)
+    assert (d.repeat_weight, d.repeat_idf_scale, d.filter_threshold) == (0.9, 3.0, 1e-5)
 
 
 def test_sensitivity_presets():
@@ -85,10 +109,11 @@ def test_parse_canu_command_line():
     assert (p.k, p.num_hashes, p.num_min_matches, p.ordered_sketch_size) == (16, 768, 2, 1536)
     assert abs(p.threshold - 0.73) < 1e-12 and p.min_olap_length == 500
     assert (p.repeat_weight, p.repeat_idf_scale, p.filter_threshold) == (0.9, 10.0, 0.000005)
-    assert not p.no_tf
+    assert not p.no_tf and not p.no_rc and p.max_shift == 0.2
     assert io["-s"] == "./blocks/000001.dat" and io["--num-threads"] == "8"
     assert mhap.parse_mhap_args(["--no-tf"])[0].no_tf
-    assert p.supress_noise == 0
+    q = mhap.parse_mhap_args(["--max-shift", "0.3", "--min-store-length", "900", "--no-rc"])[0]
+    assert (q.max_shift, q.min_store_length, q.no_rc) == (0.3, 900, True)
     assert mhap.parse_mhap_args(["--supress-noise", "2"])[0].supress_noise == 2
     with pytest.raises(mhap.MhapError):
         mhap.parse_mhap_args(["--supress-noise", "3"])
@@ -107,112 +132,112 @@ def test_frequency_file(tmp_path):
     assert km[0] == "ACGTACGTACGTACGT" and len(km) == 4 and fr[2] == 5e-6
 
 
-def _weighted_params(**kw):
-    p = M.default_params(num_hashes=96)
-    p.update(repeat_weight=0.9, repeat_idf_scale=10.0, filter_threshold=5e-6)
-    p.update(kw)
-    return p
+def test_murmur3_published_vectors():
+    """Guava's Murmur3 functions are MurmurHash3_x64_128 / x86_32 (seed 0): the published
+    test vectors of both, and Guava's hashUnencodedChars = the chars as UTF-16LE bytes."""
+    assert M.murmur3_32(b"") == 0
+    assert M.murmur3_32(b"hello") & M.M32 == 0x248BFA47
+    assert M.murmur3_32(b"abc") & M.M32 == 0xB3DD93FA
+    assert M.murmur3_32(b"The quick brown fox jumps over the lazy dog") & M.M32 == 0x2E4FF723
+    assert M.murmur3_128_h1(b"") == 0
+    assert M.murmur3_128_h1(b"hello") & M.M64 == 0xCBD8A7B341BD9B02
+    # Guava's own test vector: "6c1b07bc7bbc4be347939ac4a93c437a" = bytes of (h1, h2)
+    assert M.murmur3_128_h1(b"The quick brown fox jumps over the lazy dog") & M.M64 == \
+        0xE34BBC7BBC071B6C
+    assert M._chars(b"AC") == b"A\x00C\x00"
 
 
-def _freq_for(rs, every=11):
-    """-f entries for a read set: some of read 0's 16-mers at graded fractions, both
-    strands written as canu does."""
-    r0 = rs.read(0).decode()
-    comp = str.maketrans("ACGT", "TGCA")
-    km, fr = [], []
-    for j, i in enumerate(range(0, 2400, every)):
-        m = r0[i:i + 16]
-        f = 5e-6 * (1.5 ** (j % 12))
-        km += [m, m.translate(comp)[::-1]]
-        fr += [f, f]
-    return km, np.array(fr)
+def test_window_hashes_equal_the_scalar_restatement():
+    rng = np.random.default_rng(1)
+    for k in list(range(1, 33)):
+        s = bytes(rng.choice(list(b"ACGTNacgRY"), size=70).astype(np.uint8))
+        assert np.array_equal(M.murmur128_h1_windows(s, k),
+                              np.array(M.seq_hashes_long(s, k), dtype=np.int64)), k
+        assert np.array_equal(M.murmur32_windows(s, k), M.seq_hashes_int(s, k)), k
+    assert M.murmur128_h1_windows(b"ACG", 4).shape == (0,)
 
 
-def test_oracle_weighting_properties():
-    """The restated weighting (canu_mhap.h): with weight 1 everywhere the weighted sketch
-    IS the unweighted one; tf weighting changes only reads with repeated k-mers; the -f
-    table lowers the weight of listed (frequent) k-mers relative to the rest."""
-    rs = _reads(n=6, L=3000, cov=10, seed=17)
-    base = M.sketch(rs, M.default_params(num_hashes=96))
-    # no -f, no tf: every weight is 1
-    w1 = M.sketch_weighted(rs, _weighted_params(no_tf=True), None)
-    assert np.array_equal(w1, base)
-    # r >= 1: m = 1 for every k-mer (tf only); a read with no repeated k-mer is unchanged
-    tfo = M.sketch_weighted(rs, _weighted_params(repeat_weight=1.0), _freq_for(rs))
-    assert np.array_equal(tfo, M.sketch_weighted(rs, _weighted_params(repeat_weight=1.0)))
-    # the multipliers: frequent k-mers get the smallest, unlisted ones the largest
-    km, fr = _freq_for(rs)
-    codes, mult, dm = M.kmer_multipliers(km, fr, _weighted_params())
-    assert codes.size == np.unique(codes).size and mult.min() >= 1.0 - 1e-12
-    assert abs(dm - (0.9 + 0.1 * 10.0)) < 1e-12 and mult.max() <= dm
-    assert abs(mult.min() - 1.0) < 1e-12                 # the most frequent: scaled idf 1
-    # a read whose k-mers are all listed at one fraction gets a sketch unlike the tf one
-    full = M.sketch_weighted(rs, _weighted_params(), (km, fr))
-    assert not np.array_equal(full, tfo)
+def test_reverse_complement_is_utils_rc():
+    """Utils.rc: reverse, upper case, IUPAC complement (Utils$Translate); other bytes -> 0."""
+    assert M.rc(b"ACGTN") == b"NACGT"
+    assert M.rc(b"acgt") == b"ACGT"
+    assert M.rc(b"RYKMBDHVSW") == b"WSBDHVKMRY"
+    assert M.rc(b"X") == b"\x00"
 
 
-def _noise_freq(rs, every=3):
-    """An mhapFilterUnique-style -f list (Meryl.pm:678-714: every k-mer at or above the
-    unique-count threshold, with its fraction): some of the reads' k-mers, most of them
-    below --filter-threshold, a few repeats above it."""
-    km, fr = _freq_for(rs, every=every)
-    fr = fr.copy()
-    fr[np.arange(fr.size) % 6 >= 2] = 2e-7        # solid but not repeated: below 5e-6
-    return km, fr
+def test_java_arithmetic():
+    assert [M.java_round(x) for x in (0.5, 1.5, 2.4999999, -0.5, -1.5, -2.6)] == \
+        [1, 2, 2, 0, -1, -3]
+    assert M.i32(2 ** 31) == -2 ** 31 and M.i32(-1) == -1 and M.i32(3 * 2 ** 32 + 5) == 5
+    # String.format("%.6f"): the shortest decimal, half up (C's printf rounds the binary value)
+    assert mhap.java_fixed6(5e-7) == "0.000001" and "%.6f" % 5e-7 == "0.000000"
+    assert mhap.java_fixed6(116.0) == "116.000000"
+    assert mhap.java_fixed6(0.0) == "0.000000"
+    assert mhap.java_fixed6(0.06954645004) == "0.069546"
+    assert mhap.java_fixed6(1.0000005) == "1.000001"
 
 
-def test_oracle_supress_noise():
-    """--supress-noise (canu_mhap.h, restated from the jar's option text; unpinned): every
-    -f k-mer is in the table (those below the threshold at the top multiplier); an unlisted
-    k-mer is weighted like the most frequent one (2) or never enters a sketch (1)."""
-    rs = _reads(n=6, L=3000, cov=10, seed=17)
-    km, fr = _noise_freq(rs)
-    p0 = _weighted_params()
-    c0, m0, d0 = M.kmer_multipliers(km, fr, p0)
-    for mode in (1, 2):
-        c, m, d = M.kmer_multipliers(km, fr, dict(p0, supress_noise=mode))
-        assert c.size > c0.size                   # the below-threshold k-mers are listed
-        assert abs(m.max() - d0) < 1e-12          # ... at the top multiplier
-        assert (abs(d - m.min()) < 1e-12) if mode == 2 else d == -1.0
-    s0 = M.sketch_weighted(rs, p0, (km, fr))
-    s1 = M.sketch_weighted(rs, dict(p0, supress_noise=1), (km, fr))
-    s2 = M.sketch_weighted(rs, dict(p0, supress_noise=2), (km, fr))
-    assert not np.array_equal(s0, s2) and not np.array_equal(s1, s2)
-    # mode 1 keeps only listed k-mers: every read's sketch values are >= mode 0's
-    assert (s1 >= s0).all() and (s1 != s0).any()
-    # nothing listed: with mode 1 no k-mer is left (empty sketches)
-    none = ([km[0]], np.array([fr[0]]))
-    c, m, d = M.kmer_multipliers(none[0], none[1], dict(p0, supress_noise=1))
-    assert c.size == 1 and d == -1.0
+def _random_sketch(rng, n, sl, nh):
+    """An ordered sketch with many repeated hashes: (hashes sorted, positions by hash then
+    position, seqLength)."""
+    h = rng.integers(-nh, nh, n).astype(np.int32)
+    pos = rng.choice(sl, n, replace=False).astype(np.int32)
+    o = np.lexsort((pos, h))
+    return h[o], pos[o], sl
 
 
-def test_oracle_kmer_codes():
-    """Canonical 2-bit codes, first base most significant; non-ACGT breaks k-mers."""
-    c = M._CODE[np.frombuffer(b"ACGTNACGTA", dtype=np.uint8)]
-    pos, can, s = M.kmers(c, 4)
-    # ACGT is its own reverse complement; CGTA/ACGT after the N
-    assert pos.tolist() == [0, 5, 6]
-    assert int(can[0]) == 0b00011011 == int(can[1])      # ACGT = its own reverse complement
-    assert int(can[2]) == 0b01101100                      # CGTA < rc TACG (0b11000110)
-    assert s.tolist() == [0, 0, 0]
-    pos, can, s = M.kmers(M._CODE[np.frombuffer(b"TTTT", dtype=np.uint8)], 4)
-    assert int(can[0]) == 0 and s.tolist() == [1]        # AAAA on the other strand
+def test_group_form_of_the_merge_equals_the_literal_merge():
+    """overlap_info with the jar's merge itself (recordMatchingKmers, literal) and with its
+    group form (what the GPU evaluates): the same records, edges and score, over random
+    sketches with heavy hash duplication and every shift regime."""
+    rng = np.random.default_rng(5)
+    diffs = 0
+    for trial in range(400):
+        nh = int(rng.choice([3, 8, 40, 400]))
+        A = _random_sketch(rng, int(rng.integers(1, 120)), int(rng.integers(130, 900)), nh)
+        B = _random_sketch(rng, int(rng.integers(1, 120)), int(rng.integers(130, 900)), nh)
+        ms = float(rng.choice([0.05, 0.2, 0.5, -0.5]))
+        lit = M.overlap_info(A, B, ms, 12, literal=True)
+        grp = M.overlap_info(A, B, ms, 12)
+        assert lit == grp, trial
+        diffs += lit is not None
+    assert diffs > 100
+
+
+def test_frequency_counts_keys_and_scaled_idf():
+    """FrequencyCounts: a k-mer and its reverse complement share one key (the smaller
+    string's hash); scaled idf runs from 1 (the most frequent k-mer) to the scale (a k-mer
+    at the cutoff; also every k-mer not in the table); lines below the cutoff are dropped."""
+    p = M.default_params(repeat_idf_scale=10.0, filter_threshold=1e-5)
+    km = ["AAAAAAAAAAAAAAAC", "GTTTTTTTTTTTTTTT", "ACGTACGTACGTACGA", "CCCCCCCCCCCCCCCC"]
+    fr = [1e-3, 1e-3, 1e-5, 1e-6]
+    fc = M.FrequencyCounts(km, fr, p)
+    k0 = M.seq_hashes_long(km[0].encode(), 16, True)[0]
+    assert k0 == M.seq_hashes_long(km[1].encode(), 16, True)[0]      # reverse complements
+    assert k0 == M.seq_hashes_long(b"AAAAAAAAAAAAAAAC", 16, False)[0]   # the smaller string
+    assert len(fc.counts) == 2
+    assert abs(fc.scaled_idf(k0) - 1.0) < 1e-12
+    k2 = M.seq_hashes_long(km[2].encode(), 16, True)[0]
+    assert abs(fc.scaled_idf(k2) - 10.0) < 1e-9
+    assert fc.scaled_idf(12345) == 10.0
 
 
 def test_oracle_finds_the_true_overlaps(small, small_oracle):
     """Sanity of the restated algorithm: overlaps it reports are real (genome intervals
-    intersect, orientation = strand difference, offset close to the truth) and it finds
-    most true overlaps of >= 1.5 kb."""
+    intersect, orientation = strand difference), a is the larger ID (the self search), and
+    it finds most true overlaps of >= 1.5 kb."""
     rs, rec = small, small_oracle
     assert len(rec) > 100
     st, sd, L = rs.starts, rs.strands.astype(int), rs.lengths.astype(int)
     for r in rec:
         a, b = int(r["a"]) - 1, int(r["b"]) - 1
+        assert b < a
         ov = min(st[a] + L[a], st[b] + L[b]) - max(st[a], st[b])
         assert ov > 0, (a, b)
         assert int(r["o"]) == (sd[a] ^ sd[b])
+        assert r["count"] >= 3 and 0.0 <= r["erate"] <= 0.22
     found = {(int(r["a"]) - 1, int(r["b"]) - 1) for r in rec}
-    true = [(a, b) for a in range(rs.nreads) for b in range(a + 1, rs.nreads)
+    true = [(a, b) for a in range(rs.nreads) for b in range(a)
             if min(st[a] + L[a], st[b] + L[b]) - max(st[a], st[b]) >= 1500]
     hit = sum((a, b) in found for a, b in true)
     assert hit >= 0.9 * len(true), (hit, len(true))
@@ -246,33 +271,55 @@ def test_reference_mhapconvert_reads_our_lines(small, small_oracle, tmp_path):
 
 # ------------------------------------------------------------------------------- GPU ----
 
-def _gpu(rs, P, filt=None):
-    m = mhap.Mhap(P, device=0)
-    rec = m.run(rs, filter_kmers=filt)
-    st = m.stats()
-    m.close()
-    return rec, st
-
-
 def _same(got, want):
     assert got.shape == want.shape, (got.shape, want.shape)
     for f in FIELDS:
-        assert np.array_equal(got[f].astype(np.int64), want[f].astype(np.int64)), f
-    assert np.max(np.abs(got["erate"] - want["erate"]), initial=0.0) <= 1e-6
+        assert np.array_equal(got[f], want[f]), f
+
+
+def _rows(m, n, P):
+    """The context's sketch rows (mhap_sketch_buffers) copied to the host."""
+    import ctypes
+    pmh, pord, pcnt = m.sketch_buffers()
+    H, S = P.num_hashes, P.ordered_sketch_size
+    mh = np.zeros((n, 2, H), dtype=np.int32)
+    od = np.zeros((n, 2, S), dtype=np.uint64)
+    oc = np.zeros((n, 2), dtype=np.uint32)
+    hip = ctypes.CDLL("libamdhip64.so")        # hipMemcpy D2H (synchronous) of the rows
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for arr, ptr in ((mh, pmh), (od, pord), (oc, pcnt)):
+        assert hip.hipMemcpy(arr.ctypes.data, ptr, arr.nbytes, 2) == 0
+    return mh, od, oc
+
+
+def _same_rows(got, want):
+    mh, od, oc = got
+    wmh, wod, woc = want
+    assert np.array_equal(oc, woc)
+    used = oc > 0
+    assert np.array_equal(mh[used], wmh[used])
+    for i, s in zip(*np.nonzero(used)):
+        assert np.array_equal(od[i, s, :oc[i, s]], wod[i, s, :woc[i, s]]), (i, s)
 
 
 CASES = {
     "normal": (dict(), mhap.MhapParameters()),
-    "high_ragged_ns": (dict(n=80, L=3000, err=0.05, seed=5, len_jitter=0.5, n_rate=0.002),
-                       mhap.MhapParameters.sensitivity("high", min_olap=300)),
-    "low_k14": (dict(n=70, L=5000, err=0.03, seed=6),
+    "high_ragged_ns": (dict(n=70, L=3000, err=0.05, seed=5, len_jitter=0.5, n_rate=0.002),
+                       mhap.MhapParameters.sensitivity("high", min_olap=1500)),
+    "low_k14": (dict(n=50, L=5000, err=0.03, seed=6),
                 mhap.MhapParameters.sensitivity("low", min_olap=500)),
     # BASELINE configs[3]'s read length: 15 kb reads at 25x, 5 % error, the 'normal' preset
-    "configs3_15kb": (dict(n=300, L=15000, cov=25, err=0.05, seed=9), mhap.MhapParameters()),
-    "utg_small_k": (dict(n=60, L=2500, err=0.02, seed=7),
+    "configs3_15kb": (dict(n=60, L=15000, cov=25, err=0.05, seed=9), mhap.MhapParameters()),
+    "utg_small_k": (dict(n=50, L=2500, err=0.02, seed=7),
                     mhap.MhapParameters(k=12, num_hashes=128, num_min_matches=5,
                                         ordered_kmer_size=18, ordered_sketch_size=700,
                                         min_olap_length=200, threshold=0.8)),
+    "max_shift_min_store": (dict(n=60, L=3000, err=0.04, seed=8, len_jitter=0.4),
+                            mhap.MhapParameters(num_hashes=256, max_shift=0.05,
+                                                min_store_length=2800, min_olap_length=300)),
+    "no_rc_odd_k": (dict(n=50, L=3000, err=0.03, seed=10),
+                    mhap.MhapParameters(k=13, num_hashes=200, ordered_kmer_size=11,
+                                        ordered_sketch_size=900, no_rc=True)),
 }
 
 
@@ -281,122 +328,78 @@ CASES = {
 def test_gpu_matches_oracle(built, name):
     kw, P = CASES[name]
     rs = _reads(**kw)
-    got, st = _gpu(rs, P)
+    m = mhap.Mhap(P, device=0)
+    got = m.run(rs)
+    st = m.stats()
+    rows = _rows(m, rs.nreads, P)
+    m.close()
     want = M.run(rs, P.as_oracle())
     assert len(want) > 20
     _same(got, want)
-    assert st["overlaps"] == len(want)
+    assert st["overlaps"] == len(want) and st["candidates"] >= len(want)
+    _same_rows(rows, M.sketch_rows(rs, P.as_oracle()))
+
+
+def _freq_for(rs, every=11, span=2400):
+    """-f entries for a read set: some of read 0's 16-mers at graded fractions, both
+    strands written as canu does (Meryl.pm:699-716)."""
+    r0 = rs.read(0).decode()
+    comp = str.maketrans("ACGT", "TGCA")
+    km, fr = [], []
+    for j, i in enumerate(range(0, span, every)):
+        m = r0[i:i + 16]
+        f = 5e-6 * (1.5 ** (j % 12))
+        km += [m, m.translate(comp)[::-1]]
+        fr += [f, f]
+    return km, np.array(fr)
 
 
 @pytest.mark.gpu
-def test_gpu_filter_kmers(built, small):
-    """-f: frequent k-mers never enter a sketch."""
-    P = mhap.MhapParameters()
-    r0 = small.read(0).decode()
-    filt = [r0[i:i + 16] for i in range(0, 3000, 7)]
-    got, _ = _gpu(small, P, filt)
-    want = M.run(small, P.as_oracle(), skip_kmers=filt)
-    _same(got, want)
-
-
-@pytest.mark.gpu
-def test_gpu_shards_and_text(built, small, small_oracle, tmp_path):
-    """Query-range shards (the multi-GPU split) union to the whole job, and the text the
-    library writes is byte-identical to the oracle records' lines (and, where built, goes
-    through the reference mhapConvert)."""
-    P = mhap.MhapParameters()
-    m = mhap.Mhap(P, device=0)
-    m.load_reads(small)
-    m.sketch()
-    m.build_index()
-    parts = []
-    for lo, hi in ((1, 30), (31, 60), (61, small.nreads)):
-        m.compare(lo, hi)
-        parts.append(m.fetch())
-    m.compare()
-    path = str(tmp_path / "all.mhap")
-    m.write_text(path, 1, small.nreads, 1)
-    m.close()
-    whole = np.concatenate(parts)
-    _same(whole, small_oracle)
-    want = "".join(mhap.format_line(r, 1, small.nreads, 1) + "\n" for r in small_oracle)
-    assert open(path).read() == want
-    oracle.require_reference(mhap_convert=True)
-    assert len(oracle.mhap_convert(small, path)) == len(small_oracle)
-
-
-@pytest.mark.gpu
-def test_gpu_sketch_rows_match_oracle(built, small):
-    """Stage outputs directly: the MinHash rows and ordered-sketch rows in HBM."""
-    import ctypes
-    P = mhap.MhapParameters()
-    m = mhap.Mhap(P, device=0)
-    m.load_reads(small)
-    m.sketch()
-    pmh, pord, pcnt = m.sketch_buffers()
-    n, H, S = small.nreads, P.num_hashes, P.ordered_sketch_size
-    mh = np.zeros((n, H), dtype=np.int32)
-    od = np.zeros((n, S), dtype=np.uint64)
-    oc = np.zeros(n, dtype=np.uint32)
-    hip = ctypes.CDLL("libamdhip64.so")        # hipMemcpy D2H (synchronous) of the rows
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    assert hip.hipMemcpy(mh.ctypes.data, pmh, mh.nbytes, 2) == 0
-    assert hip.hipMemcpy(od.ctypes.data, pord, od.nbytes, 2) == 0
-    assert hip.hipMemcpy(oc.ctypes.data, pcnt, oc.nbytes, 2) == 0
-    m.close()
-    assert np.array_equal(mh, M.sketch(small, P.as_oracle()))
-    for i in range(0, n, 7):
-        h, pos, s = M.ordered_sketch(small, i, P.as_oracle())
-        assert oc[i] == h.shape[0]
-        key = (h.astype(np.uint64) << np.uint64(32)) | (pos.astype(np.uint64) << np.uint64(1)) \
-            | s.astype(np.uint64)
-        assert np.array_equal(od[i, :oc[i]], key), i
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "repeat_read", "k20", "noise1",
-                                     "noise2"])
+@pytest.mark.parametrize("variant", ["canu", "no_tf", "tf_only", "count", "unweighted",
+                                     "repeat_read", "k20"])
 def test_gpu_weighted_sketch_rows_match_oracle(built, variant):
-    """The weighted MinHash rows in HBM (distinct k-mers by a radix sort, tf as run lengths,
-    the -f multipliers) equal the restatement's, bit for bit."""
-    import ctypes
-    kw = dict(n=40, L=3000, cov=12, seed=19)
+    """The weighted MinHash rows in HBM (distinct k-mers by a segmented radix sort, tf as run
+    lengths, the -f table's scaled idf) equal the restatement's, bit for bit; every mode of
+    computeNgramMinHashesWeighted's weight: tf-idf (canu), no tf, repeat weight >= 1 (the
+    count), no table (the count), repeat weight < 0 (1, table k-mers dropped)."""
+    kw = dict(n=24, L=3000, cov=8, seed=19)
     if variant == "repeat_read":
         kw.update(n_repeats=6, repeat_len=400)        # tf > 1 inside reads
     rs = _reads(**kw)
-    P = mhap.MhapParameters(num_hashes=128, ordered_sketch_size=600, ordered_kmer_size=14,
+    P = mhap.MhapParameters(num_hashes=48, ordered_sketch_size=600, ordered_kmer_size=14,
                             min_olap_length=300).canu_weighting()
     freq = _freq_for(rs)
     if variant == "no_tf":
         P.no_tf = True
     if variant == "tf_only":
         P.repeat_weight = 1.0
-    if variant == "k20":                 # 64-bit (read, code) keys: one sort per batch
+    if variant == "count":
+        freq = None
+    if variant == "unweighted":
+        P.repeat_weight = -1.0
+    if variant == "k20":
         P.k = 20
         freq = ([x + "ACGT" for x in freq[0]], freq[1])
-    if variant in ("noise1", "noise2"):  # --supress-noise with an mhapFilterUnique -f list
-        P.supress_noise = int(variant[-1])
-        freq = _noise_freq(rs)
     m = mhap.Mhap(P, device=0)
     m.load_reads(rs)
-    m.set_kmer_frequencies(*freq)
+    if freq is None:
+        m.set_weighting()
+    else:
+        m.set_kmer_frequencies(*freq)
     m.sketch()
-    pmh, _, _ = m.sketch_buffers()
-    mh = np.zeros((rs.nreads, P.num_hashes), dtype=np.int32)
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    assert hip.hipMemcpy(mh.ctypes.data, pmh, mh.nbytes, 2) == 0
+    st = m.stats()
+    got = _rows(m, rs.nreads, P)
     m.close()
-    want = M.sketch_weighted(rs, P.as_oracle(), freq)
-    assert np.array_equal(mh, want)
+    _same_rows(got, M.sketch_rows(rs, P.as_oracle(), freq))
+    assert st["sketch_draws"] >= st["sketch_kmers"] * P.num_hashes > 0
 
 
 @pytest.mark.gpu
 def test_gpu_weighted_job_matches_oracle(built):
-    """canu's weighting end to end: records of the weighted all-vs-all equal the
-    restatement's (integers bit-exact, erate within 1e-6)."""
-    rs = _reads(n=70, L=4000, cov=14, seed=23)
-    P = mhap.MhapParameters(num_hashes=256, ordered_sketch_size=1000,
+    """canu's weighting end to end (-f table, --repeat-weight 0.9 --repeat-idf-scale 10):
+    records of the self job equal the restatement's."""
+    rs = _reads(n=40, L=3000, cov=10, seed=23)
+    P = mhap.MhapParameters(num_hashes=96, ordered_sketch_size=1000,
                             min_olap_length=400).canu_weighting()
     freq = _freq_for(rs, every=5)
     m = mhap.Mhap(P, device=0)
@@ -405,3 +408,97 @@ def test_gpu_weighted_job_matches_oracle(built):
     want = M.run(rs, P.as_oracle(), freq=freq)
     assert len(want) > 20
     _same(got, want)
+
+
+def _odd_reads():
+    """Edge cases of one read set: a read shorter than k (not used), one shorter than
+    --min-olap-length (not used), a homopolymer (one hash repeated: the ordered sketch's
+    radix select must descend past its first digit), lower case / IUPAC / N bases (the
+    complement table), and ordinary reads overlapping them."""
+    base = _reads(n=20, L=2500, cov=6, err=0.03, seed=31)
+    seqs = [base.read(i) for i in range(base.nreads)]
+    g = bytearray(seqs[3])
+    g[100:140] = b"acgtacgtacgtRYKMnnnnNNNNswSWbdhv" + b"A" * 8
+    seqs[3] = bytes(g)
+    seqs += [b"ACGTACGTAC", seqs[5][:400], b"A" * 2600, seqs[7][:1200] + b"T" * 1400]
+    lens = np.array([len(s) for s in seqs], dtype=np.uint32)
+    offs = np.zeros(len(seqs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return ReadSet(bases=np.frombuffer(b"".join(seqs), dtype=np.uint8).copy(), offsets=offs,
+                   lengths=lens, first_iid=1)
+
+
+@pytest.mark.gpu
+def test_gpu_edge_reads_match_oracle(built):
+    rs = _odd_reads()
+    P = mhap.MhapParameters(num_hashes=128, ordered_sketch_size=800, min_olap_length=500,
+                            threshold=0.6)
+    m = mhap.Mhap(P, device=0)
+    got = m.run(rs)
+    st = m.stats()
+    rows = _rows(m, rs.nreads, P)
+    m.close()
+    want_rows = M.sketch_rows(rs, P.as_oracle())
+    _same_rows(rows, want_rows)
+    assert rows[2][20].tolist() == [0, 0] and rows[2][21].tolist() == [0, 0]   # not used
+    assert rows[2][22, 0] == 800                                             # homopolymer
+    assert st["sketched_reads"] == rs.nreads - 2
+    _same(got, M.run(rs, P.as_oracle()))
+
+
+@pytest.mark.gpu
+def test_gpu_shards_query_search_and_text(built, small, small_oracle, tmp_path):
+    """Query-range shards of the self search (the multi-GPU split) union to the whole job;
+    the -q search (compare_all: every stored read, toSelf false) equals the restatement's;
+    the text the library writes is byte-identical to the oracle records' lines (and, where
+    built, goes through the reference mhapConvert)."""
+    P = mhap.MhapParameters()
+    m = mhap.Mhap(P, device=0)
+    m.load_reads(small)
+    m.set_weighting()
+    m.sketch()
+    m.build_index()
+    parts = []
+    for lo, hi in ((1, 20), (21, 45), (46, small.nreads)):
+        m.compare(lo, hi)
+        parts.append(m.fetch())
+    m.compare()
+    path = str(tmp_path / "all.mhap")
+    m.write_text(path, 1, small.nreads, 1)
+    # the -q search: reads 41.. against the stored reads 1..40
+    m.build_index(1, 40)
+    m.compare(41, small.nreads, all_targets=True)
+    cross = m.fetch()
+    m.close()
+    _same(np.concatenate(parts), small_oracle)
+    want = "".join(mhap.format_line(r, 1, small.nreads, 1) + "\n" for r in small_oracle)
+    assert open(path).read() == want
+    P0 = P.as_oracle()
+    _same(cross, M.run(small, P0, q_range=(40, small.nreads), t_range=(0, 40), to_self=False))
+    oracle.require_reference(mhap_convert=True)
+    assert len(oracle.mhap_convert(small, path)) == len(small_oracle)
+
+
+@pytest.mark.gpu
+def test_gpu_supress_noise_is_refused(built):
+    P = mhap.MhapParameters(supress_noise=2)
+    m = mhap.Mhap(P, device=0)
+    with pytest.raises(mhap.MhapError, match="supress-noise"):
+        m.set_weighting()
+    m.close()
+
+
+def test_library_formats_lines_like_java(built):
+    """mhap_format_line (the C library's MatchResult.toString) equals format_line for
+    values on both sides of every rounding edge."""
+    import ctypes
+    lib = mhap.load_library()
+    rng = np.random.default_rng(2)
+    vals = [5e-7, 1.0000005, 0.0, 1.0, 0.123456499999, 0.1234565, 2.5e-7, 0.9999995]
+    vals += list(rng.random(300)) + [round(float(x), 7) for x in rng.random(300)]
+    r = np.zeros(1, dtype=mhap.MHAP_DTYPE)
+    buf = ctypes.create_string_buffer(256)
+    for i, v in enumerate(vals):
+        r[0] = (7, 3, v, float(i % 50), 1, 2, 3, i % 2, 4, 5, 6, 9)
+        assert lib.mhap_format_line(r.ctypes.data, 1, 0, 1, buf, 256) == 0
+        assert buf.value.decode() == mhap.format_line(r[0]), v

@@ -4,7 +4,7 @@
 canu runs MHAP as a prebuilt jar (src/mhap/mhap-2.1.2.tar, OverlapMhap.pm:374-498); no Java
 sources or fixtures ship with it and no JVM exists here, so the jar is never run.  This tool
 parses class files as DATA -- constant pool, methods, bytecode -- and prints a method's
-instructions with their constants resolved, so that oracle/mhap_oracle.py's restatement
+instructions with their constants resolved, so that oracle/mhap_jar.py's restatement
 (hash family, seeding, weighting) can be checked against what the bytecode does.
 
     python tools/classfile.py edu/umd/marbl/mhap/sketch/HashUtils [method-substring]

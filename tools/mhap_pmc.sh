@@ -1,5 +1,5 @@
 # MHAP configs[3] counter evidence (bench_mhap.py, one step, serial read generation): PMC
-# passes summed over the sketch kernels (k_mh_sketch_w: the weighted sketch canu runs;
+# passes summed over the sketch kernels (k_mh_minhash: the weighted MinHash draws;
 # k_mh_ordered: the ordered sketch), each pass a run of its own under its own time limit:
 #   issue:  VALU / SALU instructions, active / wait cycles, wave cycles
 #   bytes:  FETCH_SIZE, then WRITE_SIZE (HBM traffic, the guide's passes)
@@ -17,7 +17,7 @@ pass() {   # name counters...
   local name=$1; shift
   timeout -k 10 -s KILL 300 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/${TAG}_$name \
     -o run -- $JOB > $R/gpurun_out/${TAG}_$name.log 2>&1 || { tail -5 $R/gpurun_out/${TAG}_$name.log; return 1; }
-  for k in k_mh_sketch_w k_mh_ordered k_mh_compare; do
+  for k in k_mh_minhash k_mh_keys k_mh_ordered k_mh_compare; do
     python3 $R/tools/pmc_sum.py $R/gpurun_out/${TAG}_$name $k | sed "s/^/$k /" | tee -a $R/gpurun_out/${TAG}_pmc.txt
   done
 }
