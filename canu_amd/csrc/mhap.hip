@@ -393,28 +393,54 @@ __device__ __forceinline__ uint64_t xs64(uint64_t x) {
   return x;
 }
 
+// exact minimum (signed) of w xorshift64 draws from chain state x (w = 0: x is the value)
+__device__ __forceinline__ int64_t exact_min(uint64_t x, int32_t w) {
+  if (w == 0) return (int64_t)x;
+  int64_t m = LMAX;
+  for (int32_t t = 0; t < w; t++) {
+    x = xs64(x);
+    m = (int64_t)x < m ? (int64_t)x : m;
+  }
+  return m;
+}
+
+// A best draw of one hash function: its high word decides almost every comparison; the
+// exact value is recomputed from (state, w) -- the k-mer's chain before the function's w
+// draws -- only when two candidates tie on the high word (w = 0: state is the value).
+struct BestRec {
+  int32_t hi;
+  uint32_t fp;                    // first position of the k-mer (0xFFFFFFFF: none yet)
+  uint32_t v;                     // the value stored: the key's low / high 32 bits
+  int32_t w;
+  uint64_t state;
+};
+
+constexpr uint32_t FP_NONE = 0xFFFFFFFFu;
+
+// the jar's order of candidates: the smaller draw, then the earlier first occurrence
+__device__ __forceinline__ bool rec_less(const BestRec &a, const BestRec &b) {
+  if (b.fp == FP_NONE) return a.fp != FP_NONE;
+  if (a.fp == FP_NONE) return false;
+  if (a.hi != b.hi) return a.hi < b.hi;
+  const int64_t xa = exact_min(a.state, a.w), xb = exact_min(b.state, b.w);
+  return xa < xb || (xa == xb && a.fp < b.fp);
+}
+
 // MinHashSketch.computeNgramMinHashesWeighted @0-476 (oracle mhap_jar.minhash); one block
-// per strand.  LDS: per wave and hash function the best (draw, first position, value).
+// per strand, RKW distinct k-mers per thread per round.  LDS: per wave and hash function the
+// best candidate so far (BestRec).
 __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
   extern __shared__ uint8_t s_raw[];
   const int32_t H = A.H;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  int64_t *bx_all = (int64_t *)s_raw;                       // [4][H]
-  uint32_t *bp_all = (uint32_t *)(bx_all + 4 * H);          // [4][H]
-  uint32_t *bv_all = bp_all + 4 * H;                        // [4][H]
+  BestRec *best_all = (BestRec *)s_raw;                      // [4][H]
   __shared__ uint32_t s_live;
-  for (int32_t j = tid; j < 4 * H; j += 256) {
-    bx_all[j] = LMAX;
-    bp_all[j] = 0xFFFFFFFFu;
-    bv_all[j] = 0;
-  }
+  for (int32_t j = tid; j < 4 * H; j += 256) best_all[j] = BestRec{0x7FFFFFFF, FP_NONE, 0, 0, 0};
   if (tid == 0) s_live = 0;
   __syncthreads();
   const uint32_t bi = blockIdx.x, sid = A.sids[bi];
   const uint64_t s0 = A.koff[bi], s1 = A.koff[bi + 1];
-  int64_t *bx = bx_all + wave * H;
-  uint32_t *bp = bp_all + wave * H;
-  uint32_t *bv = bv_all + wave * H;
+  BestRec *best = best_all + wave * H;
   unsigned long long nkm = 0, ndraw = 0;
   for (uint64_t base = s0; base < s1; base += 256 * RKW) {
     const uint64_t p0 = base + (uint64_t)tid * RKW;
@@ -423,7 +449,7 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
     int32_t W[RKW];
 #pragma unroll
     for (int i = 0; i < RKW; i++) {
-      X[i] = 0; KL[i] = KH[i] = 0; FP[i] = 0xFFFFFFFFu; W[i] = 0;
+      X[i] = 0; KL[i] = KH[i] = 0; FP[i] = FP_NONE; W[i] = 0;
       const uint64_t p = p0 + i;
       if (p < s1) {
         const uint64_t key = A.keys[p];
@@ -453,44 +479,151 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
         }
       }
     }
-    int32_t wl = 0;
+    // dead slots (W = 0) take a live slot's chain, weight and payload: a duplicate candidate
+    // changes no minimum and no tie; a lane with no live slot is masked at the wave minimum
+    bool live = false;
+    {
+      uint64_t x0 = 0;
+      uint32_t l0 = 0, h0 = 0, f0 = FP_NONE;
+      int32_t w0 = 0;
 #pragma unroll
-    for (int i = 0; i < RKW; i++) wl = W[i] > wl ? W[i] : wl;
-    if (__builtin_amdgcn_ballot_w64(wl > 0) == 0) continue;   // nothing in this wave
+      for (int i = RKW - 1; i >= 0; i--)
+        if (W[i] > 0) { x0 = X[i]; l0 = KL[i]; h0 = KH[i]; f0 = FP[i]; w0 = W[i]; live = true; }
+#pragma unroll
+      for (int i = 0; i < RKW; i++)
+        if (W[i] == 0) { X[i] = x0; KL[i] = l0; KH[i] = h0; FP[i] = f0; W[i] = w0; }
+    }
+    if (__builtin_amdgcn_ballot_w64(live) == 0) continue;   // nothing in this wave
+    // one weight for every live slot of the wave (canu's weighting: a k-mer seen once and not
+    // in the -f table weighs round(1 x 10) = 10, nearly all of them): the draws are a
+    // wave-uniform loop instead of a per-lane one under an exec mask per slot and draw
+    int32_t wmn = 0x7FFFFFFF, wmx = 0;
+#pragma unroll
+    for (int i = 0; i < RKW; i++) { wmn = min(wmn, W[i]); wmx = max(wmx, W[i]); }
+    if (!live) { wmn = 0x7FFFFFFF; wmx = 0; }
+    wmn = wave_min_i32(wmn);
+    wmx = wave_max_i32(wmx);
+    const int32_t wu = wmn == wmx ? __builtin_amdgcn_readfirstlane(wmx) : 0;
     for (int32_t j = 0; j < H; j++) {
-      int64_t mx = LMAX;
-      uint32_t mp = 0xFFFFFFFFu, mv = 0;
+      const BestRec cur = best[j];                     // uniform (LDS broadcast)
+      if (wu >= 2) {
+        // high-word minima: one v_min per draw instead of a 64-bit compare and two selects
+        uint64_t X0[RKW];
+        int32_t mh[RKW];
 #pragma unroll
-      for (int i = 0; i < RKW; i++) {
-        int64_t mi = LMAX;
-        for (int32_t t = 0; t < W[i]; t++) {
-          X[i] = xs64(X[i]);
-          mi = (int64_t)X[i] < mi ? (int64_t)X[i] : mi;
+        for (int i = 0; i < RKW; i++) { X0[i] = X[i]; mh[i] = 0x7FFFFFFF; }
+        for (int32_t t = 0; t < wu; t++) {
+#pragma unroll
+          for (int i = 0; i < RKW; i++) {
+            X[i] = xs64(X[i]);
+            const int32_t h = (int32_t)(X[i] >> 32);
+            mh[i] = h < mh[i] ? h : mh[i];
+          }
+        }
+        int32_t lh = mh[0];
+#pragma unroll
+        for (int i = 1; i < RKW; i++) lh = mh[i] < lh ? mh[i] : lh;
+        if (!live) lh = 0x7FFFFFFF;
+        const int32_t wh = wave_min_i32(lh);
+        if (cur.fp != FP_NONE && wh > cur.hi) continue;       // cannot beat the best so far
+        // slots holding the wave's smallest high word
+        uint32_t nmine = 0, li = 0;
+#pragma unroll
+        for (int i = RKW - 1; i >= 0; i--)
+          if (live && mh[i] == wh) { nmine++; li = i; }
+        const uint64_t who = __builtin_amdgcn_ballot_w64(nmine > 0);
+        const uint32_t ln = (uint32_t)__builtin_ctzll(who);
+        const bool unique = popc64(who) == 1 && __builtin_amdgcn_readlane(nmine, ln) == 1 &&
+                            wh != 0x7FFFFFFF && (cur.fp == FP_NONE || wh < cur.hi);
+        BestRec nb;
+        if (unique) {
+          // the candidate's own (state, w) stand for its exact value, fetched from lane ln
+          uint64_t st = 0;
+          uint32_t fp = 0, v = 0;
+#pragma unroll
+          for (int i = 0; i < RKW; i++)
+            if ((uint32_t)i == li) { st = X0[i]; fp = FP[i]; v = (j & 1) ? KH[i] : KL[i]; }
+          nb.hi = wh;
+          nb.fp = __builtin_amdgcn_readlane(fp, ln);
+          nb.v = __builtin_amdgcn_readlane(v, ln);
+          nb.w = wu;
+          nb.state = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), ln) << 32) |
+                     __builtin_amdgcn_readlane((uint32_t)st, ln);
+        } else {
+          // a tie on the high word (rare): exact values by replaying the tied slots' draws
+          int64_t ex = LMAX;
+          uint32_t ep = FP_NONE, ev = 0;
+          uint64_t es = 0;
+#pragma unroll
+          for (int i = 0; i < RKW; i++) {
+            if (live && mh[i] == wh) {
+              const int64_t e = exact_min(X0[i], wu);
+              if (e < ex || (e == ex && FP[i] < ep)) {
+                ex = e; ep = FP[i]; es = X0[i]; ev = (j & 1) ? KH[i] : KL[i];
+              }
+            }
+          }
+          const int64_t wx = wave_min_i64(ex);
+          const uint32_t wp = wave_min_u32(ex == wx ? ep : FP_NONE);
+          const uint64_t w2 = __builtin_amdgcn_ballot_w64(ex == wx && ep == wp);
+          const uint32_t l2 = (uint32_t)__builtin_ctzll(w2);
+          if (wx == LMAX) continue;                   // never below the jar's initial value
+          nb.hi = (int32_t)((uint64_t)wx >> 32);
+          nb.fp = wp;
+          nb.v = __builtin_amdgcn_readlane(ev, l2);
+          nb.w = 0;
+          nb.state = (uint64_t)wx;
+          (void)es;
+        }
+        if (rec_less(nb, cur) && lane == 0) best[j] = nb;
+      } else {
+        // exact 64-bit minima (one draw per function, or weights that differ in the wave)
+        int64_t mi[RKW];
+#pragma unroll
+        for (int i = 0; i < RKW; i++) mi[i] = LMAX;
+        if (wu == 1) {
+#pragma unroll
+          for (int i = 0; i < RKW; i++) {
+            X[i] = xs64(X[i]);
+            mi[i] = (int64_t)X[i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < RKW; i++) {
+            for (int32_t t = 0; t < W[i]; t++) {
+              X[i] = xs64(X[i]);
+              mi[i] = (int64_t)X[i] < mi[i] ? (int64_t)X[i] : mi[i];
+            }
+          }
         }
         // the jar's strict '<' in key order: equal draws keep the earlier first occurrence
-        if (mi < mx || (mi == mx && FP[i] < mp)) {
-          mx = mi;
-          mp = FP[i];
-          mv = (j & 1) ? KH[i] : KL[i];
+        int64_t mx = LMAX;
+        uint32_t mp = FP_NONE, mv = 0;
+#pragma unroll
+        for (int i = 0; i < RKW; i++) {
+          if (mi[i] < mx || (mi[i] == mx && FP[i] < mp)) {
+            mx = mi[i];
+            mp = FP[i];
+            mv = (j & 1) ? KH[i] : KL[i];
+          }
         }
-      }
-      const int64_t wx = wave_min_i64(mx);
-      if (wx == LMAX) continue;                     // no draw below the initial value
-      const uint64_t hold = __builtin_amdgcn_ballot_w64(mx == wx);
-      uint32_t wp, wv;
-      if (popc64(hold) == 1) {
-        const uint32_t ln = (uint32_t)__builtin_ctzll(hold);
-        wp = __builtin_amdgcn_readlane(mp, ln);
-        wv = __builtin_amdgcn_readlane(mv, ln);
-      } else {
-        wp = wave_min_u32(mx == wx ? mp : 0xFFFFFFFFu);
-        const uint64_t who = __builtin_amdgcn_ballot_w64(mx == wx && mp == wp);
-        wv = __builtin_amdgcn_readlane(mv, (uint32_t)__builtin_ctzll(who));
-      }
-      if (lane == 0 && (wx < bx[j] || (wx == bx[j] && wp < bp[j]))) {
-        bx[j] = wx;
-        bp[j] = wp;
-        bv[j] = wv;
+        if (!live) mx = LMAX;
+        const int64_t wx = wave_min_i64(mx);
+        if (wx == LMAX) continue;                     // no draw below the initial value
+        if (cur.fp != FP_NONE && (int32_t)((uint64_t)wx >> 32) > cur.hi) continue;
+        const uint64_t hold = __builtin_amdgcn_ballot_w64(mx == wx);
+        uint32_t wp, wv;
+        if (popc64(hold) == 1) {
+          const uint32_t ln = (uint32_t)__builtin_ctzll(hold);
+          wp = __builtin_amdgcn_readlane(mp, ln);
+          wv = __builtin_amdgcn_readlane(mv, ln);
+        } else {
+          wp = wave_min_u32(mx == wx ? mp : FP_NONE);
+          const uint64_t who = __builtin_amdgcn_ballot_w64(mx == wx && mp == wp);
+          wv = __builtin_amdgcn_readlane(mv, (uint32_t)__builtin_ctzll(who));
+        }
+        const BestRec nb{(int32_t)((uint64_t)wx >> 32), wp, wv, 0, (uint64_t)wx};
+        if (rec_less(nb, cur) && lane == 0) best[j] = nb;
       }
     }
   }
@@ -507,14 +640,12 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
   }
   __syncthreads();
   for (int32_t j = tid; j < H; j += 256) {
-    int64_t x = bx_all[j];
-    uint32_t p = bp_all[j], v = bv_all[j];
+    BestRec b = best_all[j];
     for (int w = 1; w < 4; w++) {
-      const int64_t y = bx_all[w * H + j];
-      const uint32_t q = bp_all[w * H + j];
-      if (y < x || (y == x && q < p)) { x = y; p = q; v = bv_all[w * H + j]; }
+      const BestRec c = best_all[w * H + j];
+      if (rec_less(c, b)) b = c;
     }
-    A.minhash[(size_t)sid * H + j] = x == LMAX ? 0 : (int32_t)v;
+    A.minhash[(size_t)sid * H + j] = b.fp == FP_NONE ? 0 : (int32_t)b.v;
   }
   // no k-mer of positive weight: the jar's sketch constructor fails and the read (or this
   // strand) is skipped
@@ -1370,7 +1501,7 @@ static int sketch_minhash(mhap_ctx *c, const std::vector<uint32_t> &sids) {
     SketchArgs SA{c->mkeys2.p, c->mpos2.p, c->mkoff.p, c->msids.p, (int32_t)c->P.num_hashes,
                   mode, c->has_table ? c->ftab.p : nullptr, c->fmask, c->W.repeat_idf_scale,
                   c->W.no_tf, c->minhash.p, c->ocount.p, c->kctr.p};
-    const size_t lds = 16ull * 4 * c->P.num_hashes;
+    const size_t lds = sizeof(BestRec) * 4 * c->P.num_hashes;
     MHC(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(k_mh_minhash, dim3(nb), dim3(256), lds, s, SA);
     MHC(hipGetLastError());
