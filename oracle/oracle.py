@@ -261,8 +261,11 @@ def mhap_convert(rs, mhap_path: str, hash_base: int = 1, num_hash: int | None = 
         raise FileNotFoundError(MHAPCONVERT_BIN)
     nh = rs.nreads if num_hash is None else num_hash
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as wd:
-        reads = os.path.join(wd, "reads.bin")
-        write_reads_file(reads, rs)
+        # reads_path: a reads file written beforehand (rs is then None; read sets too large
+        # to hold twice in host memory are written piecewise, tools/make_c4_chunk_digest.py)
+        reads = reads_path or os.path.join(wd, "reads.bin")
+        if reads_path is None:
+            write_reads_file(reads, rs)
         cp = subprocess.run([REF_BIN, reads, os.path.join(wd, "w"), "-", "--gkp-only"],
                             capture_output=True, text=True)
         if cp.returncode != 0:
@@ -394,7 +397,7 @@ def run_oracle_driver(rs, params: dict, hash_range=(1, UINT32_MAX), ref_range=(1
 def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
                   skip_kmers=None, minkmers: bool = False, extra=None, workdir=None,
                   with_time=False, batching: dict | None = None, with_stats=False,
-                  libs=None):
+                  libs=None, reads_path=None):
     """Run the reference overlapInCore (built from its sources) on `rs`.
 
     By default the whole read set is one hash batch and one ref range, so every pair (a<b)

@@ -142,7 +142,9 @@ int main(int argc, char **argv) {
   if (nreads && fread(lens.data(), 4, nreads, R) != nreads) die("short lengths");
   uint64_t total = 0;
   for (uint32_t i = 0; i < nreads; i++) total += lens[i];
-  std::vector<char> bases(total + 1), quals(total + 1);
+  //  quals only when the file has them (a 2 M x 12 kb read set would otherwise hold 24 GB
+  //  of zeros beside its bases)
+  std::vector<char> bases(total + 1), quals(hasq ? total + 1 : 1);
   if (total && fread(bases.data(), 1, total, R) != total) die("short bases");
   if (hasq && total && fread(quals.data(), 1, total, R) != total) die("short quals");
   fclose(R);
