@@ -72,6 +72,10 @@ def parse_args(argv=None):
                     help="skip the configs[1] seed-hit figure (profiling passes)")
     ap.add_argument("--no-shard-timing", action="store_true",
                     help="skip the per-shard timing (1 GPU: each of the 8 query shards in turn)")
+    ap.add_argument("--ovb-out", default=None,
+                    help="after the timed region, write the last job's records as the job's "
+                         ".ovb + .counts (+ the -s stats) into this directory and time it "
+                         "(configs[4]'s per-rank output, overlapInCore.C:197)")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the side lines (configs[4] rank job, MHAP configs[3]) that the "
                          "default 1-GPU run adds after the headline")
@@ -166,6 +170,7 @@ def main() -> None:
         parity = job.parity(st, reduce, SUM, torch)
 
     roof, probe_roof, traffic_note = rooflines(args, job, st, world)
+    ovb = job.write_output(args.ovb_out) if args.ovb_out else None
 
     seed_only = job.seed_only() if world == 1 and not args.no_seed_only else None
     shard = job.shard_timing(ms_step) if world == 1 and not args.no_shard_timing else None
@@ -221,6 +226,8 @@ def main() -> None:
             "index_allgather": xgmi,
             "cpu_baseline": cpu,
         }
+        if ovb is not None:
+            line["ovb_output"] = ovb
         if side is not None:
             line.update(side)
         print(json.dumps(line), flush=True)
@@ -344,6 +351,26 @@ class Configs2:
                          out.get("sha256_ok", True))
         out["check_s"] = round(time.time() - t0, 2)
         return out
+
+    def write_output(self, out_dir: str) -> dict:
+        """This rank's output files as overlapInCore writes them with -o / -s
+        (overlapInCore.C:197, :569): <dir>/<rank>.ovb (snappy-framed ovFile) + .counts, and
+        the -s stats text -- timed from the device-resident records (fetch, host sort,
+        encode, write).  The host merge of the ranks' files into one store is canu's own
+        ovStoreBuild (tests/test_store_merge.py)."""
+        os.makedirs(out_dir, exist_ok=True)
+        base = os.path.join(out_dir, f"rank{self.rank:02d}")
+        t0 = time.perf_counter()
+        self.oic.write_ovb(base + ".ovb")
+        t1 = time.perf_counter()
+        self.oic.write_stats(base + ".stats")
+        size = sum(os.path.getsize(base + x) for x in (".ovb", ".counts")
+                   if os.path.exists(base + x))
+        return {"ovb": os.path.relpath(base + ".ovb", ROOT) if base.startswith(ROOT) else
+                base + ".ovb", "records": int(self.oic.stats()["total_overlaps"]),
+                "bytes": size, "write_s": round(t1 - t0, 2),
+                "note": "after the timed region: fetch + host sort + .ovb/.counts encode and "
+                        "write of this rank's records (ovl_ctx_write_ovb)"}
 
     def seed_only(self):
         """BASELINE configs[1] on the same read set: the hash index + seed-hit kernels alone
@@ -773,7 +800,7 @@ def side_runs(timeout_s: int = 300) -> dict:
     import subprocess
     keep4 = ("value", "unit", "ms_per_step", "breakdown_ms", "pairs", "pair_kernels",
              "roofline", "probe_roofline", "traffic_source", "config", "setup_s", "setup_hbm",
-             "parity", "counters")
+             "parity", "counters", "ovb_output")
     keep3 = ("value", "unit", "ms_per_step", "breakdown_ms", "config", "setup_s", "roofline",
              "candidates_per_step", "overlaps_per_step", "parity")
     runs = {"configs4_rank": ([sys.executable, os.path.join(ROOT, "bench.py"), "--workload",

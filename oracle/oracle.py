@@ -261,11 +261,8 @@ def mhap_convert(rs, mhap_path: str, hash_base: int = 1, num_hash: int | None = 
         raise FileNotFoundError(MHAPCONVERT_BIN)
     nh = rs.nreads if num_hash is None else num_hash
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as wd:
-        # reads_path: a reads file written beforehand (rs is then None; read sets too large
-        # to hold twice in host memory are written piecewise, tools/make_c4_chunk_digest.py)
-        reads = reads_path or os.path.join(wd, "reads.bin")
-        if reads_path is None:
-            write_reads_file(reads, rs)
+        reads = os.path.join(wd, "reads.bin")
+        write_reads_file(reads, rs)
         cp = subprocess.run([REF_BIN, reads, os.path.join(wd, "w"), "-", "--gkp-only"],
                             capture_output=True, text=True)
         if cp.returncode != 0:
@@ -411,8 +408,11 @@ def run_reference(rs, params: dict, threads: int = 1, hash_bits: int = 20,
     own = workdir is None
     wd = workdir or tempfile.mkdtemp(prefix="oicref_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
-        reads = os.path.join(wd, "reads.bin")
-        write_reads_file(reads, rs)
+        # reads_path: a reads file written beforehand (rs is then None; read sets too large
+        # to hold twice in host memory are written piecewise, tools/make_c4_chunk_digest.py)
+        reads = reads_path or os.path.join(wd, "reads.bin")
+        if reads_path is None:
+            write_reads_file(reads, rs)
         out = os.path.join(wd, "records.bin")
         args = [REF_BIN, reads, os.path.join(wd, "w"), out, "-t", str(threads),
                 "--hashbits", str(hash_bits), "--time"]

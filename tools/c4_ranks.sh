@@ -14,6 +14,6 @@ c = d.get("counters", {})
 print(json.dumps({"job": d["config"]["job"], "ms": d["ms_per_step"], "setup_s": d["setup_s"],
                   "records": d["overlaps_per_step"], "breakdown_ms": d["breakdown_ms"],
                   "sb": c.get("super_batches"), "chunks": c.get("query_chunks"),
-                  "free_gb": d["setup_hbm"]["device_free_gb"]}))
+                  "free_gb": d["setup_hbm"]["device_free_gb"], "ovb": d.get("ovb_output")}))
 PY
 done

@@ -78,6 +78,7 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--reuse", action="store_true", help="reuse <workdir>/reads.bin")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     out = args.out or os.path.join(ROOT, "tests", "golden", f"c4chunk{args.hi // 1000}k.json")
@@ -85,8 +86,14 @@ def main() -> None:
     os.makedirs(wd, exist_ok=True)
     reads = os.path.join(wd, "reads.bin")
     t0 = time.time()
-    total, lens = write_reads_piecewise(reads, args.reads, args.hi, args.read_len,
-                                        args.coverage, args.read_error, args.seed)
+    if args.reuse and os.path.exists(reads):          # a reads file an earlier run wrote
+        with open(reads, "rb") as f:
+            assert f.read(4) == b"OICR" and struct.unpack("<III", f.read(12))[1] == args.hi
+            lens = np.frombuffer(f.read(4 * args.hi), dtype="<u4")
+        total = int(lens.sum(dtype=np.uint64))
+    else:
+        total, lens = write_reads_piecewise(reads, args.reads, args.hi, args.read_len,
+                                            args.coverage, args.read_error, args.seed)
     t_gen = time.time() - t0
     h_lo, h_hi = args.hi - args.slice + 1, args.hi
     hashed = int(lens[h_lo - 1:h_hi].sum(dtype=np.uint64)) + (h_hi - h_lo + 1)
