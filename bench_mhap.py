@@ -215,10 +215,11 @@ def main() -> None:
     value = total_ovl * args.steps / elapsed
     gbp = total_bases / 1e9
 
-    # Dominant kernel: the MinHash draw kernel k_mh_minhash (its launches timed live by the
-    # library's events, ms_sketch_kernel).  It is bound by vector-instruction issue: every
-    # distinct k-mer of both strands makes w x H xorshift64 draws, each a 64-bit
-    # shift / xor chain and a signed 64-bit minimum.  With the PMC pass of this
+    # Dominant kernel: the MinHash draws -- k_mh_minhash (the exact sample and the k-mers of
+    # other weights) and k_mh_bitslice (the rest, 32 chains per lane in bit planes), timed
+    # together live by the library's events (ms_sketch_kernel: both launches of a batch).
+    # They are bound by vector-instruction issue: every distinct k-mer of both strands makes
+    # w x H xorshift64 draws.  With the PMC pass of this
     # workload and these sources (profiles/traffic_mhap.json) the roofline is VALU
     # wave-instructions/s against 1,024 SIMDs x 2.4 GHz / 2 (wave64 over 2 cycles); its HBM
     # figures beside: algorithmic bytes = the sorted (key, position) pairs read once (12 B
@@ -226,12 +227,21 @@ def main() -> None:
     draws = int(st.get("sketch_draws", 0))
     nl = max(int(st.get("sketch_launches", 0)), 1)
     k_ms = st.get("ms_sketch_kernel", 0.0) / nl
-    kname = "k_mh_minhash"
+    kname = "k_mh_minhash + k_mh_bitslice"
     strands = 2 * (hi - lo)
     positions = max(0, int(np.maximum(lengths[lo:hi].astype(np.int64) - P.k + 1, 0).sum())) * 2
     per_launch = (12.0 * positions + 4.0 * H * strands) / nl
     pmc, pmc_note = load_pmc(args, world)
-    kp = (pmc or {}).get(kname, {})
+    # the two draw kernels' per-launch figures (one launch of each per batch) added
+    kp = {}
+    for kk in ("k_mh_minhash", "k_mh_bitslice"):
+        e = (pmc or {}).get(kk)
+        if not e:
+            continue
+        for f in ("valu_insts", "hbm_bytes_per_launch"):
+            kp[f] = kp.get(f, 0.0) + e.get(f, 0.0)
+        if kk == "k_mh_bitslice":
+            kp["wait_inst_any_frac"] = e.get("wait_inst_any_frac", 0.0)
     hbm = {"achieved": round(per_launch / (k_ms * 1e-3) / 1e9, 2) if k_ms > 0 else None,
            "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "algorithmic_bytes_per_launch": int(per_launch),

@@ -364,6 +364,23 @@ struct SketchArgs {
   int32_t *minhash;               // [strand][H]
   uint32_t *ocount;               // zeroed for a strand with no k-mer of weight > 0
   unsigned long long *stat;       // [0] distinct k-mers, [1] draws
+  // bit-sliced draws (k_mh_bitslice; bs_w = 0: every k-mer here).  The k-mers of weight bs_w
+  // past the strand's first round go to its list (bs_key / bs_fp at koff[b], bs_cnt[b] of
+  // them) and this kernel leaves its exact minima in best_out instead of the sketch
+  int32_t bs_w;
+  uint32_t bs_sample;             // a strand's first bs_sample sorted k-mers are drawn here
+  uint64_t *bs_key;
+  uint32_t *bs_fp;
+  uint32_t *bs_cnt;
+  struct BestOut *best_out;       // [batch strand][H]
+};
+
+// one hash function's minimum so far: the exact draw, the k-mer's first position
+// (FP_NONE: none yet) and the value stored (a key half)
+struct BestOut {
+  int64_t val;
+  uint32_t fp;
+  uint32_t v;
 };
 
 __device__ __forceinline__ uint64_t slot_hash(uint64_t key) {
@@ -434,9 +451,9 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
   const int32_t H = A.H;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   BestRec *best_all = (BestRec *)s_raw;                      // [4][H]
-  __shared__ uint32_t s_live;
+  __shared__ uint32_t s_live, s_bsn;
   for (int32_t j = tid; j < 4 * H; j += 256) best_all[j] = BestRec{0x7FFFFFFF, FP_NONE, 0, 0, 0};
-  if (tid == 0) s_live = 0;
+  if (tid == 0) { s_live = 0; s_bsn = 0; }
   __syncthreads();
   const uint32_t bi = blockIdx.x, sid = A.sids[bi];
   const uint64_t s0 = A.koff[bi], s1 = A.koff[bi + 1];
@@ -466,6 +483,17 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
             const double tf = A.no_tf ? 1.0 : (double)cnt;
             w = java_round(__dmul_rn(tf, sidf));
             if (w < 1) w = 1;
+          }
+          if (w > 0 && w == A.bs_w && p >= s0 + A.bs_sample) {
+            // past the strand's first bs_sample sorted positions (a sample whose minima make
+            // the bit-sliced threshold tight), the dominant weight's k-mers are drawn
+            // bit-sliced (k_mh_bitslice, from the minima this kernel leaves): listed here
+            const uint32_t slot = atomicAdd(&s_bsn, 1u);
+            A.bs_key[s0 + slot] = key;
+            A.bs_fp[s0 + slot] = A.pos[p];
+            nkm++;
+            ndraw += (unsigned long long)w * (unsigned long long)H;
+            w = 0;
           }
           if (w > 0) {
             W[i] = (int32_t)(w > 0x7FFFFFFF ? 0x7FFFFFFF : w);
@@ -547,8 +575,10 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
           nb.fp = __builtin_amdgcn_readlane(fp, ln);
           nb.v = __builtin_amdgcn_readlane(v, ln);
           nb.w = wu;
-          nb.state = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), ln) << 32) |
-                     __builtin_amdgcn_readlane((uint32_t)st, ln);
+          // (readlane returns an int: the low word is widened unsigned, or a set bit 31 would
+          // smear over the high word -- the state is a number k_mh_bitslice compares with)
+          nb.state = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), ln) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)st, ln);
         } else {
           // a tie on the high word (rare): exact values by replaying the tied slots' draws
           int64_t ex = LMAX;
@@ -639,17 +669,182 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
     }
   }
   __syncthreads();
+  if (A.bs_w && tid == 0) A.bs_cnt[bi] = s_bsn;
   for (int32_t j = tid; j < H; j += 256) {
     BestRec b = best_all[j];
     for (int w = 1; w < 4; w++) {
       const BestRec c = best_all[w * H + j];
       if (rec_less(c, b)) b = c;
     }
-    A.minhash[(size_t)sid * H + j] = b.fp == FP_NONE ? 0 : (int32_t)b.v;
+    if (A.bs_w) {
+      BestOut o;
+      o.val = b.fp == FP_NONE ? LMAX : exact_min(b.state, b.w);
+      o.fp = b.fp;
+      o.v = b.v;
+      A.best_out[(size_t)bi * H + j] = o;
+    } else {
+      A.minhash[(size_t)sid * H + j] = b.fp == FP_NONE ? 0 : (int32_t)b.v;
+    }
   }
   // no k-mer of positive weight: the jar's sketch constructor fails and the read (or this
   // strand) is skipped
   if (tid == 0 && s_live == 0) A.ocount[sid] = 0;
+}
+
+// ---- bit-sliced draws ------------------------------------------------------------------
+// Nearly every k-mer of a canu sketch has the same weight (seen once, not in the -f table:
+// round(1 x 10) = 10), so after a strand's first round (k_mh_minhash, exact, which leaves the
+// minima so far in best_out) its k-mers of that weight are drawn 32 to a lane in BIT PLANES:
+// plane b (one VGPR) holds bit b of 32 chains' states (bit p: the lane's chain p, list entry
+// base + 64 p + lane).  A xorshift64 step is then 132 plane XORs for 32 chains -- the shifts
+// are renamings of planes -- instead of 2 64-bit shifts, 5 XORs and a right shift per chain.
+// The minimum is not tracked per chain: a draw matters only if it is <= the function's best
+// so far T, and since T is small after the exact round (the minimum of ~20 k draws), a draw
+// can be below it only if the top Z bits of x ^ 2^63 are zero, Z = clz(T ^ 2^63): one OR over
+// Z planes tests 32 chains.  The few chains that pass are read out of the planes (the exact
+// 64-bit draw) and compared with the best in the jar's order -- smaller draw, then earlier
+// first occurrence -- so the result is the exact minimum whatever the draw order.
+constexpr uint32_t BS_CHAINS = 2048;     // k-mers per wave per batch (64 lanes x 32 planes)
+
+__device__ __forceinline__ void bs_step(uint32_t (&S)[64]) {
+#pragma unroll
+  for (int b = 63; b >= 21; b--) S[b] ^= S[b - 21];       // x ^= x << 21
+#pragma unroll
+  for (int b = 0; b <= 28; b++) S[b] ^= S[b + 35];        // x ^= x >>> 35
+#pragma unroll
+  for (int b = 63; b >= 4; b--) S[b] ^= S[b - 4];         // x ^= x << 4
+}
+
+// draws t.. of the current function until one leaves a chain that may be <= T (its top Z
+// bits of x ^ 2^63 all zero) or the function's w draws are done; returns the next draw
+template <int Z>
+__device__ __forceinline__ int32_t bs_draws(uint32_t (&S)[64], uint32_t valid, int32_t t,
+                                            int32_t w, uint32_t &cand) {
+  for (; t < w;) {
+    bs_step(S);
+    t++;
+    uint32_t c = valid;
+    if constexpr (Z > 0) {
+      uint32_t z = ~S[63];                                  // the sign bit, flipped
+#pragma unroll
+      for (int i = 1; i < Z; i++) z |= S[63 - i];
+      c &= ~z;
+    }
+    if (__builtin_amdgcn_ballot_w64(c != 0)) { cand = c; return t; }
+  }
+  cand = 0;
+  return t;
+}
+
+struct BsArgs {
+  const uint64_t *bs_key;         // per batch strand at koff[b]: keys of its listed k-mers
+  const uint32_t *bs_fp;          //   and their first positions
+  const uint32_t *bs_cnt;
+  const uint64_t *koff;
+  const uint32_t *sids;
+  const BestOut *best_in;         // [batch strand][H]: k_mh_minhash's minima
+  int32_t H;
+  int32_t w;                      // the listed k-mers' weight
+  int32_t *minhash;               // [strand][H]
+  int32_t zmax;                   // planes tested at most (MHAP_BS_ZMAX, A/B and checks: 64)
+};
+
+__device__ __forceinline__ uint32_t uni_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)v);
+}
+
+// one wave per strand
+__global__ void __launch_bounds__(64, 5) k_mh_bitslice(BsArgs A) {
+  extern __shared__ uint8_t s_raw[];
+  BestOut *best = (BestOut *)s_raw;                          // [H]
+  const uint32_t lane = threadIdx.x, bi = blockIdx.x, sid = A.sids[bi];
+  const int32_t H = A.H, w = A.w;
+  for (int32_t j = lane; j < H; j += 64) best[j] = A.best_in[(size_t)bi * H + j];
+  wave_sync();
+  const uint64_t s0 = A.koff[bi];
+  const uint32_t n = A.bs_cnt[bi];
+  const uint64_t *keys = A.bs_key + s0;
+  const uint32_t *fps = A.bs_fp + s0;
+  for (uint32_t base = 0; base < n; base += BS_CHAINS) {
+    uint32_t S[64];
+#pragma unroll
+    for (int b = 0; b < 64; b++) S[b] = 0;
+    uint32_t valid = 0;
+    for (uint32_t p = 0; p < 32; p++) {
+      const uint32_t idx = base + p * 64 + lane;
+      if (idx < n) {
+        const uint64_t key = keys[idx];
+        const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+        valid |= 1u << p;
+#pragma unroll
+        for (int b = 0; b < 32; b++) {
+          S[b] |= ((lo >> b) & 1u) << p;
+          S[b + 32] |= ((hi >> b) & 1u) << p;
+        }
+      }
+    }
+    for (int32_t j = 0; j < H; j++) {
+      BestOut cur = best[j];
+      cur.fp = uni_u32(cur.fp);
+      cur.v = uni_u32(cur.v);
+      cur.val = (int64_t)(((uint64_t)uni_u32((uint32_t)((uint64_t)cur.val >> 32)) << 32) |
+                          uni_u32((uint32_t)cur.val));
+      bool changed = false;
+      for (int32_t t = 0; t < w;) {
+        // draws may be <= T only with their top Z bits (of x ^ 2^63) clear; fewer planes
+        // tested is a looser filter, never a wrong one
+        const uint64_t U = cur.fp == FP_NONE ? ~0ull : ((uint64_t)cur.val ^ (1ull << 63));
+        const int32_t Z = min(U == 0 ? 64 : (int32_t)__builtin_clzll(U), A.zmax);
+        uint32_t cand = 0;
+        if (Z >= 20)      t = bs_draws<20>(S, valid, t, w, cand);
+        else if (Z >= 16) t = bs_draws<16>(S, valid, t, w, cand);
+        else if (Z >= 13) t = bs_draws<13>(S, valid, t, w, cand);
+        else if (Z >= 10) t = bs_draws<10>(S, valid, t, w, cand);
+        else if (Z >= 6)  t = bs_draws<6>(S, valid, t, w, cand);
+        else              t = bs_draws<0>(S, valid, t, w, cand);
+        if (!__builtin_amdgcn_ballot_w64(cand != 0)) continue;
+        // the lane's smallest (draw, first position) among its passing chains that beats the
+        // best so far (a strict '<' on the draw, then the earlier first occurrence)
+        int64_t bv = LMAX;
+        uint32_t bfp = FP_NONE, bidx = 0;
+        for (uint32_t m = cand; m;) {
+          const uint32_t c = (uint32_t)__builtin_ctz(m);
+          m &= m - 1;
+          uint32_t lo = 0, hi = 0;
+#pragma unroll
+          for (int b = 0; b < 32; b++) {
+            lo |= ((S[b] >> c) & 1u) << b;
+            hi |= ((S[b + 32] >> c) & 1u) << b;
+          }
+          const int64_t v = (int64_t)(((uint64_t)hi << 32) | lo);
+          const uint32_t idx = base + c * 64 + lane;
+          const uint32_t fp = fps[idx];
+          const bool beats = cur.fp == FP_NONE ? v < LMAX
+                                               : (v < cur.val || (v == cur.val && fp < cur.fp));
+          if (beats && (v < bv || (v == bv && fp < bfp))) { bv = v; bfp = fp; bidx = idx; }
+        }
+        const int64_t wv = wave_min_i64(bv);
+        if (wv == LMAX) continue;                              // no draw beat it
+        const uint32_t wp = wave_min_u32(bv == wv ? bfp : FP_NONE);
+        const uint64_t who = __builtin_amdgcn_ballot_w64(bv == wv && bfp == wp);
+        const uint32_t widx = uni_u32(__builtin_amdgcn_readlane(bidx, (uint32_t)__builtin_ctzll(who)));
+        const uint64_t key = keys[widx];
+        cur.val = wv;
+        cur.fp = wp;
+        cur.v = (j & 1) ? (uint32_t)(key >> 32) : (uint32_t)key;
+        changed = true;
+      }
+      if (changed) {
+        if (lane == 0) best[j] = cur;
+        wave_sync();
+      }
+    }
+  }
+  wave_sync();
+  for (int32_t j = lane; j < H; j += 64) {
+    const BestOut b = best[j];
+    A.minhash[(size_t)sid * H + j] = b.fp == FP_NONE ? 0 : (int32_t)b.v;
+  }
 }
 
 // a read whose forward strand was skipped is skipped whole (SequenceSketchStreamer
@@ -1196,6 +1391,8 @@ struct mhap_ctx {
   MBuf<uint32_t> mpos, mpos2, msids;
   MBuf<uint64_t> mkoff;
   MBuf<uint8_t> msort_tmp;
+  MBuf<uint32_t> mbscnt;          // bit-sliced draws: per batch strand, its listed k-mers
+  MBuf<BestOut> mbest;            //   and the exact pass's minima [batch strand][H]
   // index
   MBuf<uint64_t> keys, keys2, toff;
   MBuf<uint32_t> vals, vals2;
@@ -1460,14 +1657,34 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   return M_OK;
 }
 
+// The weight of a k-mer seen once in its strand and not in the -f table -- nearly all of a
+// sketch's k-mers -- whose draws k_mh_bitslice takes (0: off; MHAP_BITSLICE=0 for A/Bs)
+static int32_t bitslice_weight(const mhap_ctx *c, int mode) {
+  if (const char *e = getenv("MHAP_BITSLICE"))
+    if (atoi(e) == 0) return 0;
+  if (mode != W_TFIDF) return 1;                    // W_ONE: 1 (not popular); W_COUNT: count
+  const double x = c->W.repeat_idf_scale;           // tf(1) x scaledIdf of an absent k-mer
+  const double f = floor(x);
+  const int64_t w = (int64_t)f + (x - f >= 0.5 ? 1 : 0);   // Math.round
+  return (int32_t)std::min<int64_t>(std::max<int64_t>(w, 1), 0x7FFFFFFF);
+}
+
 // The MinHash sketches of strands (sids) in batches of <= KEY_BUDGET k-mers: keys, segmented
-// radix sort of (key, position), draws.
+// radix sort of (key, position), draws (exact for the first round of every strand and for
+// k-mers of other weights, bit-sliced for the rest).
 static int sketch_minhash(mhap_ctx *c, const std::vector<uint32_t> &sids) {
   hipStream_t s = c->stream;
   const int32_t k = (int32_t)c->P.k;
   const uint64_t KEY_BUDGET = 1ull << 29;
   const int mode = c->W.repeat_weight < 0.0 ? W_ONE
                  : (c->has_table && c->W.repeat_weight < 1.0) ? W_TFIDF : W_COUNT;
+  const int32_t bs_w = bitslice_weight(c, mode);
+  const int32_t H = (int32_t)c->P.num_hashes;
+  // the exact sample: 512 k-mers x w draws put a function's minimum near 2^64 / 5,120 above
+  // -2^63, so a bit-sliced draw passes the 12-13-plane filter about once per 2,048-chain
+  // batch and function (MHAP_BS_SAMPLE for A/Bs)
+  uint32_t bs_sample = 512;
+  if (const char *e = getenv("MHAP_BS_SAMPLE")) bs_sample = (uint32_t)std::max(0, atoi(e));
   for (size_t a = 0; a < sids.size();) {
     std::vector<uint64_t> koff;
     uint64_t tot = 0;
@@ -1498,13 +1715,38 @@ static int sketch_minhash(mhap_ctx *c, const std::vector<uint32_t> &sids) {
     MHC(hipcub::DeviceSegmentedRadixSort::SortPairs(c->msort_tmp.p, tb, c->mkeys.p, c->mkeys2.p,
                                                     c->mpos.p, c->mpos2.p, (int)tot, (int)nb,
                                                     c->mkoff.p, c->mkoff.p + 1, 0, 64, s));
-    SketchArgs SA{c->mkeys2.p, c->mpos2.p, c->mkoff.p, c->msids.p, (int32_t)c->P.num_hashes,
+    if (bs_w && (c->mbscnt.alloc(nb) || c->mbest.alloc((size_t)nb * H)))
+      return mfail(M_OOM, "bit-sliced draws (%u strands)", nb);
+    // the sorted keys are in mkeys2 / mpos2: mkeys / mpos hold the bit-sliced lists
+    SketchArgs SA{c->mkeys2.p, c->mpos2.p, c->mkoff.p, c->msids.p, H,
                   mode, c->has_table ? c->ftab.p : nullptr, c->fmask, c->W.repeat_idf_scale,
-                  c->W.no_tf, c->minhash.p, c->ocount.p, c->kctr.p};
+                  c->W.no_tf, c->minhash.p, c->ocount.p, c->kctr.p,
+                  bs_w, bs_sample, c->mkeys.p, c->mpos.p, c->mbscnt.p, c->mbest.p};
     const size_t lds = sizeof(BestRec) * 4 * c->P.num_hashes;
     MHC(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(k_mh_minhash, dim3(nb), dim3(256), lds, s, SA);
     MHC(hipGetLastError());
+    if (bs_w && getenv("MHAP_BS_DUMP")) {      // checks: the exact pass's minima and lists
+      MHC(hipStreamSynchronize(s));
+      std::vector<BestOut> hb((size_t)nb * H);
+      std::vector<uint32_t> hc(nb);
+      MHC(hipMemcpy(hb.data(), c->mbest.p, sizeof(BestOut) * hb.size(), hipMemcpyDeviceToHost));
+      MHC(hipMemcpy(hc.data(), c->mbscnt.p, 4ull * nb, hipMemcpyDeviceToHost));
+      if (FILE *f = fopen(getenv("MHAP_BS_DUMP"), "wb")) {
+        fwrite(&nb, 4, 1, f);
+        fwrite(sids.data() + a, 4, nb, f);
+        fwrite(hc.data(), 4, nb, f);
+        fwrite(hb.data(), sizeof(BestOut), hb.size(), f);
+        fclose(f);
+      }
+    }
+    if (bs_w) {
+      const char *zm = getenv("MHAP_BS_ZMAX");
+      BsArgs BA{c->mkeys.p, c->mpos.p, c->mbscnt.p, c->mkoff.p, c->msids.p, c->mbest.p, H, bs_w,
+                c->minhash.p, zm ? atoi(zm) : 64};
+      hipLaunchKernelGGL(k_mh_bitslice, dim3(nb), dim3(64), sizeof(BestOut) * H, s, BA);
+      MHC(hipGetLastError());
+    }
     MHC(hipEventRecord(c->ev[3], s));
     MHC(hipStreamSynchronize(s));                 // koff / sids are rewritten next batch
     float t = 0;

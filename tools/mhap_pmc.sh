@@ -17,7 +17,7 @@ pass() {   # name counters...
   local name=$1; shift
   timeout -k 10 -s KILL 300 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/${TAG}_$name \
     -o run -- $JOB > $R/gpurun_out/${TAG}_$name.log 2>&1 || { tail -5 $R/gpurun_out/${TAG}_$name.log; return 1; }
-  for k in k_mh_minhash k_mh_keys k_mh_ordered k_mh_compare; do
+  for k in k_mh_minhash k_mh_bitslice k_mh_keys k_mh_ordered k_mh_compare; do
     python3 $R/tools/pmc_sum.py $R/gpurun_out/${TAG}_$name $k | sed "s/^/$k /" | tee -a $R/gpurun_out/${TAG}_pmc.txt
   done
 }

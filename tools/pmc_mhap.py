@@ -14,7 +14,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_mh_minhash", "k_mh_keys", "k_mh_ordered", "k_mh_candidates", "k_mh_compare")
+KERNELS = ("k_mh_minhash", "k_mh_bitslice", "k_mh_keys", "k_mh_ordered", "k_mh_candidates",
+           "k_mh_compare")
 
 
 def mhap_source_hash() -> str:
