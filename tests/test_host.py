@@ -112,6 +112,29 @@ def test_driver6_replays_the_driver_plans():
         assert abs(p["est_s"] - secs) / secs < 0.06, (lo, hi, p["est_s"], secs)
 
 
+# round 6: every job of the derived plan (dist.c4_plan) measured at full size, one MI355X
+# each (profiles/r06j_c4r{0,3,7}_c4full.json, r06k_c4r{1,2,4,5,6}_c4full.json): block ->
+# (seconds, hash batches, super-batches, query chunks)
+C4_PLAN_RUNS = {(1, 1429263): (26.67, 129, 17, 6), (1429264, 2049284): (26.90, 56, 7, 8),
+                (2049285, 2497633): (26.00, 41, 6, 10), (2497634, 2881292): (26.01, 35, 5, 12),
+                (2881293, 3199278): (25.30, 29, 4, 14), (3199279, 3499780): (26.30, 28, 4, 15),
+                (3499781, 3762174): (25.75, 24, 4, 16), (3762175, 4000000): (24.77, 22, 3, 17)}
+
+
+def test_driver6_model_against_the_measured_plan():
+    """The eight measured jobs are the plan's, and the model replays each one's structure: the
+    same super-batches, query chunks within one (the chunk cap is planned from the free HBM the
+    first super-batch leaves, which the model estimates), time within 8 % (all faster)."""
+    from canu_amd import dist
+    js = dist.c4_plan(4_000_000, 8, 12_000)
+    assert sorted(C4_PLAN_RUNS) == [j["h"] for j in js]
+    for (lo, hi), (secs, nb, nsb, nch) in C4_PLAN_RUNS.items():
+        p = dist.driver_plan(4_000_000, 12_000, lo, hi)
+        assert abs(p["hash_batches"] - nb) <= 1 and p["super_batches"] == nsb, (lo, hi, p)
+        assert abs(p["query_chunks"] - nch) <= 1, (lo, hi, p)
+        assert 0 <= (p["est_s"] - secs) / secs < 0.08, (lo, hi, p["est_s"], secs)
+
+
 def test_c4_full_plan_covers_the_reads(monkeypatch):
     """configs[4]'s plan at 4M reads (dist.c4_plan, cut on DRIVER6): eight contiguous
     `-h lo-hi -r 1-hi` blocks over 1..4M with equal modelled time, and bench.py's
