@@ -464,6 +464,7 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
     uint64_t X[RKW];
     uint32_t KL[RKW], KH[RKW], FP[RKW];
     int32_t W[RKW];
+    uint32_t listed = 0;                 // bit i: slot i's k-mer goes to the bit-sliced list
 #pragma unroll
     for (int i = 0; i < RKW; i++) {
       X[i] = 0; KL[i] = KH[i] = 0; FP[i] = FP_NONE; W[i] = 0;
@@ -487,10 +488,8 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
           if (w > 0 && w == A.bs_w && p >= s0 + A.bs_sample) {
             // past the strand's first bs_sample sorted positions (a sample whose minima make
             // the bit-sliced threshold tight), the dominant weight's k-mers are drawn
-            // bit-sliced (k_mh_bitslice, from the minima this kernel leaves): listed here
-            const uint32_t slot = atomicAdd(&s_bsn, 1u);
-            A.bs_key[s0 + slot] = key;
-            A.bs_fp[s0 + slot] = A.pos[p];
+            // bit-sliced (k_mh_bitslice, from the minima this kernel leaves): listed below
+            listed |= 1u << i;
             nkm++;
             ndraw += (unsigned long long)w * (unsigned long long)H;
             w = 0;
@@ -504,6 +503,23 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
             nkm++;
             ndraw += (unsigned long long)W[i] * (unsigned long long)H;
           }
+        }
+      }
+    }
+    if (A.bs_w) {
+      // the listed k-mers appended to the strand's list, one LDS atomic per wave and slot
+      const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int i = 0; i < RKW; i++) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64((listed >> i) & 1u);
+        if (!m) continue;
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(&s_bsn, (uint32_t)popc64(m));
+        at = (uint32_t)__shfl((int)at, 0) + popc64(m & lt);
+        if ((listed >> i) & 1u) {
+          const uint64_t p = p0 + i;
+          A.bs_key[s0 + at] = A.keys[p];
+          A.bs_fp[s0 + at] = A.pos[p];
         }
       }
     }
@@ -796,13 +812,19 @@ __global__ void __launch_bounds__(64, 5) k_mh_bitslice(BsArgs A) {
         const uint64_t U = cur.fp == FP_NONE ? ~0ull : ((uint64_t)cur.val ^ (1ull << 63));
         const int32_t Z = min(U == 0 ? 64 : (int32_t)__builtin_clzll(U), A.zmax);
         uint32_t cand = 0;
+        // a filter of fewer planes than Z lets up to 2^(Z - planes) x the true candidates
+        // through: a step per plane where the sample leaves Z (13-16), coarser outside
         if (Z >= 20)      t = bs_draws<20>(S, valid, t, w, cand);
+        else if (Z >= 18) t = bs_draws<18>(S, valid, t, w, cand);
         else if (Z >= 16) t = bs_draws<16>(S, valid, t, w, cand);
-        else if (Z >= 13) t = bs_draws<13>(S, valid, t, w, cand);
+        else if (Z == 15) t = bs_draws<15>(S, valid, t, w, cand);
+        else if (Z == 14) t = bs_draws<14>(S, valid, t, w, cand);
+        else if (Z == 13) t = bs_draws<13>(S, valid, t, w, cand);
         else if (Z >= 10) t = bs_draws<10>(S, valid, t, w, cand);
         else if (Z >= 6)  t = bs_draws<6>(S, valid, t, w, cand);
         else              t = bs_draws<0>(S, valid, t, w, cand);
         if (!__builtin_amdgcn_ballot_w64(cand != 0)) continue;
+        const uint32_t T_hi = (uint32_t)((uint64_t)cur.val >> 32);
         // the lane's smallest (draw, first position) among its passing chains that beats the
         // best so far (a strict '<' on the draw, then the earlier first occurrence)
         int64_t bv = LMAX;
@@ -810,12 +832,14 @@ __global__ void __launch_bounds__(64, 5) k_mh_bitslice(BsArgs A) {
         for (uint32_t m = cand; m;) {
           const uint32_t c = (uint32_t)__builtin_ctz(m);
           m &= m - 1;
-          uint32_t lo = 0, hi = 0;
+          // the high word first: most passing chains are above T there
+          uint32_t hi = 0;
 #pragma unroll
-          for (int b = 0; b < 32; b++) {
-            lo |= ((S[b] >> c) & 1u) << b;
-            hi |= ((S[b + 32] >> c) & 1u) << b;
-          }
+          for (int b = 0; b < 32; b++) hi |= ((S[b + 32] >> c) & 1u) << b;
+          if (cur.fp != FP_NONE && (int32_t)hi > (int32_t)T_hi) continue;
+          uint32_t lo = 0;
+#pragma unroll
+          for (int b = 0; b < 32; b++) lo |= ((S[b] >> c) & 1u) << b;
           const int64_t v = (int64_t)(((uint64_t)hi << 32) | lo);
           const uint32_t idx = base + c * 64 + lane;
           const uint32_t fp = fps[idx];
@@ -823,8 +847,8 @@ __global__ void __launch_bounds__(64, 5) k_mh_bitslice(BsArgs A) {
                                                : (v < cur.val || (v == cur.val && fp < cur.fp));
           if (beats && (v < bv || (v == bv && fp < bfp))) { bv = v; bfp = fp; bidx = idx; }
         }
+        if (!__builtin_amdgcn_ballot_w64(bv != LMAX)) continue;   // no draw beat it
         const int64_t wv = wave_min_i64(bv);
-        if (wv == LMAX) continue;                              // no draw beat it
         const uint32_t wp = wave_min_u32(bv == wv ? bfp : FP_NONE);
         const uint64_t who = __builtin_amdgcn_ballot_w64(bv == wv && bfp == wp);
         const uint32_t widx = uni_u32(__builtin_amdgcn_readlane(bidx, (uint32_t)__builtin_ctzll(who)));
@@ -1680,10 +1704,11 @@ static int sketch_minhash(mhap_ctx *c, const std::vector<uint32_t> &sids) {
                  : (c->has_table && c->W.repeat_weight < 1.0) ? W_TFIDF : W_COUNT;
   const int32_t bs_w = bitslice_weight(c, mode);
   const int32_t H = (int32_t)c->P.num_hashes;
-  // the exact sample: 512 k-mers x w draws put a function's minimum near 2^64 / 5,120 above
-  // -2^63, so a bit-sliced draw passes the 12-13-plane filter about once per 2,048-chain
-  // batch and function (MHAP_BS_SAMPLE for A/Bs)
-  uint32_t bs_sample = 512;
+  // the exact sample: a strand's first 2,048 sorted k-mers (x w draws) put a function's
+  // minimum near 2^64 / 20,480 above -2^63, so the bit-sliced filter starts at ~14 planes;
+  // measured on configs[3]: sketch 5.62 s with 2,048, 6.37 s with 512, 6.61 s with 128
+  // (profiles/r06s_mhap_sample_ab.txt; MHAP_BS_SAMPLE for A/Bs)
+  uint32_t bs_sample = 2048;
   if (const char *e = getenv("MHAP_BS_SAMPLE")) bs_sample = (uint32_t)std::max(0, atoi(e));
   for (size_t a = 0; a < sids.size();) {
     std::vector<uint64_t> koff;
