@@ -204,6 +204,50 @@ def test_group_form_of_the_merge_equals_the_literal_merge():
     assert diffs > 100
 
 
+def test_bit_plane_draws_equal_the_xorshift_chain():
+    """The bit-sliced draws of k_mh_bitslice (mhap.hip), restated on the host: 32 chains in
+    64 planes (plane b, bit p = bit b of chain p), a xorshift64 step as plane XORs -- x ^= x <<
+    21 is plane b ^= plane b - 21 from the top down, x ^= x >>> 35 plane b ^= plane b + 35 from
+    the bottom up, x ^= x << 4 plane b ^= plane b - 4 from the top down -- equals the jar's
+    chain (MinHashSketch.computeNgramMinHashesWeighted @334-445) draw for draw, and the
+    filter (the top Z = clz(T ^ 2^63) planes of x ^ 2^63 all zero) lets every draw <= T
+    through."""
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 2**63, size=32, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    planes = [np.uint32(0)] * 64
+    for b in range(64):
+        planes[b] = np.uint32(sum(int((int(x[p]) >> b) & 1) << p for p in range(32)))
+    M64 = (1 << 64) - 1
+    chains = [int(v) for v in x]
+    for _ in range(40):
+        for b in range(63, 20, -1):
+            planes[b] ^= planes[b - 21]
+        for b in range(0, 29):
+            planes[b] ^= planes[b + 35]
+        for b in range(63, 3, -1):
+            planes[b] ^= planes[b - 4]
+        for p in range(32):
+            c = chains[p]
+            c ^= (c << 21) & M64
+            c ^= c >> 35
+            c ^= (c << 4) & M64
+            chains[p] = c
+        back = [sum(((int(planes[b]) >> p) & 1) << b for b in range(64)) for p in range(32)]
+        assert back == chains
+        # the filter: for a threshold between the chains' values, every chain <= T passes
+        signed = sorted((c - (1 << 64) if c >> 63 else c) for c in chains)
+        T = signed[3]
+        U = (T & M64) ^ (1 << 63)
+        Z = 64 if U == 0 else 64 - U.bit_length()
+        z = ~int(planes[63]) & 0xFFFFFFFF
+        for i in range(1, Z):
+            z |= int(planes[63 - i])
+        for p in range(32):
+            v = chains[p] - (1 << 64) if chains[p] >> 63 else chains[p]
+            if v <= T:
+                assert not (z >> p) & 1
+
+
 def test_frequency_counts_keys_and_scaled_idf():
     """FrequencyCounts: a k-mer and its reverse complement share one key (the smaller
     string's hash); scaled idf runs from 1 (the most frequent k-mer) to the scale (a k-mer
