@@ -28,9 +28,29 @@ STAT_KEYS = [("total", "total_overlaps"), ("kmer_hits_with_olap", "kmer_hits_wit
              ("contained", "contained_overlaps"), ("dovetail", "dovetail_overlaps")]
 
 
+_PRE = {}
+
+
 def _golden():
     with open(GOLDEN) as f:
         return json.load(f)
+
+
+def _reads():
+    from canu_amd.synth import synth_reads_parallel
+    w = _golden()["workload"]
+    n = w["reads"]
+    return synth_reads_parallel(n, w["read_len"], int(n * w["read_len"] / w["coverage"]),
+                                w["read_error"], seed=w["seed"], len_jitter=0.2,
+                                read_range=(0, w["loaded_reads"]), workers=16)
+
+
+def pregenerate():
+    """conftest's session-start hook: the 2M reads in a forked pool (~40 s) before any test
+    initialises the GPU."""
+    if "rs" not in _PRE:
+        print(f"\n[{os.path.basename(__file__)}] generating the 2M x 12 kb reads", flush=True)
+        _PRE["rs"] = _reads()
 
 
 def test_chunk_digest_is_a_thin_slice_of_the_configs4_reads():
@@ -48,13 +68,10 @@ def test_chunk_digest_is_a_thin_slice_of_the_configs4_reads():
 @pytest.mark.gpu
 def test_gpu_chunked_sorted_search_matches_reference(monkeypatch):
     from canu_amd.overlap_in_core import OicParameters, OverlapInCore
-    from canu_amd.synth import synth_reads_parallel
     g = _golden()
     w, gj = g["workload"], g["jobs"][0]
-    n, hi = w["reads"], w["loaded_reads"]
-    rs = synth_reads_parallel(n, w["read_len"], int(n * w["read_len"] / w["coverage"]),
-                              w["read_error"], seed=w["seed"], len_jitter=0.2,
-                              read_range=(0, hi), workers=16)
+    n = w["reads"]
+    rs = _PRE.pop("rs", None) or _reads()
     assert rs.total_bases() == w["loaded_bases"]
     (h_lo, h_hi), (r_lo, r_hi) = gj["h"], gj["r"]
     hashed = int(rs.lengths[h_lo - 1:h_hi].sum(dtype=np.uint64)) + (h_hi - h_lo + 1)
