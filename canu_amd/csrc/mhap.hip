@@ -130,6 +130,44 @@ __device__ __host__ __forceinline__ uint64_t murmur128_h1(CH ch, int32_t k) {
   return h1 + h2;
 }
 
+// --supress-noise 1: the jar's bundled Guava 19.0 BloomFilter (MURMUR128_MITZ_64) over the
+// -f file's keys (FrequencyCounts.<init> @189-207, lambda$1 @162-185; keepKmer @0-21).  The
+// Long funnel hashes the key's 8 little-endian bytes with murmur3_128(0); bit i of a key is
+// (h1 + i * h2 & Long.MAX_VALUE) % bitSize (BloomFilterStrategies$2.put / mightContain;
+// oracle mhap_jar.GuavaBloom)
+__device__ __host__ __forceinline__ void murmur128_u64(uint64_t key, uint64_t &h1, uint64_t &h2) {
+  const uint64_t c1 = 0x87C37B91114253D5ull, c2 = 0x4CF5AD432745937Full;
+  uint64_t k1 = key * c1;
+  k1 = rotl64(k1, 31);
+  k1 *= c2;
+  h1 = k1 ^ 8u;                                   // one 8-byte tail, length 8
+  h2 = 8u;
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  h2 += h1;
+}
+
+struct BloomDev {
+  const uint64_t *words;        // null: keep every k-mer
+  uint64_t bit_size;            // 64 x words
+  int32_t k;                    // hash functions
+};
+
+__device__ __host__ __forceinline__ bool bloom_has(const uint64_t *words, uint64_t bit_size,
+                                                   int32_t k, uint64_t key) {
+  uint64_t h1, h2;
+  murmur128_u64(key, h1, h2);
+  uint64_t c = h1;
+  for (int32_t i = 0; i < k; i++, c += h2) {
+    const uint64_t b = (c & 0x7FFFFFFFFFFFFFFFull) % bit_size;
+    if (!((words[b >> 6] >> (b & 63)) & 1ull)) return false;
+  }
+  return true;
+}
+
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
 // Guava Hashing.murmur3_32(0) of the chars as UTF-16 (HashUtils.computeSequenceHashes
@@ -373,6 +411,7 @@ struct SketchArgs {
   uint32_t *bs_fp;
   uint32_t *bs_cnt;
   struct BestOut *best_out;       // [batch strand][H]
+  BloomDev keep;                  // --supress-noise 1: k-mers the filter rejects never count
 };
 
 // one hash function's minimum so far: the exact draw, the k-mer's first position
@@ -476,7 +515,9 @@ __global__ void __launch_bounds__(256) k_mh_minhash(SketchArgs A) {
           while (e < s1 && A.keys[e] == key) e++;
           const uint32_t cnt = (uint32_t)(e - p);
           int64_t w = cnt;
-          if (A.mode == W_ONE) {
+          if (A.keep.words && !bloom_has(A.keep.words, A.keep.bit_size, A.keep.k, key)) {
+            w = 0;                         // keepKmer @70-83: never in the map, never drawn
+          } else if (A.mode == W_ONE) {
             w = (A.ftab && table_find(A.ftab, A.fmask, key)) ? 0 : 1;
           } else if (A.mode == W_TFIDF) {
             const FreqSlot *f = A.ftab ? table_find(A.ftab, A.fmask, key) : nullptr;
@@ -1404,6 +1445,10 @@ struct mhap_ctx {
   bool has_table = false;
   MBuf<FreqSlot> ftab;
   uint64_t fmask = 0;
+  bool has_bloom = false;               // --supress-noise 1 with a -f table
+  MBuf<uint64_t> bloom;
+  uint64_t bloom_bits = 0;
+  int32_t bloom_k = 0;
   // second-stage acceptance: identity(inter / n) >= threshold, per (n, inter)
   MBuf<uint32_t> pass;
   uint32_t pass_empty = 0;
@@ -1605,12 +1650,8 @@ static int check_weighting(const mhap_weighting *w) {
   if (!w) return mfail(M_BAD_PARAM, "null weighting");
   if (!(w->repeat_idf_scale >= 1.0))
     return mfail(M_BAD_PARAM, "The minimum repeat idf scale must be >=1.0.");
-  if (w->supress_noise < 0 || w->supress_noise > 2)
-    return mfail(M_BAD_PARAM, "--supress-noise %d (0, 1 or 2)", w->supress_noise);
-  if (w->supress_noise != 0)
-    return mfail(M_BAD_PARAM, "--supress-noise %d: the jar's Bloom-filter noise suppression "
-                              "is not implemented (canu passes it only with mhapFilterUnique)",
-                 w->supress_noise);
+  if (w->supress_noise < 0 || w->supress_noise > 2)            // FrequencyCounts.<init> @10-50
+    return mfail(M_BAD_PARAM, "Unknown removeUnique option %d.", w->supress_noise);
   return M_OK;
 }
 
@@ -1619,17 +1660,41 @@ int mhap_set_weighting(mhap_ctx *c, const mhap_weighting *w) {
   const int rc = check_weighting(w);
   if (rc) return rc;
   c->W = *w;
-  c->has_table = false;
+  c->has_table = false;                 // no -f: no FrequencyCounts, so no keepKmer either
+  c->has_bloom = false;
   return M_OK;
 }
 
-// FrequencyCounts.<init> @0-429 and its lambda$1 (oracle mhap_jar.FrequencyCounts)
 int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *fractions,
                               uint64_t n, const mhap_weighting *w) {
+  return mhap_set_kmer_frequencies_ex(c, kmers, fractions, n, n, w);
+}
+
+// FrequencyCounts.<init> @0-429 and its lambda$1 (oracle mhap_jar.FrequencyCounts); with
+// --supress-noise 1 also its Bloom filter of every line's key (oracle mhap_jar.GuavaBloom)
+int mhap_set_kmer_frequencies_ex(mhap_ctx *c, const char *kmers, const double *fractions,
+                                 uint64_t n, uint64_t expected, const mhap_weighting *w) {
   if (!c) return mfail(M_STATE, "null context");
   int rc = check_weighting(w);
   if (rc) return rc;
   if (n && (!kmers || !fractions)) return mfail(M_BAD_PARAM, "null k-mers / fractions");
+  // Guava BloomFilter.create(funnel, expected (0 -> 1), 1e-5): optimalNumOfBits,
+  // optimalNumOfHashFunctions, BitArray of ceil(bits / 64) longs.  removeUnique 2 builds it
+  // and never reads it (keepKmer @0-21), so only 1 does here.
+  const bool bloom = w->supress_noise == 1;
+  std::vector<uint64_t> bw;
+  uint64_t bloom_bits = 0;
+  int32_t bloom_k = 0;
+  if (bloom) {
+    const int64_t ne = expected ? (int64_t)expected : 1;
+    const int64_t bits = (int64_t)((double)(-ne) * log(1e-5) / (log(2.0) * log(2.0)));
+    const double hk = (double)bits / (double)ne * log(2.0);
+    const double fk = floor(hk);
+    bloom_k = std::max<int32_t>(1, (int32_t)((int64_t)fk + (hk - fk >= 0.5 ? 1 : 0)));
+    bw.assign((size_t)((bits + 63) / 64), 0ull);
+    if (bw.empty()) return mfail(M_BAD_PARAM, "Bloom filter of 0 bits");
+    bloom_bits = 64ull * bw.size();
+  }
   const uint32_t k = c->P.k;
   const bool do_rc = !c->P.no_rc;
   const double offset = (w->repeat_weight >= 0.0 && w->repeat_weight < 1.0) ? w->repeat_weight : 0.0;
@@ -1640,7 +1705,7 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   std::vector<uint8_t> km(k), rk(k);
   for (uint64_t i = 0; i < n; i++) {
     const double f = fractions[i];
-    if (!(f >= cutoff)) continue;
+    if (!(f >= cutoff) && !bloom) continue;
     for (uint32_t t = 0; t < k; t++) km[t] = (uint8_t)kmers[i * k + t];
     const uint8_t *use = km.data();
     if (do_rc) {                                  // Utils.rc: reverse, upper case, complement
@@ -1655,6 +1720,16 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
       if (memcmp(rk.data(), km.data(), k) < 0) use = rk.data();   // String.compareTo
     }
     const uint64_t key = murmur128_h1([&](int32_t q) { return (uint64_t)use[q]; }, (int32_t)k);
+    if (bloom) {                              // lambda$1 @162-185: every line, any fraction
+      uint64_t h1, h2;
+      murmur128_u64(key, h1, h2);
+      uint64_t x = h1;
+      for (int32_t j = 0; j < bloom_k; j++, x += h2) {
+        const uint64_t b = (x & 0x7FFFFFFFFFFFFFFFull) % bloom_bits;
+        bw[b >> 6] |= 1ull << (b & 63);
+      }
+    }
+    if (!(f >= cutoff)) continue;
     max_value = std::max(max_value, f);
     kv.emplace_back(key, f);
   }
@@ -1676,6 +1751,13 @@ int mhap_set_kmer_frequencies(mhap_ctx *c, const char *kmers, const double *frac
   if (c->ftab.alloc(slots)) return mfail(M_OOM, "k-mer frequency table");
   MHC(hipMemcpy(c->ftab.p, tab.data(), sizeof(FreqSlot) * slots, hipMemcpyHostToDevice));
   c->fmask = slots - 1;
+  if (bloom) {
+    if (c->bloom.alloc(bw.size())) return mfail(M_OOM, "k-mer Bloom filter");
+    MHC(hipMemcpy(c->bloom.p, bw.data(), 8ull * bw.size(), hipMemcpyHostToDevice));
+    c->bloom_bits = bloom_bits;
+    c->bloom_k = bloom_k;
+  }
+  c->has_bloom = bloom;
   c->W = *w;
   c->has_table = true;
   return M_OK;
@@ -1746,7 +1828,8 @@ static int sketch_minhash(mhap_ctx *c, const std::vector<uint32_t> &sids) {
     SketchArgs SA{c->mkeys2.p, c->mpos2.p, c->mkoff.p, c->msids.p, H,
                   mode, c->has_table ? c->ftab.p : nullptr, c->fmask, c->W.repeat_idf_scale,
                   c->W.no_tf, c->minhash.p, c->ocount.p, c->kctr.p,
-                  bs_w, bs_sample, c->mkeys.p, c->mpos.p, c->mbscnt.p, c->mbest.p};
+                  bs_w, bs_sample, c->mkeys.p, c->mpos.p, c->mbscnt.p, c->mbest.p,
+                  BloomDev{c->has_bloom ? c->bloom.p : nullptr, c->bloom_bits, c->bloom_k}};
     const size_t lds = sizeof(BestRec) * 4 * c->P.num_hashes;
     MHC(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(k_mh_minhash, dim3(nb), dim3(256), lds, s, SA);

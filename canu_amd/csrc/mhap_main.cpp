@@ -19,8 +19,8 @@
 //
 // The sketch, the weighting (--repeat-weight, --repeat-idf-scale, --filter-threshold,
 // --no-tf, -f with its fractions) and both filter stages are the jar's, read from its
-// bytecode (include/canu_mhap.h, oracle/mhap_jar.py).  --supress-noise 1/2 (the jar's Guava
-// Bloom filter; canu: only with mhapFilterUnique) is refused.
+// bytecode (include/canu_mhap.h, oracle/mhap_jar.py), --supress-noise's Guava Bloom filter
+// of the -f keys among them (sized by the file's count line).
 #include <zlib.h>
 
 #include <algorithm>
@@ -58,7 +58,7 @@ int usage(const char *prog) {
           "  --ordered-sketch-size n  --ordered-kmer-size n  --min-olap-length n\n"
           "  --num-threads n (ignored: one GPU)   CANU_MHAP_DEVICE picks the GPU\n"
           "  --repeat-weight x  --repeat-idf-scale x  --filter-threshold x  --no-tf\n"
-          "  --max-shift x  --min-store-length n  --no-rc  --supress-noise 0\n",
+          "  --max-shift x  --min-store-length n  --no-rc  --supress-noise 0|1|2\n",
           prog, prog);
   return 1;
 }
@@ -95,9 +95,11 @@ bool read_fasta(const char *path, std::vector<uint8_t> &bases, std::vector<uint6
 // canu's frequentMers.ignore.gz (Meryl.pm:699-712): a count line, then "kmer<TAB>fraction"
 // for both orientations.  gzopen reads plain files too.
 // The -f file (Meryl.pm:699-716): a count line, then "kmer<TAB>fraction" lines.
-bool read_filter(const char *path, uint32_t k, std::string &kmers, std::vector<double> &fr) {
+bool read_filter(const char *path, uint32_t k, std::string &kmers, std::vector<double> &fr,
+                 uint64_t &count) {
   gzFile G = gzopen(path, "rb");
   if (!G) return false;
+  bool have_count = false;
   char buf[4096];
   bool first = true;
   while (gzgets(G, buf, sizeof buf)) {
@@ -107,6 +109,10 @@ bool read_filter(const char *path, uint32_t k, std::string &kmers, std::vector<d
     const bool count_line = first && L > 0 && strspn(buf, "0123456789") == L &&
                             buf[L] != '\t' && buf[L] != ' ';
     first = false;
+    if (count_line) {                     // sizes --supress-noise's Bloom filter
+      count = strtoull(buf, nullptr, 10);
+      have_count = true;
+    }
     if (L == 0 || count_line) continue;
     if (L != k) continue;
     kmers.append(buf, L);
@@ -115,6 +121,7 @@ bool read_filter(const char *path, uint32_t k, std::string &kmers, std::vector<d
     fr.push_back((*f && *f != '\n' && *f != '\r') ? strtod(f, nullptr) : 1.0);
   }
   gzclose(G);
+  if (!have_count) count = fr.size();
   return true;
 }
 
@@ -234,9 +241,8 @@ int main(int argc, char **argv) {
       return usage(argv[0]);
     }
   }
-  if (W.supress_noise != 0) {
-    fprintf(stderr, "mhap: --supress-noise %d: the jar's Bloom-filter noise suppression is not "
-                    "implemented\n", W.supress_noise);
+  if (W.supress_noise < 0 || W.supress_noise > 2) {
+    fprintf(stderr, "mhap: Unknown removeUnique option %d.\n", W.supress_noise);
     return 1;
   }
   if ((fasta != nullptr) == (spath != nullptr)) {
@@ -275,10 +281,12 @@ int main(int argc, char **argv) {
       } else {
         std::string kmers;
         std::vector<double> fr;
-        if (fpath && !read_filter(fpath, P.k, kmers, fr)) {
+        uint64_t count = 0;
+        if (fpath && !read_filter(fpath, P.k, kmers, fr, count)) {
           fprintf(stderr, "mhap: cannot read filter '%s'\n", fpath);
           rc = 1;
-        } else if (fpath ? mhap_set_kmer_frequencies(ctx, kmers.data(), fr.data(), fr.size(), &W)
+        } else if (fpath ? mhap_set_kmer_frequencies_ex(ctx, kmers.data(), fr.data(), fr.size(),
+                                                        count, &W)
                          : mhap_set_weighting(ctx, &W)) {
           rc = fail_lib("weighting");
         }

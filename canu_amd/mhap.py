@@ -25,10 +25,11 @@ EXPORTS = ["mhap_params_init", "mhap_ctx_create", "mhap_ctx_destroy", "mhap_last
            "mhap_set_weighting", "mhap_sketch", "mhap_sketch_buffers", "mhap_copy_sketches",
            "mhap_build_index", "mhap_build_index_range", "mhap_compare_all",
            "mhap_copy_sketches_host", "mhap_weighting_init", "mhap_set_kmer_frequencies",
+           "mhap_set_kmer_frequencies_ex",
            "mhap_compare", "mhap_fetch", "mhap_write_text", "mhap_format_line",
            "mhap_get_stats"]
 
-ABI_VERSION = 6          # MHAP_ABI_VERSION of include/canu_mhap.h
+ABI_VERSION = 7          # MHAP_ABI_VERSION of include/canu_mhap.h
 
 
 class MhapError(RuntimeError):
@@ -97,6 +98,7 @@ def load_library(path: str | None = None):
     lib.mhap_get_stats.argtypes = [V, P(_Stats)]
     lib.mhap_weighting_init.argtypes = [P(_Weighting)]
     lib.mhap_set_kmer_frequencies.argtypes = [V, ctypes.c_char_p, V, U64, P(_Weighting)]
+    lib.mhap_set_kmer_frequencies_ex.argtypes = [V, ctypes.c_char_p, V, U64, U64, P(_Weighting)]
     _lib = lib
     return lib
 
@@ -122,8 +124,9 @@ class MhapParameters:
     repeat_idf_scale: float = 3.0
     filter_threshold: float = 1e-5
     no_tf: bool = False
-    # --supress-noise 1 / 2 (canu: with mhapFilterUnique, OverlapMhap.pm:483) build a Guava
-    # Bloom filter in the jar; not implemented: the library refuses them
+    # --supress-noise (canu: 2 with mhapFilterUnique, OverlapMhap.pm:483): with a -f table, 1
+    # keeps only k-mers the jar's Guava Bloom filter of the file's keys accepts (keepKmer),
+    # 2 builds that filter and never reads it
     supress_noise: int = 0
 
     @classmethod
@@ -228,23 +231,29 @@ def parse_mhap_args(argv: list[str]) -> tuple[MhapParameters, dict]:
     return p, io
 
 
-def read_frequency_file(path: str, k: int) -> tuple[list[str], np.ndarray]:
+def read_frequency_file(path: str, k: int, with_count: bool = False):
     """The -f file canu writes (Meryl.pm:699-716): optionally gzipped, a first line with
-    the number of k-mer lines, then "kmer<TAB>fraction" lines (both strands)."""
+    the number of k-mer lines, then "kmer<TAB>fraction" lines (both strands).  Returns
+    (k-mers, fractions), with_count: and the count line's value (the number of k-mer lines
+    when the file has none), which sizes the jar's --supress-noise Bloom filter."""
     import gzip
     op = gzip.open if path.endswith(".gz") else open
     kmers, fr = [], []
+    count = None
     with op(path, "rt") as f:
         for j, line in enumerate(f):
             parts = line.split()
             if not parts:
                 continue
             if j == 0 and len(parts) == 1 and parts[0].isdigit():
+                count = int(parts[0])
                 continue                                   # the count line
             if len(parts[0]) != k:
                 raise MhapError(-4, f"{path}:{j + 1}: k-mer of length {len(parts[0])}, not {k}")
             kmers.append(parts[0])
             fr.append(float(parts[1]) if len(parts) > 1 else 1.0)
+    if with_count:
+        return kmers, np.asarray(fr, dtype=np.float64), len(kmers) if count is None else count
     return kmers, np.asarray(fr, dtype=np.float64)
 
 
@@ -296,14 +305,17 @@ class Mhap:
         w = self.params.weighting_c()
         self._check(self.lib.mhap_set_weighting(self.ctx, ctypes.byref(w)))
 
-    def set_kmer_frequencies(self, kmers: list[str], fractions) -> None:
-        """-f with fractions (file order), under this job's weighting options."""
+    def set_kmer_frequencies(self, kmers: list[str], fractions, expected: int | None = None
+                             ) -> None:
+        """-f with fractions (file order), under this job's weighting options; expected = the
+        file's count line (sizes --supress-noise's Bloom filter; None: the number of lines)."""
         blob = "".join(kmers).encode()
         fr = np.ascontiguousarray(fractions, dtype=np.float64)
         w = self.params.weighting_c()
-        self._check(self.lib.mhap_set_kmer_frequencies(self.ctx, blob,
-                                                       fr.ctypes.data if fr.size else None,
-                                                       len(kmers), ctypes.byref(w)))
+        n = len(kmers)
+        self._check(self.lib.mhap_set_kmer_frequencies_ex(
+            self.ctx, blob, fr.ctypes.data if fr.size else None, n,
+            n if expected is None else int(expected), ctypes.byref(w)))
 
     def sketch(self, bgn: int | None = None, end: int | None = None) -> None:
         bgn = self.first_iid if bgn is None else bgn
@@ -367,8 +379,9 @@ class Mhap:
         file."""
         self.load_reads(rs)
         if frequencies is not None:
-            km, fr = frequencies
-            self.set_kmer_frequencies(list(km), fr)
+            km, fr = frequencies[0], frequencies[1]
+            self.set_kmer_frequencies(list(km), fr,
+                                      frequencies[2] if len(frequencies) > 2 else None)
         else:
             self.set_weighting()
         self.sketch()

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MHAP_ABI_VERSION 6
+#define MHAP_ABI_VERSION 7
 
 typedef struct {
   uint32_t k;               /* -k                      MinHash k-mer size, 1..32        */
@@ -126,8 +126,10 @@ typedef struct {
   double  repeat_idf_scale;   /* --repeat-idf-scale                                      */
   double  filter_threshold;   /* --filter-threshold                                      */
   int32_t no_tf;              /* --no-tf                                                 */
-  int32_t supress_noise;      /* --supress-noise: only 0 (the jar's Bloom-filter modes 1
-                                 and 2 are not restated: mhap_set_* refuse them)          */
+  int32_t supress_noise;      /* --supress-noise 0 / 1 / 2 (FrequencyCounts.removeUnique):
+                                 with a -f table, 1 drops every k-mer a Guava 19 Bloom
+                                 filter of the file's keys rejects (keepKmer); 2 builds
+                                 the filter and never reads it (= 0); without -f no effect */
 } mhap_weighting;
 
 void        mhap_weighting_init(mhap_weighting *w);
@@ -145,6 +147,13 @@ int         mhap_set_weighting(mhap_ctx *ctx, const mhap_weighting *w);
  *   repeat_weight >= 1:      c */
 int         mhap_set_kmer_frequencies(mhap_ctx *ctx, const char *kmers, const double *fractions,
                                       uint64_t n, const mhap_weighting *w);
+/* (ABI 7) the same with the file's first line, the k-mer count the jar sizes its Bloom
+ * filter by (FrequencyCounts.<init> @149-207: BloomFilter.create(funnel, count, 1e-5), a
+ * count of 0 read as 1); mhap_set_kmer_frequencies passes n.  Every line's key enters the
+ * filter whatever its fraction. */
+int         mhap_set_kmer_frequencies_ex(mhap_ctx *ctx, const char *kmers,
+                                         const double *fractions, uint64_t n,
+                                         uint64_t expected, const mhap_weighting *w);
 
 /* Sketch reads bgn_iid..end_iid (inclusive): both strands' MinHash + ordered sketches. */
 int         mhap_sketch(mhap_ctx *ctx, uint32_t bgn_iid, uint32_t end_iid);

@@ -68,9 +68,9 @@ def _fmix64(k):
     return k
 
 
-def murmur3_128_h1(data: bytes, seed: int = 0) -> int:
-    """MurmurHash3_x64_128's first 64 bits (Guava HashCode.asLong: the first 8 bytes of the
-    hash, little-endian = h1), as a signed Java long."""
+def murmur3_128(data: bytes, seed: int = 0) -> tuple[int, int]:
+    """MurmurHash3_x64_128: (h1, h2) as unsigned 64-bit values (Guava's HashCode bytes are h1
+    then h2, each little-endian)."""
     c1, c2 = 0x87C37B91114253D5, 0x4CF5AD432745937F
     h1 = h2 = seed & M64
     n = len(data)
@@ -114,6 +114,14 @@ def murmur3_128_h1(data: bytes, seed: int = 0) -> int:
     h1 = _fmix64(h1)
     h2 = _fmix64(h2)
     h1 = (h1 + h2) & M64
+    h2 = (h2 + h1) & M64
+    return h1, h2
+
+
+def murmur3_128_h1(data: bytes, seed: int = 0) -> int:
+    """MurmurHash3_x64_128's first 64 bits (Guava HashCode.asLong: the first 8 bytes of the
+    hash, little-endian = h1), as a signed Java long."""
+    h1 = murmur3_128(data, seed)[0]
     return h1 - (1 << 64) if h1 >> 63 else h1
 
 
@@ -279,6 +287,41 @@ def murmur32_windows(s: bytes, k: int) -> np.ndarray:
     return h.view(np.int32)
 
 
+# ---- Guava 19.0 BloomFilter (bundled in the jar: META-INF/maven/com.google.guava) ----------
+class GuavaBloom:
+    """com.google.common.hash.BloomFilter as the jar's bundled Guava 19.0 builds it, restated
+    from its bytecode: create(funnel, n, fpp) @0-136 -> MURMUR128_MITZ_64 with
+      numBits = (long) (-n * ln(fpp) / (ln 2 * ln 2))          optimalNumOfBits @0-33
+      k = max(1, (int) Math.round((double) numBits / n * ln 2))  optimalNumOfHashFunctions
+      BitArray: ceil(numBits / 64) longs, bitSize = 64 x that   BitArray.<init>, bitSize
+    put / mightContain (BloomFilterStrategies$2): the murmur3_128 of the funnel's bytes (the
+    Long funnel, FrequencyCounts.lambda$0: putLong = 8 little-endian bytes), hash1 = h1
+    (lowerEight), hash2 = h2 (upperEight); for i < k the bit (hash1 + i * hash2 (wrapping) &
+    Long.MAX_VALUE) % bitSize, word bit >>> 6, bit (int) bit & 63 (Java's << takes 6 bits)."""
+
+    def __init__(self, n: int, fpp: float):
+        if n == 0:
+            n = 1
+        bits = int(float(-n) * math.log(fpp) / (math.log(2.0) * math.log(2.0)))
+        self.k = max(1, java_round(bits / float(n) * math.log(2.0)))
+        self.words = np.zeros(-(-bits // 64), dtype=np.uint64)
+        self.bit_size = 64 * self.words.shape[0]
+
+    def _bits(self, key: int):
+        h1, h2 = murmur3_128((key & M64).to_bytes(8, "little"))
+        c = h1
+        for _ in range(self.k):
+            yield (c & LONG_MAX) % self.bit_size
+            c = (c + h2) & M64
+
+    def put(self, key: int) -> None:
+        for b in self._bits(key):
+            self.words[b >> 6] |= np.uint64(1 << (b & 63))
+
+    def might_contain(self, key: int) -> bool:
+        return all((int(self.words[b >> 6]) >> (b & 63)) & 1 for b in self._bits(key))
+
+
 # ---- FrequencyCounts (-f) ----------------------------------------------------------------
 class FrequencyCounts:
     """FrequencyCounts.<init>(reader, filterCutoff, offset, removeUnique, noTf, threads,
@@ -286,13 +329,20 @@ class FrequencyCounts:
     lines; a k-mer's key is computeSequenceHashesLong(kmer, len, 0, doRC)[0]; lines with
     frac >= filterCutoff enter fractionCounts (key -> frac) and raise maxValue.
     MhapMain passes offset = --repeat-weight when it lies in [0, 1) (else 0), range =
-    --repeat-idf-scale, doRC = !--no-rc.  removeUnique (--supress-noise) > 0 builds a Guava
-    Bloom filter of the keys; it is not restated (canu passes it only with
-    mhapFilterUnique) and is refused."""
+    --repeat-idf-scale, doRC = !--no-rc.  removeUnique (--supress-noise) > 0 (@189-207): a
+    Guava BloomFilter.create(Long funnel, expected = line 1's count (0 -> 1, @171-187),
+    1e-5) into which lambda$1 @162-185 puts EVERY line's key, whatever its fraction;
+    keepKmer @0-21 asks it only when removeUnique == 1 (2 builds it and never reads it).
+    expected: line 1's count (None: the number of lines)."""
 
-    def __init__(self, kmers, fractions, p: dict):
-        if int(p.get("supress_noise", 0)):
-            raise NotImplementedError("--supress-noise (Guava BloomFilter) is not restated")
+    def __init__(self, kmers, fractions, p: dict, expected=None):
+        self.remove_unique = int(p.get("supress_noise", 0))
+        if self.remove_unique not in (0, 1, 2):
+            raise ValueError("Unknown removeUnique option")
+        self.valid = None
+        if self.remove_unique > 0:
+            n = len(kmers) if expected is None else int(expected)
+            self.valid = GuavaBloom(n if n > 0 else 1, 1e-5)
         rw = float(p["repeat_weight"])
         self.offset = rw if 0.0 <= rw < 1.0 else 0.0
         self.range = float(p["repeat_idf_scale"])
@@ -304,6 +354,8 @@ class FrequencyCounts:
         for km, f in zip(kmers, fractions):
             km = km.encode() if isinstance(km, str) else bytes(km)
             key = seq_hashes_long(km, len(km), do_rc)[0]
+            if self.valid is not None:
+                self.valid.put(key)
             f = float(f)
             if f >= self.filter_cutoff:
                 self.max_value = max(self.max_value, f)
@@ -313,7 +365,13 @@ class FrequencyCounts:
         self.max_idf = self.idf(self.min_value)
 
     def idf(self, x: float) -> float:               # idf(D) @0-14
-        return math.log(self.max_value / x - self.offset)
+        v = self.max_value / x - self.offset         # Math.log: NaN below 0 (no -f line
+        if v != v or v < 0.0:                         # over the cutoff: maxValue -inf)
+            return math.nan
+        return math.log(v) if v > 0.0 else -math.inf
+
+    def keep_kmer(self, key: int) -> bool:           # keepKmer @0-21
+        return self.valid.might_contain(key) if self.remove_unique == 1 else True
 
     def is_popular(self, key: int) -> bool:          # isPopular @0-13
         return key in self.counts
@@ -360,6 +418,9 @@ def minhash(s: bytes, p: dict, fc: FrequencyCounts | None):
     if len(s) - k + 1 < 1:
         return None
     keys = murmur128_h1_windows(s, k)                # = seq_hashes_long(s, k, False)
+    if fc is not None and fc.remove_unique == 1:      # keepKmer @70-83: never counted
+        keep = np.array([fc.keep_kmer(int(x)) for x in np.unique(keys)], dtype=bool)
+        keys = keys[keep[np.searchsorted(np.unique(keys), keys)]] if keys.size else keys
     uk, first, cnt = np.unique(keys, return_index=True, return_counts=True)
     order = np.argsort(first, kind="stable")          # LinkedOpenHashMap: insertion order
     counts = dict(zip(uk[order].tolist(), cnt[order].tolist()))
@@ -670,6 +731,13 @@ MHAP_DTYPE = np.dtype([("a", "<u4"), ("b", "<u4"), ("erate", "<f8"), ("raw", "<f
                        ("count", "<u4")])
 
 
+def frequency_counts(freq, p: dict):
+    """freq: None, (k-mers, fractions) or (k-mers, fractions, line 1's count)."""
+    if freq is None:
+        return None
+    return FrequencyCounts(freq[0], freq[1], p, freq[2] if len(freq) > 2 else None)
+
+
 def sketch_read(s: bytes, p: dict, fc):
     """SequenceSketch.<init> for one strand: (minhash, ordered) or None (skipped read)."""
     mh = minhash(s, p, fc)
@@ -710,7 +778,7 @@ def sketch_rows(rs, p: dict, freq=None, reads=None):
     """The sketches in the library's layout (canu_mhap.h mhap_sketch_buffers): minhash
     int32 [n][2][H], ordered uint64 [n][2][S] ((hash ^ 0x80000000) << 32 | position),
     ocount uint32 [n][2] (0: strand not stored); rows of reads not sketched stay zero."""
-    fc = FrequencyCounts(freq[0], freq[1], p) if freq is not None else None
+    fc = frequency_counts(freq, p)
     n, H, S = rs.nreads, p["num_hashes"], p["ordered_sketch"]
     mh = np.zeros((n, 2, H), dtype=np.int32)
     od = np.zeros((n, 2, S), dtype=np.uint64)
@@ -770,7 +838,7 @@ def run(rs, p: dict, freq=None, q_range=None, t_range=None, to_self: bool = True
     query reads q_range (default: the stored reads, the -s self search).  to_self: the self
     search (MinHashSearch.findMatches toSelf: only stored reads of smaller ID); False: the -q
     search.  Rows sorted by (a, b, o)."""
-    fc = FrequencyCounts(freq[0], freq[1], p) if freq is not None else None
+    fc = frequency_counts(freq, p)
     t_lo, t_hi = t_range if t_range is not None else (0, rs.nreads)
     q_lo, q_hi = q_range if q_range is not None else (t_lo, t_hi)
     store = sketches(rs, p, fc, range(t_lo, t_hi))

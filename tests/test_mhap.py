@@ -56,7 +56,7 @@ def test_header_declares_the_python_exports():
 def test_library_exports_every_declared_symbol(built):
     lib = mhap.load_library()
     assert [f for f in mhap.EXPORTS if not hasattr(lib, f)] == []
-    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 6
+    assert lib.mhap_abi_version() == mhap.ABI_VERSION == 7
 
 
 def test_record_layout_matches_the_header(built):
@@ -145,6 +145,37 @@ def test_murmur3_published_vectors():
     assert M.murmur3_128_h1(b"The quick brown fox jumps over the lazy dog") & M.M64 == \
         0xE34BBC7BBC071B6C
     assert M._chars(b"AC") == b"A\x00C\x00"
+    # the whole 128 bits (h1, h2), which Guava's BloomFilter strategy reads
+    assert M.murmur3_128(b"hello") == (0xCBD8A7B341BD9B02, 0x5B1E906A48AE1D19)
+    assert M.murmur3_128(b"The quick brown fox jumps over the lazy dog") == \
+        (0xE34BBC7BBC071B6C, 0x7A433CA9C49A9347)
+
+
+def test_guava_bloom_filter_restatement():
+    """--supress-noise's filter (Guava 19.0 BloomFilter, MURMUR128_MITZ_64, as bundled in the
+    jar): sizing by optimalNumOfBits / optimalNumOfHashFunctions, whole 64-bit words; every
+    key put is found; ~1e-5 false positives; FrequencyCounts puts every line's key (any
+    fraction) and keepKmer asks the filter only for removeUnique 1."""
+    b = M.GuavaBloom(1000, 1e-5)
+    assert b.bit_size == 24000 and b.words.shape[0] == 375 and b.k == 17   # 23,962 bits
+    b0 = M.GuavaBloom(0, 1e-5)                       # a count line of 0 reads as 1
+    assert b0.bit_size == 64 and b0.k == 16            # 23 bits, round(15.9)
+    rng = np.random.default_rng(3)
+    keys = [int(x) for x in rng.integers(-2**63, 2**63 - 1, 1000, dtype=np.int64)]
+    for x in keys:
+        b.put(x)
+    assert all(b.might_contain(x) for x in keys)
+    other = [int(x) for x in rng.integers(-2**63, 2**63 - 1, 20000, dtype=np.int64)]
+    assert sum(b.might_contain(x) for x in other) <= 3
+    p = M.default_params(filter_threshold=1e-5)
+    km = ["AAAAAAAAAAAAAAAC", "ACGTACGTACGTACGA", "CCCCCCCCCCCCCCCA"]
+    fr = [1e-3, 1e-7, 1e-6]                           # two lines below the cutoff
+    keys = [M.seq_hashes_long(x.encode(), 16, True)[0] for x in km]
+    for mode in (1, 2):
+        fc = M.FrequencyCounts(km, fr, dict(p, supress_noise=mode), expected=3)
+        assert len(fc.counts) == 1 and all(fc.valid.might_contain(x) for x in keys)
+        assert fc.keep_kmer(keys[2]) and (fc.keep_kmer(12345) == (mode == 2))
+    assert M.FrequencyCounts(km, fr, p).keep_kmer(12345)
 
 
 def test_window_hashes_equal_the_scalar_restatement():
@@ -524,12 +555,64 @@ def test_gpu_shards_query_search_and_text(built, small, small_oracle, tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_supress_noise_is_refused(built):
-    P = mhap.MhapParameters(supress_noise=2)
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gpu_supress_noise_rows_match_oracle(built, mode):
+    """--supress-noise with canu's -f table: 1 keeps only the k-mers the jar's Guava Bloom
+    filter of the file's keys accepts -- here read 0's k-mers of the table, so every other
+    read loses nearly all of its k-mers (those strands skipped, ocount 0) -- and 2 builds
+    the filter and never reads it (the rows of --supress-noise 0).  The filter is sized by
+    the file's count line (a smaller count: more false positives kept)."""
+    rs = _reads(n=24, L=3000, cov=8, seed=19)
+    P = mhap.MhapParameters(num_hashes=48, ordered_sketch_size=600, ordered_kmer_size=14,
+                            min_olap_length=300, supress_noise=mode).canu_weighting()
+    km, fr = _freq_for(rs, every=3)
+    for expected in (len(km), 40):
+        m = mhap.Mhap(P, device=0)
+        m.load_reads(rs)
+        m.set_kmer_frequencies(km, fr, expected)
+        m.sketch()
+        got = _rows(m, rs.nreads, P)
+        m.close()
+        want = M.sketch_rows(rs, P.as_oracle(), (km, fr, expected))
+        _same_rows(got, want)
+        if mode == 2:
+            _same_rows(got, M.sketch_rows(rs, dict(P.as_oracle(), supress_noise=0), (km, fr)))
+        elif expected == len(km):
+            assert want[2][0].all() and (want[2][1:] == 0).sum() > 0
+    # without a -f table there is no FrequencyCounts and so no filter
     m = mhap.Mhap(P, device=0)
-    with pytest.raises(mhap.MhapError, match="supress-noise"):
-        m.set_weighting()
+    m.load_reads(rs)
+    m.set_weighting()
+    m.sketch()
+    got = _rows(m, rs.nreads, P)
     m.close()
+    _same_rows(got, M.sketch_rows(rs, P.as_oracle()))
+
+
+@pytest.mark.gpu
+def test_gpu_supress_noise_job_matches_oracle(built):
+    """--supress-noise 1 end to end (self job) against the restatement; the filter's keys
+    are the k-mers of reads 0-9 (every line below --filter-threshold: an empty tf-idf table,
+    the filter alone), so the sketches hold only those k-mers."""
+    rs = _reads(n=40, L=3000, cov=10, seed=23)
+    P = mhap.MhapParameters(num_hashes=96, ordered_sketch_size=1000, min_olap_length=400,
+                            supress_noise=1).canu_weighting()
+    comp = str.maketrans("ACGT", "TGCA")
+    km, fr = [], []
+    for r in range(10):
+        s = rs.read(r).decode()
+        for i in range(0, len(s) - 16, 2):
+            km += [s[i:i + 16], s[i:i + 16].translate(comp)[::-1]]
+            fr += [1e-7, 1e-7]                       # below the cutoff: filter only
+    freq = (km, np.array(fr), len(km))
+    m = mhap.Mhap(P, device=0)
+    got = m.run(rs, frequencies=freq)
+    m.close()
+    want = M.run(rs, P.as_oracle(), freq=freq)
+    assert len(want) > 5
+    # the sketches hold only the filter's k-mers: another set of records than without it
+    assert len(want) != len(M.run(rs, dict(P.as_oracle(), supress_noise=0), freq=freq))
+    _same(got, want)
 
 
 def test_library_formats_lines_like_java(built):

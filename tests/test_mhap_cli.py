@@ -42,8 +42,7 @@ def test_cli_usage_errors(cli):
     for args in ([], ["-p", "x.fasta"], ["-p", "x.fasta", "-s", "y.dat", "-q", "."],
                  ["--bogus"], ["-k"], ["--no-tf", "-s", "missing.dat"],
                  ["--supress-noise", "5", "-s", "y.dat"],
-                 # the jar's Bloom-filter noise suppression is not implemented: refused
-                 ["--supress-noise", "2", "-p", "x.fasta", "-q", "."]):
+                 ["--supress-noise", "-1", "-p", "x.fasta", "-q", "."]):
         cp = _run(cli, args)
         assert cp.returncode == 1, (args, cp.stderr)
 
