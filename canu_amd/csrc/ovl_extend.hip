@@ -594,7 +594,11 @@ __device__ __forceinline__ void ped_traceback_codes(int32_t *log, int32_t tb_e, 
     int32_t V[G * TBR];
 #pragma unroll
     for (int i = 0; i < G * TBR; i++) {
+#ifdef OVL_ATTR_TB_FIXED                       // traffic attribution only (wrong results)
+      const int32_t kk = 0;
+#else
       const int32_t kk = kh - 1 - i < 0 ? 0 : kh - 1 - i;   // row k-1 for k = kh - i
+#endif
       if constexpr (L16) V[i] = (int32_t)rows16[(size_t)kk * W + cell];
       else               V[i] = rows[(size_t)kk * W + cell];
     }
@@ -948,7 +952,11 @@ __device__ __attribute__((OVL_PED_ATTR)) PedOut wave_ped_reg(
       int32_t kmx = NEG;
       const uint32_t kspan = (uint32_t)(nr - nl);
       const int32_t jrs = ((nr + 2 > right ? nr + 2 : right) - B) >> 6;
+#ifdef OVL_ATTR_LOG_FIXED                      // traffic attribution only (wrong results)
+      const uint32_t erow = 0u;
+#else
       const uint32_t erow = (uint32_t)e * (uint32_t)(LW * sizeof(cell_t));
+#endif
 #pragma unroll
       for (int j = 0; j < J; j++) {
         if (j >= JU && j > jrs) break;

@@ -107,6 +107,9 @@ struct BuildArgs {
 };
 
 #define OVL_CB_MAX 4096
+#ifndef OVL_COARSE_SWEEPS
+#define OVL_COARSE_SWEEPS 4      // bucket windows the coarse scatter stores in turn (1: 29.1, 4: 28.8, 8: 32.5 ms index, r06z)
+#endif
 #define OVL_SKIP_POS 0xFFFFFFFFFFFFFFFFull
 
 template <typename F>
@@ -169,15 +172,26 @@ __global__ void k_coarse_scatter(BuildArgs A, uint32_t *cursor, Rec2 *outR) {
     h[i] = 0;
   }
   __syncthreads();
-  for_block_windows(A, [&](uint64_t kmer, uint64_t pos) {
-    uint64_t M = mix64(kmer);
-    uint32_t b = (uint32_t)(M >> (64 - A.cb_bits));
-    uint32_t slot = base[b] + atomicAdd(&h[b], 1u);
-    Rec2 r;
-    r.m = M;
-    r.p = pos;
-    outR[slot] = r;
-  });
+  // Sweeps: the block's windows are re-read once per window of nb / OVL_COARSE_SWEEPS
+  // buckets and only that window's records are stored, so a block has that many write streams
+  // open at a time instead of all nb (with every bucket open, the resident blocks' half-written
+  // lines overflow the L2 and leave it partially written: 2x the record bytes in PMC writes).
+  // The re-reads hit the block's packed reads in the L2; a bucket's order is the fine pass's.
+  constexpr uint32_t NS = OVL_COARSE_SWEEPS;
+  for (uint32_t sw = 0; sw < NS; sw++) {
+    const uint32_t lo = (nb * sw) / NS, span = (nb * (sw + 1)) / NS - lo;
+    for_block_windows(A, [&](uint64_t kmer, uint64_t pos) {
+      uint64_t M = mix64(kmer);
+      uint32_t b = (uint32_t)(M >> (64 - A.cb_bits));
+      if (NS > 1 && b - lo >= span) return;
+      uint32_t slot = base[b] + atomicAdd(&h[b], 1u);
+      Rec2 r;
+      r.m = M;
+      r.p = pos;
+      outR[slot] = r;
+    });
+    if (NS > 1) __syncthreads();
+  }
 }
 
 // Sort order: M ascending, then position descending (chain order).
